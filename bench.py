@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident AES-256-GCM seal+open throughput (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..4] [--mode device|host]
+
+One step = seal every packet of the batch, then open every packet of it (in place, on device),
+i.e. one pass of the hot path (inside.go seal + outside.go open) over one 64 Ki x 1300 B batch.
+N > 1: one process per GPU (launched by torch.distributed.run), each rank owns its own batch of
+the same shape (packets are independent: no collective on the data path — SURVEY.md §8e);
+timing is bracketed by a barrier + device sync on both sides and the max over ranks is taken.
+
+Printed (rank 0, one JSON line): value = (payload sealed + payload opened, all ranks) / time.
+roofline: the seal kernel's algorithmic bytes (2p+32 per packet) / its mean launch time, from HIP
+events recorded on the kernel's stream inside the timed region; traffic = PMC-measured HBM bytes
+per launch from profiles/ when a counter pass for this kernel is committed there, else null.
+cpu_baseline: rank 0, N = 1 only, the OpenSSL-EVP port of the per-packet loop (oracle/) on a
+bounded sample of the same batch, on this box's CPU share.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E peak
+GIB = float(1 << 30)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+def cpu_share() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def cpu_baseline(b, target_s: float = 6.0):
+    """OpenSSL-EVP port (oracle/evp_baseline.c) on a bounded sample: seal then open."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    threads = cpu_share()
+    n = min(b.n, 8192)
+    desc = b.desc[:n].copy()
+    arena = b.arena[: n * b.stride].copy()
+    keys = b.keys
+    # calibrate
+    t1, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=1)
+    iters = max(1, int(target_s / max(t1, 1e-4)))
+    sealed = arena.copy()
+    ts, st = oracle.evp_batch(b.alg, 0, keys, desc, sealed, threads=threads, iters=1)
+    assert (st == 0).all()
+    work = sealed.copy()
+    to, st = oracle.evp_batch(b.alg, 1, keys, desc, work, threads=threads, iters=1)
+    assert (st == 0).all()
+    # timed: seal `iters` passes, open `iters` passes (open in place needs fresh ciphertext each pass:
+    # re-seal is not counted, so open runs on a copy that stays ciphertext by using out-of-place dst)
+    t_seal, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=iters)
+    od = desc.copy()
+    scratch_off = np.uint64(len(sealed))
+    od["dst_off"] = od["src_off"] + scratch_off  # decrypt into a scratch copy, ciphertext stays intact
+    big = np.concatenate([sealed, np.zeros_like(sealed)])
+    t_open, st = oracle.evp_batch(b.alg, 1, keys, od, big, threads=threads, iters=iters)
+    assert (st == 0).all()
+    payload = float(desc["len"].astype(np.int64).sum())
+    gibs = 2 * payload * iters / (t_seal + t_open) / GIB
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"{n} x {int(desc['len'][0])} B packets of the same batch, seal x{iters} + open x{iters} "
+                  f"({t_seal + t_open:.1f} s), OpenSSL EVP {'AES-256-GCM' if b.alg == 1 else 'ChaCha20-Poly1305'} "
+                  f"(AES-NI/PCLMUL class, as Go's crypto/cipher), {threads} pinned threads on {model}",
+    }
+
+
+def pmc_traffic(kernel_tag: str):
+    """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/pmc_traffic.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        return d.get(kernel_tag, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
+    ap.add_argument("--mode", choices=["device", "host"], default="device")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    import torch
+
+    from nebula_amd import _lib as L
+    from nebula_amd import workload as W
+    from nebula_amd.batch import DeviceBatch, host_batch, install_keys, slot_desc
+    from nebula_amd.noiseutil import Engine
+
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")  # control only (barrier / max of timings); no data-path collective
+        pg = dist
+
+    def barrier():
+        if pg is not None:
+            pg.barrier()
+
+    cfg = args.config
+    t0 = time.time()
+    b = W.make_batch(*{
+        1: (L.ALG_AESGCM, 65536, 1),
+        2: (L.ALG_AESGCM, 65536, 4096),
+        3: (L.ALG_CHACHAPOLY, 65536, 4096),
+    }[cfg], seed=W.SEED ^ rank, name=f"C{cfg + 1}") if cfg in (1, 2, 3) else \
+        W.shard(W.config(4), rank, world)
+    workload_name = {1: "C2 AES-256-GCM, 1 tunnel key, 65536 x 1300 B packets, device-resident",
+                     2: "C3 AES-256-GCM, 4096 tunnel keys, 65536 x 1300 B packets, device-resident",
+                     3: "C4 ChaCha20-Poly1305, 4096 tunnel keys, 65536 x 1300 B packets, device-resident",
+                     4: "C5 AES-256-GCM, 4096 tunnel keys, IMIX 90/576/1300 (7:4:1), 1 Mi packets sharded"}[cfg]
+    log(f"[rank {rank}] batch {b.name}: {b.n} pkts, {b.payload_bytes / 1e6:.1f} MB payload "
+        f"({time.time() - t0:.1f}s to build)")
+
+    eng = Engine(local, max_keys=max(4096, b.nkeys))
+    ciphers = install_keys(eng, b)
+    payload = float(b.payload_bytes)
+    alg_bytes = float(b.algorithmic_bytes)
+
+    if args.mode == "host":
+        from nebula_amd.batch import PinnedBuffer
+
+        d = slot_desc(b, ciphers)
+        buf = PinnedBuffer(b.arena.nbytes)
+        buf.array[:] = b.arena
+        hint = int(d["key_id"][0]) if b.nkeys == 1 else L.KEYS_MIXED
+        for _ in range(args.warmup):
+            host_batch(eng, b.alg, False, d, buf.array, hint)
+            host_batch(eng, b.alg, True, d, buf.array, hint)
+        barrier()
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            st = host_batch(eng, b.alg, False, d, buf.array, hint)
+            st2 = host_batch(eng, b.alg, True, d, buf.array, hint)
+        te = time.perf_counter()
+        assert (st == 0).all() and (st2 == 0).all()
+        dt = te - ts
+        if pg is not None:
+            t = torch.tensor([dt], dtype=torch.float64)
+            pg.all_reduce(t, op=pg.ReduceOp.MAX)
+            dt = float(t[0])
+        if rank == 0:
+            print(json.dumps({
+                "metric": "GiB/s host-resident (pinned H2D + kernel + D2H) AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch",
+                "value": round(2 * payload * args.steps * world / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "higher_is_better": True, "scaling": "weak", "data": "synthetic",
+                "config": {"workload": workload_name.replace("device-resident", "host-resident pinned")},
+            }), flush=True)
+        return
+
+    db = DeviceBatch(eng, b, ciphers)
+    stream = torch.cuda.current_stream()
+    # correctness gate before timing: one seal+open round trip must restore the plaintext
+    db.seal()
+    db.open()
+    torch.cuda.synchronize()
+    assert (db.status_host() == 0).all(), "round trip failed before timing"
+
+    for _ in range(args.warmup):
+        db.seal()
+        db.open()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        db.seal()
+        ev[i][1].record(stream)
+        db.open()
+        ev[i][2].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    te = time.perf_counter()
+    dt = te - ts
+    seal_ms = float(np.mean([a.elapsed_time(m) for a, m, _ in ev]))
+    open_ms = float(np.mean([m.elapsed_time(z) for _, m, z in ev]))
+    st = db.status_host()
+    assert (st == 0).all(), "open failed inside the timed region"
+    if pg is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        dt = float(t[0])
+
+    if rank != 0:
+        return
+    total_payload = 2 * payload * args.steps * world
+    value = total_payload / dt / GIB
+    achieved = alg_bytes / (seal_ms * 1e-3) / 1e9  # GB/s, seal kernel
+    alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
+    kern_tag = f"{'gcm' if b.alg == 1 else 'chacha'}_seal_{'single' if b.nkeys == 1 else 'mixed'}"
+    out = {
+        "metric": "GiB/s device-resident AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch"
+        if cfg == 1 else f"GiB/s device-resident {alg_name} seal+open ({workload_name})",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": workload_name, "packets_per_gpu": b.n, "payload_bytes_per_pkt":
+                   int(b.desc["len"].max()), "keys": b.nkeys, "cipher": alg_name,
+                   "parallelism": f"{world} GPU(s), independent packet shards, no collective"},
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kern_tag),
+            "kernel": kern_tag, "kernel_ms": round(seal_ms, 4), "open_kernel_ms": round(open_ms, 4),
+            "algorithmic_bytes_per_launch": int(alg_bytes),
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(b)
+        except Exception as e:  # the baseline is reported, never the product path
+            log(f"cpu_baseline failed: {e!r}")
+            out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,171 @@
+/*
+ * nebula_aead.h — C ABI of the MI355X (gfx950) AEAD engine for Nebula's per-packet data plane.
+ *
+ * Plain C: pointers, sizes and integers only; no torch or HIP types cross this boundary
+ * (streams are passed as `void*` = hipStream_t). Every entry point returns an int status
+ * (NEB_OK = 0, negative = error); nothing throws across the ABI.
+ *
+ * Reference interfaces replaced (slackhq/nebula, /root/reference):
+ *   neb_cipher_create        noise.CipherFunc.Cipher(k [32]byte) — flynn/noise v1.1.0 [ext]; the
+ *                            reference's own CipherFunc pattern is noiseutil/fips140.go:31-40,
+ *                            selected at pki.go:263-269; wrapped by noiseutil.NewCipherState
+ *                            (noiseutil/cipher_state.go:42-54, plugin hook :43-45)
+ *   neb_cipher_name          noise.CipherFunc.CipherName() ("AESGCM" / "ChaChaPoly")
+ *   neb_encrypt_danger       CipherState.EncryptDanger  noiseutil/cipher_state.go:32,
+ *                            noiseutil/aesgcm.go:24-37, noiseutil/chachapoly.go:23-36
+ *   neb_decrypt_danger       CipherState.DecryptDanger  noiseutil/cipher_state.go:35,
+ *                            noiseutil/aesgcm.go:39-49, noiseutil/chachapoly.go:38-48
+ *   neb_overhead             CipherState.Overhead       noiseutil/aesgcm.go:51-56, chachapoly.go:50-55
+ *   neb_seal_batch           the per-segment EncryptDanger loop of inside.go:123-146 / :225-236,
+ *                            batched at the TX flush point interface.go:465-469,478-487
+ *   neb_open_batch           the per-packet ConnectionState.Decrypt → DecryptDanger of
+ *                            connection_state.go:99-119 / outside.go:133, batched at the RX flush
+ *                            point interface.go:395-400; GMAC-only VerifyRelay
+ *                            (connection_state.go:121-148) is an open with len = 0
+ *   neb_header_encode/parse  header.Encode header/header.go:102-110, (*H).Parse :143-156
+ *   NEB_REJECT_AFTER_MESSAGES noiseutil/cipher_state.go:11-15
+ */
+#ifndef NEBULA_AEAD_H
+#define NEBULA_AEAD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NEB_API __attribute__((visibility("default")))
+
+/* Cipher identifiers; the names are the Noise CipherName strings hashed into the handshake. */
+#define NEB_ALG_AESGCM 1     /* "AESGCM": AES-256-GCM, nonce 00000000 || BE64(n) (aesgcm.go:31-35) */
+#define NEB_ALG_CHACHAPOLY 2 /* "ChaChaPoly": ChaCha20-Poly1305, nonce 00000000 || LE64(n) (chachapoly.go:30-34) */
+
+/* Return codes. */
+#define NEB_OK 0
+#define NEB_ERR_INVALID (-1)      /* bad argument */
+#define NEB_ERR_AUTH (-2)         /* Open: "cipher: message authentication failed"; plaintext region zeroed */
+#define NEB_ERR_EXHAUSTED (-3)    /* ErrMessageCounterExhausted (cipher_state.go:18) */
+#define NEB_ERR_NO_CIPHER (-4)    /* nil receiver on Encrypt: "no cipher state available to encrypt" */
+#define NEB_ERR_SHORT_BUFFER (-5) /* out capacity too small for the appended output */
+#define NEB_ERR_HIP (-6)          /* HIP runtime failure */
+#define NEB_ERR_NO_DEVICE (-7)    /* no gfx950 device / kernels not loadable */
+#define NEB_ERR_NO_KEY_SLOT (-8)  /* key table full */
+
+#define NEB_OVERHEAD 16 /* AEAD tag size (Overhead()) */
+#define NEB_HEADER_LEN 16
+#define NEB_REJECT_HEADROOM (1ULL << 40)
+#define NEB_REJECT_AFTER_MESSAGES (UINT64_MAX - NEB_REJECT_HEADROOM)
+
+/* Per-packet status written by the batch calls. */
+#define NEB_STATUS_OK 0
+#define NEB_STATUS_AUTH_FAILED 1 /* open: tag mismatch, payload destination zeroed */
+#define NEB_STATUS_EXHAUSTED 2   /* seal: counter >= NEB_REJECT_AFTER_MESSAGES, nothing written */
+#define NEB_STATUS_BAD_KEY 3     /* key_id not installed / wrong algorithm / violates the uniform-key hint */
+
+typedef struct neb_engine neb_engine; /* one per GPU: stream, key table, staging */
+typedef struct neb_cipher neb_cipher; /* one installed tunnel key (a CipherState) */
+
+/* One packet of a batch. Offsets index the batch arena (device memory for neb_*_batch, pinned host
+ * memory for neb_*_batch_host).
+ *   seal: reads aad[aad_len] at aad_off and pt[len] at src_off; writes ct[len] || tag[16] at dst_off.
+ *   open: reads aad at aad_off and ct[len] || tag[16] at src_off; writes pt[len] at dst_off.
+ * dst_off == src_off is the in-place form used by Nebula (connection_state.go:107). Any other
+ * overlap between one packet's regions, or between packets, is undefined. `counter` is the nonce n
+ * (= the header's message counter). */
+typedef struct neb_desc {
+    uint64_t src_off;
+    uint64_t dst_off;
+    uint64_t aad_off;
+    uint64_t counter;
+    uint32_t len;
+    uint32_t aad_len;
+    uint32_t key_id;
+    uint32_t flags; /* reserved, 0 */
+} neb_desc;
+
+/* ---- engine ------------------------------------------------------------------------------- */
+
+/* Create an engine on HIP device `device` with room for `max_keys` installed keys. */
+NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out);
+NEB_API int neb_engine_destroy(neb_engine* e);
+/* Device pointer to the engine's key table and the bytes per key record (for diagnostics). */
+NEB_API int neb_engine_info(const neb_engine* e, int* device, uint32_t* max_keys, uint32_t* key_record_bytes);
+/* Human-readable text of a return code. */
+NEB_API const char* neb_strerror(int rc);
+
+/* ---- key install: noise.CipherFunc.Cipher(k) ----------------------------------------------- */
+
+/* Install a 32-byte key: AES-256 key schedule + H = E_K(0^128) + H^1..H^16 (AESGCM), or the raw
+ * ChaCha20 key (ChaChaPoly), computed on the device into the engine's key table. */
+NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out);
+NEB_API int neb_cipher_destroy(neb_cipher* c);
+NEB_API uint32_t neb_cipher_key_id(const neb_cipher* c);
+NEB_API int neb_cipher_alg(const neb_cipher* c);
+NEB_API const char* neb_cipher_name(int alg); /* "AESGCM", "ChaChaPoly", NULL if unknown */
+
+/* ---- per-packet CipherState surface (host buffers; exact Go slice semantics) ---------------- */
+
+/* Overhead(): 16, or 0 when c == NULL. */
+NEB_API int neb_overhead(const neb_cipher* c);
+
+/* EncryptDanger(out, ad, plaintext, n, nb): keeps out[0:out_len], appends ct || tag, sets
+ * *ret_len = out_len + pt_len + 16. `ad` may alias out[0:out_len] (inside.go:131). `nb` (12 bytes,
+ * may be NULL) receives the nonce exactly as the Go code assembles it.
+ * Errors: NEB_ERR_NO_CIPHER (c == NULL), NEB_ERR_EXHAUSTED (n >= NEB_REJECT_AFTER_MESSAGES; out
+ * untouched), NEB_ERR_SHORT_BUFFER (out_cap < out_len + pt_len + 16). */
+NEB_API int neb_encrypt_danger(neb_cipher* c, uint8_t* out, size_t out_len, size_t out_cap, const uint8_t* ad,
+                               size_t ad_len, const uint8_t* pt, size_t pt_len, uint64_t n, uint8_t* nb,
+                               size_t* ret_len);
+
+/* DecryptDanger(out, ad, ciphertext, n, nb): ciphertext = ct || tag. Keeps out[0:out_len], writes
+ * the plaintext after it, *ret_len = out_len + ct_len - 16. In place when out + out_len == ct
+ * (connection_state.go:107). On tag mismatch returns NEB_ERR_AUTH, zeroes the would-be plaintext
+ * region and touches nothing else (cipher_state_test.go:194-237). c == NULL: returns NEB_OK with
+ * *ret_len = 0 (Go returns []byte{}, nil). ct_len < 16 is an auth failure. */
+NEB_API int neb_decrypt_danger(neb_cipher* c, uint8_t* out, size_t out_len, size_t out_cap, const uint8_t* ad,
+                               size_t ad_len, const uint8_t* ct, size_t ct_len, uint64_t n, uint8_t* nb,
+                               size_t* ret_len);
+
+/* ---- batched data plane: device-resident arena ----------------------------------------------- */
+
+/* Key hint for the batch calls: NEB_KEYS_MIXED, or a key_id every descriptor uses (one tunnel's
+ * batch) — the engine then keeps that key's round keys in scalar registers and its GHASH tables
+ * shared per workgroup. Descriptors whose key_id differs from the hint get NEB_STATUS_BAD_KEY. */
+#define NEB_KEYS_MIXED 0xFFFFFFFFu
+
+/* Seal/open n packets. d_desc, d_arena, d_status are device pointers; `stream` is a hipStream_t
+ * (NULL = the engine's stream). Asynchronous: returns after enqueueing. Every descriptor's key must
+ * have algorithm `alg`. */
+NEB_API int neb_seal_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                           int32_t* d_status, uint32_t key_hint, void* stream);
+NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                           int32_t* d_status, uint32_t key_hint, void* stream);
+
+/* ---- batched data plane: host-resident arena (the TUN / UDP side) ---------------------------- */
+
+/* Same as above but desc/arena/status live in host memory (ideally from neb_host_alloc). The arena
+ * range [arena_lo, arena_hi) touched by the descriptors is streamed through the device in chunks
+ * with pinned H2D -> kernel -> D2H copies overlapped on two streams. Synchronous. */
+NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
+                                size_t arena_len, int32_t* status, uint32_t key_hint);
+NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
+                                size_t arena_len, int32_t* status, uint32_t key_hint);
+
+/* Pinned host memory (hipHostMalloc) for arenas that back the reference's batch.Arena
+ * (overlay/batch/coalesce_core.go:142-169) so the batch path needs no bounce copy. */
+NEB_API int neb_host_alloc(size_t bytes, void** out);
+NEB_API int neb_host_free(void* p);
+
+/* ---- header (the AAD) --------------------------------------------------------------------- */
+
+NEB_API void neb_header_encode(uint8_t b[16], uint8_t version, uint8_t type, uint8_t subtype, uint32_t remote_index,
+                               uint64_t counter);
+/* Returns NEB_ERR_INVALID when len < 16 (ErrHeaderTooShort). */
+NEB_API int neb_header_parse(const uint8_t* b, size_t len, uint8_t* version, uint8_t* type, uint8_t* subtype,
+                             uint16_t* reserved, uint32_t* remote_index, uint64_t* counter);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEBULA_AEAD_H */

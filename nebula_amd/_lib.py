@@ -1,0 +1,110 @@
+"""ctypes binding of libnebula_aead.so (the C ABI in include/nebula_aead.h).
+
+The product path has exactly one implementation: the gfx950 kernels behind this library. If the
+library is missing or does not load, every entry point raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libnebula_aead.so")
+
+ALG_AESGCM = 1
+ALG_CHACHAPOLY = 2
+
+OK = 0
+ERR_INVALID = -1
+ERR_AUTH = -2
+ERR_EXHAUSTED = -3
+ERR_NO_CIPHER = -4
+ERR_SHORT_BUFFER = -5
+ERR_HIP = -6
+ERR_NO_DEVICE = -7
+ERR_NO_KEY_SLOT = -8
+
+STATUS_OK = 0
+STATUS_AUTH_FAILED = 1
+STATUS_EXHAUSTED = 2
+STATUS_BAD_KEY = 3
+
+OVERHEAD = 16
+HEADER_LEN = 16
+REJECT_HEADROOM = 1 << 40
+REJECT_AFTER_MESSAGES = (1 << 64) - 1 - REJECT_HEADROOM
+KEYS_MIXED = 0xFFFFFFFF
+
+# neb_desc (include/nebula_aead.h)
+DESC_DTYPE = np.dtype(
+    [("src_off", "<u8"), ("dst_off", "<u8"), ("aad_off", "<u8"), ("counter", "<u8"),
+     ("len", "<u4"), ("aad_len", "<u4"), ("key_id", "<u4"), ("flags", "<u4")]
+)
+assert DESC_DTYPE.itemsize == 48
+
+# Every symbol include/nebula_aead.h declares, with (restype, argtypes).
+_vp, _u8p, _sz, _u32, _u64, _i = C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
+SIGNATURES = {
+    "neb_engine_create": (_i, [_i, _u32, C.POINTER(_vp)]),
+    "neb_engine_destroy": (_i, [_vp]),
+    "neb_engine_info": (_i, [_vp, C.POINTER(_i), C.POINTER(_u32), C.POINTER(_u32)]),
+    "neb_strerror": (C.c_char_p, [_i]),
+    "neb_cipher_create": (_i, [_vp, _i, _u8p, C.POINTER(_vp)]),
+    "neb_cipher_destroy": (_i, [_vp]),
+    "neb_cipher_key_id": (_u32, [_vp]),
+    "neb_cipher_alg": (_i, [_vp]),
+    "neb_cipher_name": (C.c_char_p, [_i]),
+    "neb_overhead": (_i, [_vp]),
+    "neb_encrypt_danger": (_i, [_vp, _u8p, _sz, _sz, _u8p, _sz, _u8p, _sz, _u64, _u8p, C.POINTER(_sz)]),
+    "neb_decrypt_danger": (_i, [_vp, _u8p, _sz, _sz, _u8p, _sz, _u8p, _sz, _u64, _u8p, C.POINTER(_sz)]),
+    "neb_seal_batch": (_i, [_vp, _i, _vp, _u32, _vp, _vp, _u32, _vp]),
+    "neb_open_batch": (_i, [_vp, _i, _vp, _u32, _vp, _vp, _u32, _vp]),
+    "neb_seal_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _sz, _vp, _u32]),
+    "neb_open_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _sz, _vp, _u32]),
+    "neb_host_alloc": (_i, [_sz, C.POINTER(_vp)]),
+    "neb_host_free": (_i, [_vp]),
+    "neb_header_encode": (None, [_u8p, C.c_uint8, C.c_uint8, C.c_uint8, _u32, _u64]),
+    "neb_header_parse": (_i, [_u8p, _sz, _u8p, _u8p, _u8p, C.POINTER(C.c_uint16), C.POINTER(_u32),
+                              C.POINTER(_u64)]),
+}
+
+_lib = None
+
+
+class NebError(RuntimeError):
+    def __init__(self, rc: int, what: str = ""):
+        self.rc = rc
+        msg = strerror(rc) if _lib is not None else str(rc)
+        super().__init__(f"{what}: {msg} ({rc})" if what else f"{msg} ({rc})")
+
+
+def build() -> None:
+    """Compile libnebula_aead.so in-tree (hipcc --offload-arch=gfx950)."""
+    subprocess.run(["make", "-s", "-C", PKG_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` "
+                               "(nebula_amd has no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def strerror(rc: int) -> str:
+    return lib().neb_strerror(rc).decode()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != OK:
+        raise NebError(rc, what)

@@ -1,0 +1,469 @@
+// engine.cpp — host side of the C ABI in include/nebula_aead.h.
+//
+// Owns one HIP device per engine: its stream, the device key table, pinned staging for the
+// per-packet CipherState calls, and the double-buffered host-resident batch pipeline. All packet
+// arithmetic runs in the gfx950 kernels (aes_gcm.hip, chacha_poly.hip); there is no CPU path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/nebula_aead.h"
+#include "layout.hpp"
+
+extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
+extern "C" hipError_t neb_gcm_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                                    const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint, int32_t* d_status,
+                                    int cu_count, hipStream_t s);
+extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
+extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                                       const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
+                                       int32_t* d_status, int cu_count, hipStream_t s);
+
+namespace {
+
+constexpr size_t kStageMin = 1 << 16;
+constexpr int kPipeStreams = 2;
+constexpr uint32_t kPipeChunkPkts = 8192;
+
+struct PipeSlot {
+    hipStream_t stream = nullptr;
+    uint8_t* d_buf = nullptr;
+    size_t d_cap = 0;
+    neb_desc* d_desc = nullptr;
+    int32_t* d_status = nullptr;
+    neb_desc* h_desc = nullptr;  // pinned
+    int32_t* h_status = nullptr; // pinned
+    int32_t* user_status = nullptr;
+    uint32_t user_begin = 0, count = 0;
+};
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct neb_engine {
+    int device = 0;
+    int cu_count = 0;
+    hipStream_t stream = nullptr;
+    uint32_t max_keys = 0;
+    uint32_t* d_keys = nullptr;
+    std::vector<int> slot_alg;  // 0 = free
+    std::mutex key_mu;
+
+    std::mutex io_mu;  // per-packet staging
+    uint8_t* h_stage = nullptr;
+    uint8_t* d_stage = nullptr;
+    size_t stage_cap = 0;
+
+    std::mutex pipe_mu;
+    PipeSlot pipe[kPipeStreams];
+};
+
+struct neb_cipher {
+    neb_engine* e;
+    uint32_t key_id;
+    int alg;
+};
+
+#define HIP_TRY(x)                               \
+    do {                                         \
+        hipError_t err_ = (x);                   \
+        if (err_ != hipSuccess) return NEB_ERR_HIP; \
+    } while (0)
+
+static int ensure_stage(neb_engine* e, size_t bytes) {
+    if (bytes <= e->stage_cap) return NEB_OK;
+    size_t cap = std::max(kStageMin, align_up(bytes, 1 << 16));
+    if (e->h_stage) hipHostFree(e->h_stage);
+    if (e->d_stage) hipFree(e->d_stage);
+    e->h_stage = nullptr;
+    e->d_stage = nullptr;
+    e->stage_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&e->h_stage, cap, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&e->d_stage, cap));
+    e->stage_cap = cap;
+    return NEB_OK;
+}
+
+extern "C" {
+
+NEB_API const char* neb_strerror(int rc) {
+    switch (rc) {
+        case NEB_OK: return "ok";
+        case NEB_ERR_INVALID: return "invalid argument";
+        case NEB_ERR_AUTH: return "cipher: message authentication failed";
+        case NEB_ERR_EXHAUSTED: return "message counter exhausted";
+        case NEB_ERR_NO_CIPHER: return "no cipher state available to encrypt";
+        case NEB_ERR_SHORT_BUFFER: return "output buffer too small";
+        case NEB_ERR_HIP: return "HIP runtime error";
+        case NEB_ERR_NO_DEVICE: return "no usable gfx950 device";
+        case NEB_ERR_NO_KEY_SLOT: return "key table full";
+        default: return "unknown error";
+    }
+}
+
+NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
+    if (!out || max_keys == 0 || max_keys == NEB_KEYS_MIXED) return NEB_ERR_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NEB_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return NEB_ERR_NO_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NEB_ERR_NO_DEVICE;
+    HIP_TRY(hipSetDevice(device));
+    neb_engine* e = new (std::nothrow) neb_engine();
+    if (!e) return NEB_ERR_INVALID;
+    e->device = device;
+    e->cu_count = prop.multiProcessorCount;
+    e->max_keys = max_keys;
+    e->slot_alg.assign(max_keys, 0);
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess ||
+        hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess) {
+        neb_engine_destroy(e);
+        return NEB_ERR_HIP;
+    }
+    *out = e;
+    return NEB_OK;
+}
+
+NEB_API int neb_engine_destroy(neb_engine* e) {
+    if (!e) return NEB_ERR_INVALID;
+    hipSetDevice(e->device);
+    if (e->stream) hipStreamSynchronize(e->stream);
+    for (auto& s : e->pipe) {
+        if (s.stream) { hipStreamSynchronize(s.stream); hipStreamDestroy(s.stream); }
+        if (s.d_buf) hipFree(s.d_buf);
+        if (s.d_desc) hipFree(s.d_desc);
+        if (s.d_status) hipFree(s.d_status);
+        if (s.h_desc) hipHostFree(s.h_desc);
+        if (s.h_status) hipHostFree(s.h_status);
+    }
+    if (e->d_keys) hipFree(e->d_keys);
+    if (e->h_stage) hipHostFree(e->h_stage);
+    if (e->d_stage) hipFree(e->d_stage);
+    if (e->stream) hipStreamDestroy(e->stream);
+    delete e;
+    return NEB_OK;
+}
+
+NEB_API int neb_engine_info(const neb_engine* e, int* device, uint32_t* max_keys, uint32_t* key_record_bytes) {
+    if (!e) return NEB_ERR_INVALID;
+    if (device) *device = e->device;
+    if (max_keys) *max_keys = e->max_keys;
+    if (key_record_bytes) *key_record_bytes = neb::kKeyRecBytes;
+    return NEB_OK;
+}
+
+NEB_API const char* neb_cipher_name(int alg) {
+    return alg == NEB_ALG_AESGCM ? "AESGCM" : alg == NEB_ALG_CHACHAPOLY ? "ChaChaPoly" : nullptr;
+}
+
+NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out) {
+    if (!e || !key || !out || (alg != NEB_ALG_AESGCM && alg != NEB_ALG_CHACHAPOLY)) return NEB_ERR_INVALID;
+    *out = nullptr;
+    uint32_t slot;
+    {
+        std::lock_guard<std::mutex> g(e->key_mu);
+        auto it = std::find(e->slot_alg.begin(), e->slot_alg.end(), 0);
+        if (it == e->slot_alg.end()) return NEB_ERR_NO_KEY_SLOT;
+        slot = (uint32_t)(it - e->slot_alg.begin());
+        *it = -1;  // reserved
+    }
+    int rc = NEB_OK;
+    {
+        std::lock_guard<std::mutex> g(e->io_mu);
+        hipSetDevice(e->device);
+        rc = ensure_stage(e, 64);
+        if (rc == NEB_OK) {
+            std::memcpy(e->h_stage, key, 32);
+            uint32_t* rec = e->d_keys + (size_t)slot * neb::kKeyRecDwords;
+            hipError_t err = hipMemcpyAsync(e->d_stage, e->h_stage, 32, hipMemcpyHostToDevice, e->stream);
+            if (err == hipSuccess) err = hipMemsetAsync(rec, 0, neb::kKeyRecBytes, e->stream);
+            if (err == hipSuccess)
+                err = alg == NEB_ALG_AESGCM ? neb_gcm_key_setup(e->d_stage, rec, e->stream)
+                                            : neb_chacha_key_setup(e->d_stage, rec, e->stream);
+            if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+            std::memset(e->h_stage, 0, 32);
+            if (err != hipSuccess) rc = NEB_ERR_HIP;
+        }
+    }
+    std::lock_guard<std::mutex> g(e->key_mu);
+    if (rc != NEB_OK) {
+        e->slot_alg[slot] = 0;
+        return rc;
+    }
+    neb_cipher* c = new (std::nothrow) neb_cipher{e, slot, alg};
+    if (!c) {
+        e->slot_alg[slot] = 0;
+        return NEB_ERR_INVALID;
+    }
+    e->slot_alg[slot] = alg;
+    *out = c;
+    return NEB_OK;
+}
+
+NEB_API int neb_cipher_destroy(neb_cipher* c) {
+    if (!c) return NEB_ERR_INVALID;
+    neb_engine* e = c->e;
+    {
+        std::lock_guard<std::mutex> g(e->io_mu);
+        hipSetDevice(e->device);
+        hipMemsetAsync(e->d_keys + (size_t)c->key_id * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, e->stream);
+        hipStreamSynchronize(e->stream);
+    }
+    {
+        std::lock_guard<std::mutex> g(e->key_mu);
+        e->slot_alg[c->key_id] = 0;
+    }
+    delete c;
+    return NEB_OK;
+}
+
+NEB_API uint32_t neb_cipher_key_id(const neb_cipher* c) { return c ? c->key_id : NEB_KEYS_MIXED; }
+NEB_API int neb_cipher_alg(const neb_cipher* c) { return c ? c->alg : 0; }
+NEB_API int neb_overhead(const neb_cipher* c) { return c ? NEB_OVERHEAD : 0; }
+
+static void fill_nonce(int alg, uint64_t n, uint8_t* nb) {
+    if (!nb) return;
+    nb[0] = nb[1] = nb[2] = nb[3] = 0;
+    for (int i = 0; i < 8; i++) nb[4 + i] = alg == NEB_ALG_AESGCM ? (uint8_t)(n >> (56 - 8 * i)) : (uint8_t)(n >> (8 * i));
+}
+
+static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                               int32_t* d_status, uint32_t key_hint, hipStream_t s) {
+    if (alg == NEB_ALG_AESGCM)
+        return neb_gcm_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, e->cu_count, s);
+    return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, e->cu_count, s);
+}
+
+// One packet through the device: [desc | status | aad | payload (+tag)] in one staging buffer.
+static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len, const uint8_t* in, size_t in_len,
+                      size_t pay_len, uint64_t n, uint8_t* dst, int32_t* st_out) {
+    neb_engine* e = c->e;
+    const size_t o_desc = 0, o_status = 64, o_aad = 128;
+    const size_t o_pay = align_up(o_aad + ad_len, 16);
+    const size_t total = o_pay + pay_len + 16;
+    std::lock_guard<std::mutex> g(e->io_mu);
+    hipSetDevice(e->device);
+    int rc = ensure_stage(e, total);
+    if (rc != NEB_OK) return rc;
+    uint8_t* h = e->h_stage;
+    neb_desc d{};
+    d.src_off = o_pay - o_aad;
+    d.dst_off = o_pay - o_aad;
+    d.aad_off = 0;
+    d.counter = n;
+    d.len = (uint32_t)pay_len;
+    d.aad_len = (uint32_t)ad_len;
+    d.key_id = c->key_id;
+    std::memcpy(h + o_desc, &d, sizeof d);
+    if (ad_len) std::memcpy(h + o_aad, ad, ad_len);
+    if (in_len) std::memcpy(h + o_pay, in, in_len);
+    hipError_t err = hipMemcpyAsync(e->d_stage, h, o_pay + in_len, hipMemcpyHostToDevice, e->stream);
+    if (err == hipSuccess)
+        err = launch_batch(e, c->alg, open, (const neb_desc*)(e->d_stage + o_desc), 1, e->d_stage + o_aad,
+                           (int32_t*)(e->d_stage + o_status), c->key_id, e->stream);
+    const size_t out_len = open ? pay_len : pay_len + 16;
+    if (err == hipSuccess) err = hipMemcpyAsync(h + o_status, e->d_stage + o_status, 4, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess && out_len)
+        err = hipMemcpyAsync(h + o_pay, e->d_stage + o_pay, out_len, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    if (err != hipSuccess) return NEB_ERR_HIP;
+    std::memcpy(st_out, h + o_status, 4);
+    if (out_len) std::memcpy(dst, h + o_pay, out_len);
+    return NEB_OK;
+}
+
+NEB_API int neb_encrypt_danger(neb_cipher* c, uint8_t* out, size_t out_len, size_t out_cap, const uint8_t* ad,
+                               size_t ad_len, const uint8_t* pt, size_t pt_len, uint64_t n, uint8_t* nb,
+                               size_t* ret_len) {
+    if (ret_len) *ret_len = 0;
+    if (!c) return NEB_ERR_NO_CIPHER;  // aesgcm.go:25-27
+    if (n >= NEB_REJECT_AFTER_MESSAGES) return NEB_ERR_EXHAUSTED;  // aesgcm.go:28-30
+    if ((!out && out_cap) || (!ad && ad_len) || (!pt && pt_len) || pt_len > 0xFFFFFFF0u || ad_len > 0xFFFFFFF0u)
+        return NEB_ERR_INVALID;
+    if (out_cap < out_len || out_cap - out_len < pt_len + NEB_OVERHEAD) return NEB_ERR_SHORT_BUFFER;
+    fill_nonce(c->alg, n, nb);
+    int32_t st = -1;
+    int rc = one_packet(c, 0, ad, ad_len, pt, pt_len, pt_len, n, out + out_len, &st);
+    if (rc != NEB_OK) return rc;
+    if (st != NEB_STATUS_OK) return st == NEB_STATUS_EXHAUSTED ? NEB_ERR_EXHAUSTED : NEB_ERR_INVALID;
+    if (ret_len) *ret_len = out_len + pt_len + NEB_OVERHEAD;
+    return NEB_OK;
+}
+
+NEB_API int neb_decrypt_danger(neb_cipher* c, uint8_t* out, size_t out_len, size_t out_cap, const uint8_t* ad,
+                               size_t ad_len, const uint8_t* ct, size_t ct_len, uint64_t n, uint8_t* nb,
+                               size_t* ret_len) {
+    if (ret_len) *ret_len = 0;
+    if (!c) return NEB_OK;  // aesgcm.go:40-42: ([]byte{}, nil)
+    if ((!ad && ad_len) || (!ct && ct_len) || ct_len > 0xFFFFFFF0u || ad_len > 0xFFFFFFF0u) return NEB_ERR_INVALID;
+    fill_nonce(c->alg, n, nb);
+    if (ct_len < NEB_OVERHEAD) return NEB_ERR_AUTH;  // Open: ciphertext shorter than the tag
+    const size_t pt_len = ct_len - NEB_OVERHEAD;
+    if ((!out && out_cap) || out_cap < out_len || out_cap - out_len < pt_len) return NEB_ERR_SHORT_BUFFER;
+    int32_t st = -1;
+    int rc = one_packet(c, 1, ad, ad_len, ct, ct_len, pt_len, n, out + out_len, &st);
+    if (rc != NEB_OK) return rc;
+    if (st == NEB_STATUS_AUTH_FAILED) return NEB_ERR_AUTH;  // plaintext region already zeroed
+    if (st != NEB_STATUS_OK) return NEB_ERR_INVALID;
+    if (ret_len) *ret_len = out_len + pt_len;
+    return NEB_OK;
+}
+
+static int check_batch(neb_engine* e, int alg, uint32_t key_hint) {
+    if (!e || (alg != NEB_ALG_AESGCM && alg != NEB_ALG_CHACHAPOLY)) return NEB_ERR_INVALID;
+    if (key_hint != NEB_KEYS_MIXED) {
+        std::lock_guard<std::mutex> g(e->key_mu);
+        if (key_hint >= e->max_keys || e->slot_alg[key_hint] != alg) return NEB_ERR_INVALID;
+    }
+    return NEB_OK;
+}
+
+static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                        int32_t* d_status, uint32_t key_hint, void* stream) {
+    int rc = check_batch(e, alg, key_hint);
+    if (rc != NEB_OK) return rc;
+    if (n == 0) return NEB_OK;
+    if (!d_desc || !d_arena || !d_status) return NEB_ERR_INVALID;
+    hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    return launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s) == hipSuccess ? NEB_OK : NEB_ERR_HIP;
+}
+
+NEB_API int neb_seal_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                           int32_t* d_status, uint32_t key_hint, void* stream) {
+    return batch_device(e, alg, 0, d_desc, n, d_arena, d_status, key_hint, stream);
+}
+
+NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                           int32_t* d_status, uint32_t key_hint, void* stream) {
+    return batch_device(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, stream);
+}
+
+// Host-resident batch: chunks of kPipeChunkPkts packets, each chunk's arena span copied H2D,
+// processed and copied D2H on one of two streams, so chunk i+1's copies overlap chunk i's kernel.
+static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n, uint8_t* arena,
+                      size_t arena_len, int32_t* status, uint32_t key_hint) {
+    int rc = check_batch(e, alg, key_hint);
+    if (rc != NEB_OK) return rc;
+    if (n == 0) return NEB_OK;
+    if (!desc || !arena || !status) return NEB_ERR_INVALID;
+    std::lock_guard<std::mutex> g(e->pipe_mu);
+    hipSetDevice(e->device);
+    for (auto& s : e->pipe) {
+        if (!s.stream) {
+            HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+            HIP_TRY(hipMalloc((void**)&s.d_desc, kPipeChunkPkts * sizeof(neb_desc)));
+            HIP_TRY(hipMalloc((void**)&s.d_status, kPipeChunkPkts * sizeof(int32_t)));
+            HIP_TRY(hipHostMalloc((void**)&s.h_desc, kPipeChunkPkts * sizeof(neb_desc), hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&s.h_status, kPipeChunkPkts * sizeof(int32_t), hipHostMallocDefault));
+        }
+        s.count = 0;
+    }
+    int slot = 0;
+    for (uint32_t begin = 0; begin < n; begin += kPipeChunkPkts, slot ^= 1) {
+        PipeSlot& s = e->pipe[slot];
+        if (s.count) {  // retire this slot's previous chunk before reusing its buffers
+            HIP_TRY(hipStreamSynchronize(s.stream));
+            std::memcpy(s.user_status + s.user_begin, s.h_status, s.count * sizeof(int32_t));
+            s.count = 0;
+        }
+        const uint32_t cnt = std::min(kPipeChunkPkts, n - begin);
+        uint64_t lo = ~0ULL, hi = 0;
+        for (uint32_t i = 0; i < cnt; i++) {
+            const neb_desc& d = desc[begin + i];
+            const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
+            lo = std::min({lo, d.src_off, d.dst_off, d.aad_off});
+            hi = std::max({hi, d.src_off + pay, d.dst_off + outl, d.aad_off + d.aad_len});
+        }
+        if (hi > arena_len || lo > hi) return NEB_ERR_INVALID;
+        lo &= ~(uint64_t)15;
+        const size_t span = (size_t)(hi - lo);
+        if (span > s.d_cap) {
+            if (s.d_buf) { HIP_TRY(hipStreamSynchronize(s.stream)); hipFree(s.d_buf); s.d_buf = nullptr; s.d_cap = 0; }
+            size_t cap = align_up(span, 1 << 20);
+            HIP_TRY(hipMalloc((void**)&s.d_buf, cap));
+            s.d_cap = cap;
+        }
+        for (uint32_t i = 0; i < cnt; i++) {
+            neb_desc d = desc[begin + i];
+            d.src_off -= lo;
+            d.dst_off -= lo;
+            d.aad_off -= lo;
+            s.h_desc[i] = d;
+        }
+        HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s.stream));
+        HIP_TRY(hipMemcpyAsync(s.d_buf, arena + lo, span, hipMemcpyHostToDevice, s.stream));
+        HIP_TRY(launch_batch(e, alg, open, s.d_desc, cnt, s.d_buf, s.d_status, key_hint, s.stream));
+        HIP_TRY(hipMemcpyAsync(arena + lo, s.d_buf, span, hipMemcpyDeviceToHost, s.stream));
+        HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
+        s.user_status = status;
+        s.user_begin = begin;
+        s.count = cnt;
+    }
+    for (auto& s : e->pipe) {
+        if (s.count) {
+            HIP_TRY(hipStreamSynchronize(s.stream));
+            std::memcpy(s.user_status + s.user_begin, s.h_status, s.count * sizeof(int32_t));
+            s.count = 0;
+        }
+    }
+    return NEB_OK;
+}
+
+NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
+                                size_t arena_len, int32_t* status, uint32_t key_hint) {
+    return batch_host(e, alg, 0, desc, n, arena, arena_len, status, key_hint);
+}
+
+NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
+                                size_t arena_len, int32_t* status, uint32_t key_hint) {
+    return batch_host(e, alg, 1, desc, n, arena, arena_len, status, key_hint);
+}
+
+NEB_API int neb_host_alloc(size_t bytes, void** out) {
+    if (!out || !bytes) return NEB_ERR_INVALID;
+    return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? NEB_OK : NEB_ERR_HIP;
+}
+
+NEB_API int neb_host_free(void* p) {
+    if (!p) return NEB_ERR_INVALID;
+    return hipHostFree(p) == hipSuccess ? NEB_OK : NEB_ERR_HIP;
+}
+
+// header/header.go:102-110
+NEB_API void neb_header_encode(uint8_t b[16], uint8_t version, uint8_t type, uint8_t subtype, uint32_t remote_index,
+                               uint64_t counter) {
+    b[0] = (uint8_t)(version << 4 | (type & 0x0f));
+    b[1] = subtype;
+    b[2] = 0;
+    b[3] = 0;
+    for (int i = 0; i < 4; i++) b[4 + i] = (uint8_t)(remote_index >> (24 - 8 * i));
+    for (int i = 0; i < 8; i++) b[8 + i] = (uint8_t)(counter >> (56 - 8 * i));
+}
+
+// header/header.go:143-156
+NEB_API int neb_header_parse(const uint8_t* b, size_t len, uint8_t* version, uint8_t* type, uint8_t* subtype,
+                             uint16_t* reserved, uint32_t* remote_index, uint64_t* counter) {
+    if (!b || len < NEB_HEADER_LEN) return NEB_ERR_INVALID;
+    if (version) *version = (b[0] >> 4) & 0x0f;
+    if (type) *type = b[0] & 0x0f;
+    if (subtype) *subtype = b[1];
+    if (reserved) *reserved = (uint16_t)(b[2] << 8 | b[3]);
+    if (remote_index) *remote_index = (uint32_t)b[4] << 24 | (uint32_t)b[5] << 16 | (uint32_t)b[6] << 8 | b[7];
+    if (counter) {
+        uint64_t c = 0;
+        for (int i = 0; i < 8; i++) c = c << 8 | b[8 + i];
+        *counter = c;
+    }
+    return NEB_OK;
+}
+
+}  // extern "C"

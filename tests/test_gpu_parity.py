@@ -1,0 +1,280 @@
+"""GPU parity: the gfx950 kernels through the C ABI against the oracle, bit-exact.
+
+Batches are the BASELINE.json configs (full C1; C2-C5 at sizes the oracle finishes in seconds),
+the committed golden digests, edge shapes (empty payload / AAD, partial blocks, long AAD GMAC-only
+relay, jumbo), failure semantics (tampered CT / tag / AAD / counter -> status 1 and zeroed payload,
+exhausted counter -> status 2, wrong key -> status 3), and at full C2 size the size-independent
+round-trip property seal -> open == identity with every tag distinct.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from nebula_amd import _lib as L
+from nebula_amd import workload as W
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def run_device(engine, b, seal=True, arena=None, key_hint="auto", desc=None):
+    from nebula_amd.batch import DeviceBatch, install_keys
+
+    ciphers = install_keys(engine, b)
+    try:
+        db = DeviceBatch(engine, b, ciphers)
+        if arena is not None:
+            import torch
+            db.arena.copy_(torch.from_numpy(arena))
+        if desc is not None:
+            import torch
+            d = desc.copy()
+            slots = np.array([c.key_id for c in ciphers], np.uint32)
+            d["key_id"] = np.where(desc["key_id"] < len(slots), slots[np.minimum(desc["key_id"], len(slots) - 1)],
+                                   desc["key_id"])
+            db.desc.copy_(torch.from_numpy(d.view(np.uint8)))
+        if key_hint != "auto":
+            db.key_hint = key_hint
+        (db.seal if seal else db.open)()
+        import torch
+        torch.cuda.synchronize()
+        return db.arena_host(), db.status_host()
+    finally:
+        for c in ciphers:
+            c.destroy()
+
+
+def oracle_seal(oracle_mod, b, arena=None):
+    a = (b.arena if arena is None else arena).copy()
+    st = oracle_mod.batch(b.alg, 0, b.keys, b.desc, a)
+    return a, st
+
+
+def oracle_open(oracle_mod, b, arena):
+    a = arena.copy()
+    st = oracle_mod.batch(b.alg, 1, b.keys, b.desc, a)
+    return a, st
+
+
+@pytest.mark.parametrize("name", ["c1_aesgcm_1key_1024x1300", "c3_aesgcm_4096keys_512x1300",
+                                  "c4_chachapoly_4096keys_512x1300", "c5_aesgcm_imix_4096keys_2048"])
+def test_golden_batches(engine, name):
+    import make_golden
+
+    meta = json.load(open(os.path.join(GOLD, "batches.json")))[name]
+    b = make_golden.BATCHES[name]()
+    arena, st = run_device(engine, b, seal=True)
+    assert (st == 0).all()
+    assert hashlib.sha256(arena.tobytes()).hexdigest() == meta["sealed_sha256"]
+    # and back
+    opened, st2 = run_device(engine, b, seal=False, arena=arena)
+    assert (st2 == 0).all()
+    exp = b.arena.copy()
+    slots_o, slots_e = opened.reshape(b.n, b.stride), exp.reshape(b.n, b.stride)
+    for i in range(b.n):
+        ln = int(b.desc["len"][i])
+        assert np.array_equal(slots_o[i, :16 + ln], slots_e[i, :16 + ln])
+
+
+@pytest.mark.parametrize("cfg,scale", [(1, 1 / 64), (2, 1 / 64), (3, 1 / 64), (4, 1 / 512)])
+def test_configs_scaled_vs_oracle(engine, oracle_mod, cfg, scale):
+    b = W.config(cfg, scale)
+    ref, st_ref = oracle_seal(oracle_mod, b)
+    got, st = run_device(engine, b, seal=True)
+    assert (st == 0).all() and (st_ref == 0).all()
+    assert np.array_equal(got, ref)
+    ref_o, _ = oracle_open(oracle_mod, b, ref)
+    got_o, st_o = run_device(engine, b, seal=False, arena=ref)
+    assert (st_o == 0).all()
+    assert np.array_equal(got_o, ref_o)
+
+
+def _edge_batch(alg, lens, alens, nkeys=3, seed=99):
+    rng = np.random.default_rng(seed)
+    n = len(lens)
+    keys = rng.integers(0, 256, 32 * nkeys, dtype=np.uint8)
+    offs, pos = [], 0
+    for ln, al in zip(lens, alens):
+        aad_off = pos
+        src = (aad_off + al + 15) // 16 * 16
+        offs.append((aad_off, src))
+        pos = (src + ln + 16 + 63) // 64 * 64
+    arena = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    desc = np.zeros(n, L.DESC_DTYPE)
+    for i, ((a, s), ln, al) in enumerate(zip(offs, lens, alens)):
+        desc[i] = (s, s, a, int(rng.integers(0, 2**63)), ln, al, i % nkeys, 0)
+    return W.Batch(alg, keys, np.zeros(nkeys, np.uint32), desc, arena, 0, "edge")
+
+
+EDGE_LENS = [0, 1, 15, 16, 17, 31, 32, 33, 63, 64, 65, 255, 256, 257, 1299, 1300, 1301, 4096, 9001]
+
+
+@pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
+def test_edge_shapes(engine, oracle_mod, alg):
+    lens, alens = [], []
+    for ln in EDGE_LENS:
+        for al in (0, 1, 16, 17, 40):
+            lens.append(ln)
+            alens.append(al)
+    # GMAC-only relay: empty payload, AAD = whole inner packet (connection_state.go:121-148)
+    lens += [0, 0]
+    alens += [1348, 9033]
+    b = _edge_batch(alg, lens, alens)
+    ref, _ = oracle_seal(oracle_mod, b)
+    got, st = run_device(engine, b, seal=True)
+    assert (st == 0).all()
+    assert np.array_equal(got, ref)
+    ref_o, _ = oracle_open(oracle_mod, b, ref)
+    got_o, st_o = run_device(engine, b, seal=False, arena=ref)
+    assert (st_o == 0).all()
+    assert np.array_equal(got_o, ref_o)
+
+
+@pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
+def test_unaligned_offsets(engine, oracle_mod, alg):
+    """Descriptors may point anywhere (Go slices): odd AAD / payload offsets, out-of-place."""
+    rng = np.random.default_rng(5)
+    n = 40
+    keys = rng.integers(0, 256, 64, dtype=np.uint8)
+    arena = rng.integers(0, 256, n * 3000, dtype=np.uint8)
+    desc = np.zeros(n, L.DESC_DTYPE)
+    for i in range(n):
+        base = i * 3000
+        ln = int(rng.integers(0, 1400))
+        al = int(rng.integers(0, 40))
+        a = base + int(rng.integers(0, 7))
+        s = a + al + int(rng.integers(0, 5))
+        dst = s if i % 2 else base + 1500 + int(rng.integers(0, 3))
+        desc[i] = (s, dst, a, int(rng.integers(0, 2**63)), ln, al, i % 2, 0)
+    b = W.Batch(alg, keys, np.zeros(2, np.uint32), desc, arena, 0, "unaligned")
+    ref, _ = oracle_seal(oracle_mod, b)
+    got, st = run_device(engine, b, seal=True)
+    assert (st == 0).all()
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
+def test_auth_failures_zero_payload_only(engine, oracle_mod, alg):
+    b = W.make_batch(alg, 64, 4, name="tamper")
+    sealed, _ = oracle_seal(oracle_mod, b)
+    t = sealed.copy()
+    d = b.desc
+    victims = {3: "ct", 10: "tag", 17: "aad", 33: "ct-last-byte"}
+    t[int(d["src_off"][3]) + 5] ^= 0x80
+    t[int(d["src_off"][10]) + int(d["len"][10]) + 7] ^= 1
+    t[int(d["aad_off"][17]) + 12] ^= 4
+    t[int(d["src_off"][33]) + int(d["len"][33]) - 1] ^= 1
+    desc = d.copy()
+    desc["counter"][50] += 1  # wrong nonce
+    victims[50] = "nonce"
+    got, st = run_device(engine, b, seal=False, arena=t, desc=desc)
+    exp_fail = sorted(victims)
+    assert sorted(np.flatnonzero(st == L.STATUS_AUTH_FAILED).tolist()) == exp_fail
+    assert (st[[i for i in range(64) if i not in victims]] == 0).all()
+    for i in exp_fail:
+        s, ln = int(d["src_off"][i]), int(d["len"][i])
+        assert not got[s:s + ln].any(), victims[i]
+        a = int(d["aad_off"][i])
+        assert np.array_equal(got[a:a + 16], t[a:a + 16])          # header untouched
+        assert np.array_equal(got[s + ln:s + ln + 16], t[s + ln:s + ln + 16])  # tag untouched
+        nxt = a + b.stride
+        assert np.array_equal(got[s + ln + 16:nxt], t[s + ln + 16:nxt])  # neighbour untouched
+
+
+@pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
+def test_exhausted_counter_and_bad_key(engine, oracle_mod, alg):
+    b = W.make_batch(alg, 16, 2, name="ex")
+    desc = b.desc.copy()
+    desc["counter"][2] = L.REJECT_AFTER_MESSAGES
+    desc["counter"][3] = L.REJECT_AFTER_MESSAGES - 1
+    desc["key_id"][5] = 7000  # not installed
+    got, st = run_device(engine, b, seal=True, desc=desc)
+    assert st[2] == L.STATUS_EXHAUSTED and st[5] == L.STATUS_BAD_KEY
+    assert (np.delete(st, [2, 5]) == 0).all()
+    s = int(desc["src_off"][2])
+    assert np.array_equal(got[s:s + 1316], b.arena[s:s + 1316])  # nothing written
+    b2 = W.Batch(alg, b.keys, b.remote_index, desc, b.arena, b.stride, "ex")
+    ref, _ = oracle_seal(oracle_mod, W.Batch(alg, b.keys, b.remote_index, desc[[3]], b.arena, b.stride, "x"))
+    s3 = int(desc["src_off"][3])
+    assert np.array_equal(got[s3:s3 + 1316], ref[s3:s3 + 1316])
+    del b2
+
+
+def test_key_hint_mismatch_flags_bad_key(engine):
+    b = W.make_batch(L.ALG_AESGCM, 8, 2, name="hint")
+    from nebula_amd.batch import DeviceBatch, install_keys
+    import torch
+
+    ciphers = install_keys(engine, b)
+    try:
+        db = DeviceBatch(engine, b, ciphers)
+        db.key_hint = ciphers[0].key_id
+        db.seal()
+        torch.cuda.synchronize()
+        st = db.status_host()
+        kid = b.desc["key_id"]
+        assert (st[kid == 0] == 0).all() and (st[kid == 1] == L.STATUS_BAD_KEY).all()
+    finally:
+        for c in ciphers:
+            c.destroy()
+
+
+def test_full_c2_roundtrip_property(engine):
+    """Full 64 Ki x 1300 B (BASELINE configs[1]): open(seal(x)) == x, all tags distinct, and the
+    sealed digest matches the oracle on a strided sample of packets."""
+    import torch
+    from nebula_amd.batch import DeviceBatch, install_keys
+
+    b = W.config(1)
+    ciphers = install_keys(engine, b)
+    try:
+        db = DeviceBatch(engine, b, ciphers)
+        db.seal()
+        torch.cuda.synchronize()
+        assert (db.status_host() == 0).all()
+        sealed = db.arena_host()
+        tags = sealed.reshape(b.n, b.stride)[:, 16 + 1300:32 + 1300]
+        assert len({t.tobytes() for t in tags}) == b.n
+        db.open()
+        torch.cuda.synchronize()
+        assert (db.status_host() == 0).all()
+        opened = db.arena_host().reshape(b.n, b.stride)
+        assert np.array_equal(opened[:, :16 + 1300], b.arena.reshape(b.n, b.stride)[:, :16 + 1300])
+    finally:
+        for c in ciphers:
+            c.destroy()
+    import oracle
+
+    idx = np.arange(0, b.n, 257)
+    sub = W.Batch(b.alg, b.keys, b.remote_index, b.desc[idx], b.arena, b.stride, "sample")
+    ref = b.arena.copy()
+    oracle.batch(sub.alg, 0, sub.keys, sub.desc, ref)
+    s2, r2 = sealed.reshape(b.n, b.stride), ref.reshape(b.n, b.stride)
+    assert np.array_equal(s2[idx], r2[idx])
+
+
+@pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
+def test_host_pipeline_matches_device(engine, oracle_mod, alg):
+    from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
+
+    b = W.make_batch(alg, 20000, 64, sizes=(90, 576, 1300), ratio=(7, 4, 1), name="host")
+    ciphers = install_keys(engine, b)
+    try:
+        d = slot_desc(b, ciphers)
+        buf = PinnedBuffer(b.arena.nbytes)
+        buf.array[:] = b.arena
+        st = host_batch(engine, alg, False, d, buf.array)
+        assert (st == 0).all()
+        ref, _ = oracle_seal(oracle_mod, b)
+        assert np.array_equal(buf.array, ref)
+        st = host_batch(engine, alg, True, d, buf.array)
+        assert (st == 0).all()
+        ref_o, _ = oracle_open(oracle_mod, b, ref)
+        assert np.array_equal(buf.array, ref_o)
+        buf.free()
+    finally:
+        for c in ciphers:
+            c.destroy()

@@ -1,0 +1,124 @@
+"""CPU: pin the oracle (oracle/aead_oracle.c) before trusting it.
+
+- the reference's own AES-GCM KAT (noiseutil/fips140_test.go:18-31) and header KAT
+  (header/header_test.go:17-29), RFC 8439 §2.8.2 for ChaCha20-Poly1305;
+- randomised agreement with an independent implementation (OpenSSL EVP, oracle/evp_baseline.c)
+  over the edge sizes the data plane sees (empty payload, empty AAD, partial blocks, GMAC-only
+  relay with long AAD);
+- the committed batch digests in tests/golden/.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def kat():
+    with open(os.path.join(GOLD, "kat.json")) as f:
+        return json.load(f)
+
+
+def test_aesgcm_reference_kat(oracle_mod):
+    k = kat()["aesgcm_fips140_test"]
+    got = oracle_mod.seal(1, bytes.fromhex(k["key"]), bytes.fromhex(k["iv"]), bytes.fromhex(k["aad"]),
+                          bytes.fromhex(k["plaintext"]))
+    assert got.hex() == k["expected"]
+    # the KAT IV is exactly Nebula's AES nonce for n = 0xfacedbaddecaf888 (aesgcm.go:31-35)
+    assert oracle_mod.nonce(1, int(k["nebula_counter"], 16)).hex() == k["iv"]
+    assert oracle_mod.open_(1, bytes.fromhex(k["key"]), bytes.fromhex(k["iv"]), bytes.fromhex(k["aad"]),
+                            got) == bytes.fromhex(k["plaintext"])
+
+
+def test_chachapoly_rfc8439(oracle_mod):
+    k = kat()["chachapoly_rfc8439_2_8_2"]
+    got = oracle_mod.seal(2, bytes.fromhex(k["key"]), bytes.fromhex(k["iv"]), bytes.fromhex(k["aad"]),
+                          bytes.fromhex(k["plaintext"]))
+    assert got[-16:].hex() == k["expected_tag"]
+    assert got[:16].hex() == k["expected_ct_prefix"]
+
+
+def test_header_kat(oracle_mod):
+    k = kat()["header_test"]
+    f = k["fields"]
+    assert oracle_mod.header_encode(f["Version"], f["Type"], f["Subtype"], f["RemoteIndex"],
+                                    f["MessageCounter"]).hex() == k["bytes"]
+
+
+def test_nonce_layouts(oracle_mod):
+    n = 0x0102030405060708
+    assert oracle_mod.nonce(1, n).hex() == "000000000102030405060708"  # BE64, aesgcm.go:35
+    assert oracle_mod.nonce(2, n).hex() == "000000000807060504030201"  # LE64, chachapoly.go:34
+
+
+def test_reject_constants(oracle_mod):
+    assert oracle_mod.lib().ora_reject_after_messages() == (1 << 64) - 1 - (1 << 40)
+
+
+@pytest.mark.parametrize("alg", [1, 2])
+def test_oracle_matches_openssl_random(oracle_mod, alg):
+    rng = np.random.default_rng(1234 + alg)
+    sizes = list(range(0, 70)) + [127, 128, 129, 255, 256, 1299, 1300, 1301, 9001]
+    for ln in sizes:
+        for alen in (0, 1, 15, 16, 17, 40):
+            key = rng.integers(0, 256, 32, dtype=np.uint8)
+            arena = rng.integers(0, 256, 64 + alen + ln + 16, dtype=np.uint8)
+            d = np.zeros(1, oracle_mod.DESC_DTYPE)
+            d["aad_off"] = 0
+            d["aad_len"] = alen
+            d["src_off"] = d["dst_off"] = 64 + alen
+            d["len"] = ln
+            d["counter"] = int(rng.integers(0, 2**62))
+            a1, a2 = arena.copy(), arena.copy()
+            oracle_mod.batch(alg, 0, key, d, a1)
+            oracle_mod.evp_batch(alg, 0, key, d, a2)
+            assert np.array_equal(a1, a2), (alg, ln, alen)
+
+
+def test_gmac_only_relay_shape(oracle_mod):
+    """VerifyRelay (connection_state.go:121-148): empty plaintext, AAD = whole inner packet."""
+    rng = np.random.default_rng(7)
+    key = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    aad = bytes(rng.integers(0, 256, 1348, dtype=np.uint8))
+    nb = oracle_mod.nonce(1, 77)
+    tag = oracle_mod.seal(1, key, nb, aad, b"")
+    assert len(tag) == 16
+    assert oracle_mod.open_(1, key, nb, aad, tag) == b""
+    assert oracle_mod.open_(1, key, nb, aad[:-1] + b"\0", tag) is None
+
+
+def test_open_failure_zeroes_payload_only(oracle_mod):
+    """cipher_state_test.go:194-237 on the oracle: failed auth zeroes the plaintext region only."""
+    from nebula_amd import workload as W
+
+    b = W.make_batch(1, 8, 1, name="t")
+    arena = b.arena.copy()
+    oracle_mod.batch(1, 0, b.keys, b.desc, arena)
+    sealed = arena.copy()
+    arena[b.desc["src_off"][3]] ^= 1
+    st = oracle_mod.batch(1, 1, b.keys, b.desc, arena)
+    assert list(st) == [0, 0, 0, 1, 0, 0, 0, 0]
+    s3 = slice(int(b.desc["src_off"][3]), int(b.desc["src_off"][3]) + 1300)
+    assert not arena[s3].any()
+    hdr = slice(int(b.desc["aad_off"][3]), int(b.desc["aad_off"][3]) + 16)
+    tag = slice(s3.stop, s3.stop + 16)
+    assert np.array_equal(arena[hdr], sealed[hdr]) and np.array_equal(arena[tag], sealed[tag])
+
+
+@pytest.mark.parametrize("name", ["c1_aesgcm_1key_1024x1300", "c3_aesgcm_4096keys_512x1300",
+                                  "c4_chachapoly_4096keys_512x1300", "c5_aesgcm_imix_4096keys_2048"])
+def test_oracle_matches_golden_batches(oracle_mod, name):
+    import make_golden  # tests/golden is on sys.path (conftest.py)
+
+    meta = json.load(open(os.path.join(GOLD, "batches.json")))[name]
+    b = make_golden.BATCHES[name]()
+    assert hashlib.sha256(b.arena.tobytes()).hexdigest() == meta["plain_sha256"]
+    arena = b.arena.copy()
+    st = oracle_mod.batch(b.alg, 0, b.keys, b.desc, arena)
+    assert (st == 0).all()
+    assert hashlib.sha256(arena.tobytes()).hexdigest() == meta["sealed_sha256"]
+    tags = np.load(os.path.join(GOLD, f"{name}_tags.npy"))
+    assert hashlib.sha256(tags.tobytes()).hexdigest() == meta["tags_sha256"]
