@@ -93,6 +93,8 @@ NEB_API int neb_engine_destroy(neb_engine* e);
 NEB_API int neb_engine_info(const neb_engine* e, int* device, uint32_t* max_keys, uint32_t* key_record_bytes);
 /* Human-readable text of a return code. */
 NEB_API const char* neb_strerror(int rc);
+/* Detail of the last NEB_ERR_HIP / NEB_ERR_NO_DEVICE on the calling thread (HIP error string). */
+NEB_API const char* neb_last_error(void);
 
 /* ---- key install: noise.CipherFunc.Cipher(k) ----------------------------------------------- */
 
@@ -135,7 +137,7 @@ NEB_API int neb_decrypt_danger(neb_cipher* c, uint8_t* out, size_t out_len, size
 #define NEB_KEYS_MIXED 0xFFFFFFFFu
 
 /* Seal/open n packets. d_desc, d_arena, d_status are device pointers; `stream` is a hipStream_t
- * (NULL = the engine's stream). Asynchronous: returns after enqueueing. Every descriptor's key must
+ * (NULL = the HIP default stream). Asynchronous: returns after enqueueing. Every descriptor's key must
  * have algorithm `alg`. */
 NEB_API int neb_seal_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                            int32_t* d_status, uint32_t key_hint, void* stream);

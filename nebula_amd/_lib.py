@@ -52,6 +52,7 @@ SIGNATURES = {
     "neb_engine_destroy": (_i, [_vp]),
     "neb_engine_info": (_i, [_vp, C.POINTER(_i), C.POINTER(_u32), C.POINTER(_u32)]),
     "neb_strerror": (C.c_char_p, [_i]),
+    "neb_last_error": (C.c_char_p, []),
     "neb_cipher_create": (_i, [_vp, _i, _u8p, C.POINTER(_vp)]),
     "neb_cipher_destroy": (_i, [_vp]),
     "neb_cipher_key_id": (_u32, [_vp]),
@@ -78,6 +79,10 @@ class NebError(RuntimeError):
     def __init__(self, rc: int, what: str = ""):
         self.rc = rc
         msg = strerror(rc) if _lib is not None else str(rc)
+        if _lib is not None and rc in (ERR_HIP, ERR_NO_DEVICE):
+            detail = _lib.neb_last_error().decode()
+            if detail:
+                msg += f" [{detail}]"
         super().__init__(f"{what}: {msg} ({rc})" if what else f"{msg} ({rc})")
 
 
@@ -86,9 +91,24 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", PKG_DIR], check=True)
 
 
+def _pin_hip_runtime() -> None:
+    """Load PyTorch's HIP runtime before ours when torch is installed.
+
+    torch-ROCm ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's). Whichever is loaded
+    first serves the whole process, and torch cannot initialise the GPU on a runtime it did not
+    bring. Importing torch first makes every HIP call in the process, ours included, go through
+    one runtime, so torch tensors, streams and events interoperate with the engine.
+    """
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib():
     global _lib
     if _lib is None:
+        _pin_hip_runtime()
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` "
                                "(nebula_amd has no CPU fallback)")

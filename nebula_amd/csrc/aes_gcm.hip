@@ -8,30 +8,28 @@
 //  * A packet's GHASH input is n = a + m + 1 blocks (a AAD blocks, m ciphertext blocks, 1 length
 //    block), front-padded with zero blocks to n' = 16·R. In round r lane l owns padded block
 //    g' = 16r + l + 1: it runs the AES-CTR keystream for that block (if it is a ciphertext block),
-//    loads / XORs / stores the 16 payload bytes (coalesced: 16 lanes × 16 B contiguous per packet),
-//    and folds the block into its Horner accumulator A_l = A_l·H^16 ⊕ X.
-//  * After R rounds GHASH = Σ_l A_l·H^(16-l): lane l multiplies by H^(NLP - l mod NLP) from a
-//    per-lane table, the NLP-lane groups XOR-reduce, and a log-tree over the 16/NLP groups with
-//    multipliers H^NLP, H^2NLP, … finishes. The length block always lands on lane 15 of the last
-//    round; that lane also computes E_K(J0) for the tag.
-//  * AES: T-table in LDS with one copy per lane (64 copies × 1 KiB): lookups are bank-conflict-free
-//    and the address is one v_perm_b32. GF(2^128) multiply: 4-bit tables M[v] = v·H^k in LDS
-//    (16 × 16 B = 256 B: the 16 entries cover all 64 banks, so a ds_read_b128 of one table never
-//    conflicts), 32 independent lookups with deferred reduction (no serial dependency).
-//  * SINGLE (one tunnel key for the whole batch, NEB_KEYS_MIXED not set): round keys are
-//    wave-uniform (SGPRs), H^1..H^16 tables are built once per workgroup, NLP = 16.
-//    MIXED keys: each packet's round keys and 5 tables (H, H^2, H^4, H^8, H^16; NLP = 2) are
-//    staged in the wave's LDS slice per packet group.
+//    loads / XORs / stores the 16 payload bytes (16 lanes × 16 B contiguous per packet), and folds
+//    the block into its Horner accumulator A_l = A_l·H^16 ⊕ X.
+//  * After R rounds GHASH = Σ_l A_l·H^(16-l): lane l multiplies by H^(NLP - l mod NLP), the
+//    NLP-lane groups XOR-reduce, and a log-tree over the 16/NLP groups with multipliers
+//    H^NLP, H^2NLP, … finishes. The length block always lands on lane 15 of the last round; that
+//    lane also computes E_K(J0) for the tag.
+//  * AES: T-table pairs (T0[x], T2[x]) in LDS, one copy per lane of a 32-lane half (32 copies ×
+//    256 × 8 B = 64 KiB): every ds_read_b64 is bank-conflict-free and its address is one
+//    v_perm_b32; T1/T3 are one rotate of the XOR of two lookups (rotation distributes over XOR).
+//  * GHASH, one tunnel key (SINGLE): the Horner multiply by H^16 uses a "full" 4-bit table over all
+//    32 nibble positions (F_p[v] = v·x^4p·H^16, reduced): 32 conflict-free ds_read_b128 + XORs, no
+//    shifts, no reduction. The final per-lane multiply uses 4-bit Shoup tables M_k[v] = v·H^k with
+//    deferred reduction (NLP = 16). All tables are precomputed at key install and copied into LDS
+//    once per workgroup. Round keys are wave-uniform (scalar registers).
+//  * GHASH, mixed keys: each packet's round keys and Shoup tables for H, H^2, H^4, H^8, H^16
+//    (NLP = 2) are staged in the wave's LDS slice per packet group.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
 #include "layout.hpp"
-
-#ifndef NEB_WAVES_PER_WG
-#define NEB_WAVES_PER_WG 8
-#endif
 
 namespace neb {
 
@@ -71,85 +69,128 @@ constexpr T0Table make_t0() {
 __constant__ T0Table c_T0 = make_t0();
 
 // ------------------------------------------------------------------------------------------
-// LDS
+// Instruction helpers
 
-extern __shared__ __attribute__((aligned(16))) char g_lds[];
+// Three-input XOR in one VALU op. gfx950 has no v_xor3_b32; its v_bitop3_b32 evaluates any
+// 3-input truth table (0x96 = a ^ b ^ c), but hipcc does not form it from a ^ b ^ c chains.
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// same, third operand wave-uniform (a round key in an SGPR)
+__device__ __forceinline__ uint32_t x3s(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
+__device__ __forceinline__ uint4 x34(uint4 a, uint4 b, uint4 c) {
+    return make_uint4(x3(a.x, b.x, c.x), x3(a.y, b.y, c.y), x3(a.z, b.z, c.z), x3(a.w, b.w, c.w));
+}
+__device__ __forceinline__ uint4 bswap4(uint4 v) { return make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w)); }
+__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
+    return make_uint4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m), __shfl_xor(v.w, m));
+}
+// byte k of w, zero-extended (one VALU op)
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) {
+    return k == 0 ? (w & 0xFFu) : (k == 3 ? (w >> 24) : __builtin_amdgcn_ubfe(w, 8 * k, 8));
+}
 
-constexpr uint32_t kTTabBytes = 256 * 64 * 4;  // 64 KiB: entry x at x*256 + lane*4
-constexpr uint32_t kGhTabBytes = 256;          // one 4-bit GHASH table
-constexpr int kWavesPerWG = NEB_WAVES_PER_WG;
-constexpr int kThreads = kWavesPerWG * kWave;
-
-template <int NLP>
-struct GhCfg {
-    static constexpr int kLevels = NLP == 16 ? 0 : (NLP == 8 ? 1 : (NLP == 4 ? 2 : 3));
-    static constexpr int NT = NLP + kLevels;  // tables per key
-    static constexpr int kHorner = NT - 1;    // index of H^16
-    // power of table t
-    __host__ __device__ static constexpr int pw(int t) { return t < NLP ? t + 1 : (NLP << (t - NLP + 1)); }
-    // table index of H^s for s = NLP, 2NLP, ..., 8 (tree levels)
-    __host__ __device__ static constexpr int tree_tab(int s) {
-        return s == NLP ? NLP - 1 : NLP + (s == 2 * NLP ? 0 : (s == 4 * NLP ? 1 : 2));
-    }
-};
-
-// Multi-key wave slice: per packet [NT tables][round keys 240 B].
-constexpr int kMultiNLP = 2;
-constexpr uint32_t kMultiPktBytes = GhCfg<kMultiNLP>::NT * kGhTabBytes + 240;
-constexpr uint32_t kMultiWaveBytes = 4 * kMultiPktBytes;
-constexpr uint32_t kLdsSingle = kTTabBytes + GhCfg<16>::NT * kGhTabBytes;
-constexpr uint32_t kLdsMulti = kTTabBytes + kWavesPerWG * kMultiWaveBytes;
-static_assert(kLdsMulti <= 163840, "LDS budget");
-
-__device__ __forceinline__ uint32_t lds_u32(uint32_t addr) { return *reinterpret_cast<const uint32_t*>(g_lds + addr); }
-__device__ __forceinline__ uint4 lds_u128(uint32_t addr) { return *reinterpret_cast<const uint4*>(g_lds + addr); }
-__device__ __forceinline__ void lds_st128(uint32_t addr, uint4 v) { *reinterpret_cast<uint4*>(g_lds + addr) = v; }
+template <class T>
+__device__ __forceinline__ T lds_at(const void* base, uint32_t byte_off) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
 
 // ------------------------------------------------------------------------------------------
 // AES-256 encryption of one block per lane (little-endian column words in and out).
-
-// T0[byte k of s] — address = (byte << 8) | lane*4 built with one v_perm_b32.
-__device__ __forceinline__ uint32_t tlook(uint32_t s, uint32_t lb, int k) {
-    return lds_u32(perm(s, lb, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
+// ttab: LDS, 32 copies of 256 8-byte entries, entry x of copy c at byte x*256 + c*8 holding
+// (T0[x], T2[x]) for c < 16 and (T2[x], T0[x]) for c >= 16, T2 = rotl16(T0). Lane l uses copy
+// c = l mod 32 and reads single dwords: T0 at lb.x = 8c + 4(c >= 16), T2 at lb.y = 8c + 4(c < 16).
+// A ds_read_b32 banks on (addr/4) mod 32, so the 32 lanes of a half-wave hit dwords 2c + {0,1}
+// arranged to be 32 distinct banks: every lookup is conflict-free.
+__device__ __forceinline__ uint2 ttab_lane_base(uint32_t lane) {
+    const uint32_t c = lane & 31u, hi = c >> 4;
+    return make_uint2((c << 3) | (hi << 2), (c << 3) | ((hi ^ 1u) << 2));
+}
+__device__ __forceinline__ uint2 ttab_entry(uint32_t i) {  // i = x*32 + c
+    const uint32_t t = c_T0.t[i >> 5], t2 = __builtin_amdgcn_alignbit(t, t, 16);
+    return (i & 16u) ? make_uint2(t2, t) : make_uint2(t, t2);
 }
 
 struct RkRegs {  // wave-uniform round keys (scalar registers)
     const uint32_t* k;
+    static constexpr bool kUniform = true;
     __device__ __forceinline__ uint4 get(int r) const {
         return make_uint4(k[4 * r], k[4 * r + 1], k[4 * r + 2], k[4 * r + 3]);
     }
 };
 struct RkLds {  // per-packet round keys staged in LDS
-    uint32_t base;
-    __device__ __forceinline__ uint4 get(int r) const { return lds_u128(base + 16 * r); }
+    const uint4* base;
+    static constexpr bool kUniform = false;
+    __device__ __forceinline__ uint4 get(int r) const { return base[r]; }
 };
 
 template <class RK>
-__device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t lb,
-                                              const RK& rk) {
+__device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint2 lb,
+                                              const uint2* ttab, const RK& rk) {
+    // volatile keeps the 8-byte ds_read_b64 (bank = (addr/4) mod 64, conflict-free over the 32
+    // copies); a narrowed ds_read_b32 would bank mod 32 and conflict 2-way between copies c, c+16
+    // lookups are single dwords (ds_read_b32, bank = (addr/4) mod 32): T0 via lb0, T2 via lb2
+    auto T0 = [&](uint32_t s, int k) -> uint32_t {
+        return lds_at<uint32_t>(ttab, perm(s, lb.x, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
+    };
+    auto T2 = [&](uint32_t s, int k) -> uint32_t {
+        return lds_at<uint32_t>(ttab, perm(s, lb.y, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
+    };
     uint4 k = rk.get(0);
     s0 ^= k.x; s1 ^= k.y; s2 ^= k.z; s3 ^= k.w;
 #pragma unroll
     for (int r = 1; r < 14; r++) {
         k = rk.get(r);
-        uint32_t t0 = xor3(tlook(s0, lb, 0), rotr(tlook(s1, lb, 1), 24), rotr(tlook(s2, lb, 2), 16)) ^ rotr(tlook(s3, lb, 3), 8) ^ k.x;
-        uint32_t t1 = xor3(tlook(s1, lb, 0), rotr(tlook(s2, lb, 1), 24), rotr(tlook(s3, lb, 2), 16)) ^ rotr(tlook(s0, lb, 3), 8) ^ k.y;
-        uint32_t t2 = xor3(tlook(s2, lb, 0), rotr(tlook(s3, lb, 1), 24), rotr(tlook(s0, lb, 2), 16)) ^ rotr(tlook(s1, lb, 3), 8) ^ k.z;
-        uint32_t t3 = xor3(tlook(s3, lb, 0), rotr(tlook(s0, lb, 1), 24), rotr(tlook(s1, lb, 2), 16)) ^ rotr(tlook(s2, lb, 3), 8) ^ k.w;
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        const uint32_t a0 = T0(s0, 0), a1 = T0(s1, 1), a2 = T2(s2, 2), a3 = T2(s3, 3);
+        const uint32_t b0 = T0(s1, 0), b1 = T0(s2, 1), b2 = T2(s3, 2), b3 = T2(s0, 3);
+        const uint32_t c0 = T0(s2, 0), c1 = T0(s3, 1), c2 = T2(s0, 2), c3 = T2(s1, 3);
+        const uint32_t d0 = T0(s3, 0), d1 = T0(s0, 1), d2 = T2(s1, 2), d3 = T2(s2, 3);
+        // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k, T1 = rotl8 T0, T3 = rotl8 T2
+        if constexpr (RK::kUniform) {
+            s0 = x3s(a0, a2, k.x) ^ rotl8(a1 ^ a3);
+            s1 = x3s(b0, b2, k.y) ^ rotl8(b1 ^ b3);
+            s2 = x3s(c0, c2, k.z) ^ rotl8(c1 ^ c3);
+            s3 = x3s(d0, d2, k.w) ^ rotl8(d1 ^ d3);
+        } else {
+            s0 = x3(a0, a2, k.x) ^ rotl8(a1 ^ a3);
+            s1 = x3(b0, b2, k.y) ^ rotl8(b1 ^ b3);
+            s2 = x3(c0, c2, k.z) ^ rotl8(c1 ^ c3);
+            s3 = x3(d0, d2, k.w) ^ rotl8(d1 ^ d3);
+        }
     }
     k = rk.get(14);
     // last round: SubBytes+ShiftRows; S[x] is byte 1 of T0[x]
-    uint32_t o0 = xor3(perm(tlook(s1, lb, 1), tlook(s0, lb, 0), 0x0C0C0501u), perm(tlook(s3, lb, 3), tlook(s2, lb, 2), 0x05010C0Cu), k.x);
-    uint32_t o1 = xor3(perm(tlook(s2, lb, 1), tlook(s1, lb, 0), 0x0C0C0501u), perm(tlook(s0, lb, 3), tlook(s3, lb, 2), 0x05010C0Cu), k.y);
-    uint32_t o2 = xor3(perm(tlook(s3, lb, 1), tlook(s2, lb, 0), 0x0C0C0501u), perm(tlook(s1, lb, 3), tlook(s0, lb, 2), 0x05010C0Cu), k.z);
-    uint32_t o3 = xor3(perm(tlook(s0, lb, 1), tlook(s3, lb, 0), 0x0C0C0501u), perm(tlook(s2, lb, 3), tlook(s1, lb, 2), 0x05010C0Cu), k.w);
-    return make_uint4(o0, o1, o2, o3);
+    const uint32_t a0 = T0(s0, 0), a1 = T0(s1, 1), a2 = T0(s2, 2), a3 = T0(s3, 3);
+    const uint32_t b0 = T0(s1, 0), b1 = T0(s2, 1), b2 = T0(s3, 2), b3 = T0(s0, 3);
+    const uint32_t c0 = T0(s2, 0), c1 = T0(s3, 1), c2 = T0(s0, 2), c3 = T0(s1, 3);
+    const uint32_t d0 = T0(s3, 0), d1 = T0(s0, 1), d2 = T0(s1, 2), d3 = T0(s2, 3);
+    uint4 o;
+    if constexpr (RK::kUniform) {
+        o.x = x3s(perm(a1, a0, 0x0C0C0501u), perm(a3, a2, 0x05010C0Cu), k.x);
+        o.y = x3s(perm(b1, b0, 0x0C0C0501u), perm(b3, b2, 0x05010C0Cu), k.y);
+        o.z = x3s(perm(c1, c0, 0x0C0C0501u), perm(c3, c2, 0x05010C0Cu), k.z);
+        o.w = x3s(perm(d1, d0, 0x0C0C0501u), perm(d3, d2, 0x05010C0Cu), k.w);
+    } else {
+        o.x = x3(perm(a1, a0, 0x0C0C0501u), perm(a3, a2, 0x05010C0Cu), k.x);
+        o.y = x3(perm(b1, b0, 0x0C0C0501u), perm(b3, b2, 0x05010C0Cu), k.y);
+        o.z = x3(perm(c1, c0, 0x0C0C0501u), perm(c3, c2, 0x05010C0Cu), k.z);
+        o.w = x3(perm(d1, d0, 0x0C0C0501u), perm(d3, d2, 0x05010C0Cu), k.w);
+    }
+    return o;
 }
 
 // ------------------------------------------------------------------------------------------
 // GF(2^128), GCM bit order. An element is 4 big-endian words w0..w3; the coefficient of x^j is
 // bit 31 - (j mod 32) of w[j / 32], so multiplying by x is a 128-bit logical right shift.
+// Nibble p (p = 8q + r, 0..31) of x = bits 28-4r..31-4r of w[q]; its value v has MSB = x^(4p).
 
 __device__ __forceinline__ uint4 gf_mulx(uint4 v) {
     uint32_t lsb = v.w & 1u;
@@ -164,30 +205,63 @@ __device__ __forceinline__ uint4 gf_mulx(uint4 v) {
 // 256-bit product z[0..7] (x^0..x^255) -> 128-bit, modulo x^128 + x^7 + x^2 + x + 1.
 __device__ __forceinline__ uint4 gf_reduce(const uint32_t z[8]) {
     const uint32_t l0 = z[4], l1 = z[5], l2 = z[6], l3 = z[7];
-    // L·(1 + x + x^2 + x^7) with the shifted-out bits (x^128..x^134) collected in o
-    uint32_t t0 = l0 ^ (l0 >> 1) ^ (l0 >> 2) ^ (l0 >> 7);
-    uint32_t t1 = xor3(l1, shr64(l0, l1, 1), shr64(l0, l1, 2)) ^ shr64(l0, l1, 7);
-    uint32_t t2 = xor3(l2, shr64(l1, l2, 1), shr64(l1, l2, 2)) ^ shr64(l1, l2, 7);
-    uint32_t t3 = xor3(l3, shr64(l2, l3, 1), shr64(l2, l3, 2)) ^ shr64(l2, l3, 7);
-    uint32_t o = xor3(l3 << 31, l3 << 30, l3 << 25);
-    uint32_t of = xor3(o, o >> 1, o >> 2) ^ (o >> 7);
-    return make_uint4(xor3(z[0], t0, of), z[1] ^ t1, z[2] ^ t2, z[3] ^ t3);
+    // L·(1 + x + x^2 + x^7), the bits shifted out (x^128..x^134) collected in o
+    uint32_t t0 = x3(l0, l0 >> 1, l0 >> 2) ^ (l0 >> 7);
+    uint32_t t1 = x3(x3(l1, shr64(l0, l1, 1), shr64(l0, l1, 2)), shr64(l0, l1, 7), z[1]);
+    uint32_t t2 = x3(x3(l2, shr64(l1, l2, 1), shr64(l1, l2, 2)), shr64(l1, l2, 7), z[2]);
+    uint32_t t3 = x3(x3(l3, shr64(l2, l3, 1), shr64(l2, l3, 2)), shr64(l2, l3, 7), z[3]);
+    uint32_t o = x3(l3 << 31, l3 << 30, l3 << 25);
+    uint32_t of = x3(o, o >> 1, o >> 2) ^ (o >> 7);
+    return make_uint4(x3(z[0], t0, of), t1, t2, t3);
 }
 
-// x · H^k where `tab` is the LDS byte address of M[v] = v·H^k (v's MSB = coefficient x^0).
-// 32 independent 16-B lookups; partial products grouped by shift residue and reduced once.
-__device__ __forceinline__ uint4 gf_mul_tab(uint4 x, uint32_t tab) {
+// x · F where ftab (LDS) is a full table F_p[v] at byte p*256 + v*16; acc is XORed in.
+__device__ __forceinline__ uint4 gf_mul_full(uint4 x, uint4 acc, const uint4* ftab) {
     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t hi = xw[q] & 0xF0F0F0F0u;          // bytes k: nibble r = 6-2k, << 4
+        const uint32_t lo = (xw[q] << 4) & 0xF0F0F0F0u;   // bytes k: nibble r = 7-2k, << 4
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 e1 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 6 - 2 * k) * 256u + byte_of(hi, k));
+            const uint4 e2 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 7 - 2 * k) * 256u + byte_of(lo, k));
+            acc = x34(acc, e1, e2);
+        }
+    }
+    return acc;
+}
+
+// x · H^k where `tab` is the LDS byte offset (multiple of 256, < 2^24, relative to `base`) of a
+// Shoup table M[v] = v·H^k. 32 independent lookups grouped by shift residue, reduced once.
+__device__ __forceinline__ uint4 gf_mul_shoup(uint4 x, uint32_t tab, const uint4* base) {
+    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        hi[q] = xw[q] & 0xF0F0F0F0u;
+        lo[q] = (xw[q] << 4) & 0xF0F0F0F0u;
+    }
     uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        uint32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
+        // nibble r of every word: byte (3 - r/2) of hi (even r) or lo (odd r)
+        const int k = 3 - (r >> 1);
+        uint4 m[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            uint32_t v = (xw[q] >> (28 - 4 * r)) & 15u;
-            uint4 m = lds_u128(tab + (v << 4));
-            a[q] ^= m.x; a[q + 1] ^= m.y; a[q + 2] ^= m.z; a[q + 3] ^= m.w;
+            const uint32_t src = (r & 1) ? lo[q] : hi[q];
+            // address = tab | (nibble << 4): byte k of src into byte 0, tab's bytes 1..3 kept
+            m[q] = lds_at<uint4>(base, perm(src, tab, 0x03020100u | (uint32_t)(4 + k)));
         }
+        uint32_t a[7];
+        a[0] = m[0].x;
+        a[1] = m[0].y ^ m[1].x;
+        a[2] = x3(m[0].z, m[1].y, m[2].x);
+        a[3] = x3(m[0].w, m[1].z, m[2].y) ^ m[3].x;
+        a[4] = x3(m[1].w, m[2].z, m[3].y);
+        a[5] = m[2].w ^ m[3].z;
+        a[6] = m[3].w;
         if (r == 0) {
 #pragma unroll
             for (int i = 0; i < 7; i++) z[i] ^= a[i];
@@ -198,13 +272,12 @@ __device__ __forceinline__ uint4 gf_mul_tab(uint4 x, uint32_t tab) {
             for (int i = 1; i < 7; i++) z[i] ^= shr64(a[i - 1], a[i], sh);
             z[7] ^= a[6] << (32 - sh);
         }
-        // keep at most one residue's 4 lookups (16 VGPRs) in flight per wave
-        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);  // at most one residue's lookups in flight
     }
     return gf_reduce(z);
 }
 
-// Entry e (0..15) of the 4-bit table of P: XOR of P·x^j for the set bits (bit 3 ↔ x^0).
+// Entry e (0..15) of the 4-bit Shoup table of P: XOR of P·x^j for the set bits (bit 3 ↔ x^0).
 __device__ __forceinline__ uint4 gf_tab_entry(uint4 p, uint32_t e) {
     uint4 p1 = gf_mulx(p), p2 = gf_mulx(p1), p3 = gf_mulx(p2);
     uint32_t m8 = (e & 8) ? ~0u : 0u, m4 = (e & 4) ? ~0u : 0u, m2 = (e & 2) ? ~0u : 0u, m1 = (e & 1) ? ~0u : 0u;
@@ -216,18 +289,12 @@ __device__ __forceinline__ uint4 gf_tab_entry(uint4 p, uint32_t e) {
     return r;
 }
 
-__device__ __forceinline__ uint4 bswap4(uint4 v) { return make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w)); }
-__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
-__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
-    return make_uint4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m), __shfl_xor(v.w, m));
-}
-__device__ __forceinline__ uint32_t ld_rec(const uint32_t* rec, uint32_t i) { return rec[i]; }
 __device__ __forceinline__ uint4 ld_rec4(const uint32_t* rec, uint32_t i) {
     return *reinterpret_cast<const uint4*>(rec + i);
 }
 
 // ------------------------------------------------------------------------------------------
-// The batch kernel.
+// Per-packet work shared by both kernels
 
 struct GcmArgs {
     const neb_desc* desc;
@@ -239,223 +306,326 @@ struct GcmArgs {
     int32_t* status;
 };
 
-template <bool OPEN, bool SINGLE>
-__global__ __launch_bounds__(kThreads) void gcm_batch_kernel(GcmArgs args) {
-    constexpr int NLP = SINGLE ? 16 : kMultiNLP;
-    using G = GhCfg<NLP>;
+struct PktShape {
+    uint32_t na, m, n, R, pad;
+};
+
+__device__ __forceinline__ PktShape pkt_shape(const neb_desc& d, bool run) {
+    PktShape s;
+    s.na = (d.aad_len + 15u) >> 4;
+    s.m = (d.len + 15u) >> 4;
+    s.n = s.na + s.m + 1u;
+    s.R = run ? (s.n + 15u) >> 4 : 0u;
+    s.pad = 16u * s.R - s.n;
+    return s;
+}
+
+// One round of one packet lane: keystream, payload XOR, GHASH input block. Returns X (BE words).
+template <bool OPEN, class RK>
+__device__ __forceinline__ uint4 gcm_lane_round(const neb_desc& d, const PktShape& sh, uint32_t r, uint32_t l,
+                                                uint32_t c1, uint32_t c2, uint2 lb8, const uint2* ttab,
+                                                const RK& rk, uint8_t* arena, uint4& ej0) {
+    const int32_t g = (int32_t)(16u * r + l + 1u) - (int32_t)sh.pad;  // 1-based GHASH index
+    const bool is_aad = g >= 1 && g <= (int32_t)sh.na;
+    const bool is_ct = g > (int32_t)sh.na && g <= (int32_t)(sh.na + sh.m);
+    const bool is_len = g == (int32_t)sh.n;
+    const uint32_t k = (uint32_t)(g - (int32_t)sh.na);  // ciphertext block index (1-based)
+    const uint32_t ctr = is_ct ? k + 1u : 1u;
+    const uint4 ks = aes256_block(0u, c1, c2, bswap32(ctr), lb8, ttab, rk);
+    uint4 X = make_uint4(0, 0, 0, 0);
+    if (is_aad) {
+        const uint32_t off = 16u * (uint32_t)(g - 1);
+        X = bswap4(load_block(arena + d.aad_off + off, min(16u, d.aad_len - off)));
+    }
+    if (is_ct) {
+        const uint32_t off = 16u * (k - 1u);
+        const uint32_t nb = min(16u, d.len - off);
+        const uint4 in = load_block(arena + d.src_off + off, nb);
+        const uint4 out = xor4(in, mask_block(ks, nb));
+        store_block(arena + d.dst_off + off, out, nb);
+        X = bswap4(OPEN ? in : out);
+    }
+    if (is_len) {
+        const uint64_t abits = (uint64_t)d.aad_len * 8u, cbits = (uint64_t)d.len * 8u;
+        X = make_uint4((uint32_t)(abits >> 32), (uint32_t)abits, (uint32_t)(cbits >> 32), (uint32_t)cbits);
+        ej0 = ks;
+    }
+    return X;
+}
+
+// Tag finish on lane 15 (seal: store; open: compare, zero the payload on mismatch).
+template <bool OPEN>
+__device__ __forceinline__ uint32_t gcm_finish(const neb_desc& d, uint4 S, uint4 ej0, uint32_t lane, uint32_t l,
+                                               uint8_t* arena) {
+    const uint4 tag = xor4(ej0, bswap4(S));  // valid on lane 15
+    uint32_t fail = 0;
+    if (l == 15u) {
+        if constexpr (!OPEN) {
+            store_block(arena + d.dst_off + d.len, tag, 16);
+        } else {
+            const uint4 rt = load_block(arena + d.src_off + d.len, 16);
+            const uint4 df = xor4(rt, tag);
+            fail = (df.x | df.y | df.z | df.w) != 0u;
+        }
+    }
+    if constexpr (OPEN) {
+        fail = (uint32_t)__shfl((int)fail, (int)(lane | 15u));
+        if (fail) {
+            for (uint32_t off = 16u * l; off < d.len; off += 256u)
+                store_block(arena + d.dst_off + off, make_uint4(0, 0, 0, 0), min(16u, d.len - off));
+        }
+    }
+    return fail;
+}
+
+// ------------------------------------------------------------------------------------------
+// One tunnel key for the whole batch.
+
+constexpr int kSingleWaves = 8;
+constexpr int kSingleThreads = kSingleWaves * kWave;
+
+struct SingleLds {
+    uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^16 (first: its offsets fit the ds_read offset field)
+    uint4 shoup[16 * 16];    // 4 KiB  M_k[v] for H^1..H^16 (table k-1 at byte (k-1)*256)
+    uint2 ttab[256 * 32];    // 64 KiB (T0, T2) pairs, 32 copies
+};
+
+template <bool OPEN>
+__global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs args) {
+    __shared__ SingleLds lds;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    const uint32_t q = lane >> 4;   // packet slot in the wave
-    const uint32_t l = lane & 15u;  // lane within the packet
-    const uint32_t lb = lane << 2;  // T-table lane column
-
-    // T-table: 64 copies, entry x at x*256 + lane*4
-    for (uint32_t i = tid; i < 256u * 64u; i += kThreads)
-        reinterpret_cast<uint32_t*>(g_lds)[i] = c_T0.t[i >> 6];
+    const uint32_t q = lane >> 4;
+    const uint32_t l = lane & 15u;
+    const uint2 lb8 = ttab_lane_base(lane);
 
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
+    for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
+    for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull16 + 4u * i);
+    for (uint32_t i = tid; i < 16u * 16u; i += kSingleThreads) lds.shoup[i] = ld_rec4(srec, kRecShoup + 4u * i);
     uint32_t rks[60];
-    if constexpr (SINGLE) {
-        // one key for the whole batch: tables H^1..H^16 once per workgroup, round keys uniform
-        if (tid < 16u * 16u) {
-            uint32_t t = tid >> 4, e = tid & 15u;
-            uint4 p = ld_rec4(srec, kRecHPow + 4 * t);
-            lds_st128(kTTabBytes + t * kGhTabBytes + e * 16u, gf_tab_entry(p, e));
-        }
 #pragma unroll
-        for (int i = 0; i < 60; i++) rks[i] = __builtin_amdgcn_readfirstlane(ld_rec(srec, kRecRoundKeys + i));
-    }
+    for (int i = 0; i < 60; i++) rks[i] = __builtin_amdgcn_readfirstlane(srec[kRecRoundKeys + i]);
     __syncthreads();
+    const RkRegs rk{rks};
 
     const uint32_t ngroups = (args.npkt + 3u) >> 2;
-    const uint32_t wslice = kTTabBytes + wave * kMultiWaveBytes + q * kMultiPktBytes;  // MIXED only
-    const uint32_t tabbase = SINGLE ? kTTabBytes : wslice;
-    const uint32_t rkbase = wslice + G::NT * kGhTabBytes;
+    for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
+        const uint32_t p = grp * 4u + q;
+        const bool valid = p < args.npkt;
+        neb_desc d = {};
+        if (valid) d = args.desc[p];
+        uint32_t st = NEB_STATUS_OK;
+        if (d.key_id != args.key_hint) st = NEB_STATUS_BAD_KEY;
+        if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
+        const bool run = valid && st == NEB_STATUS_OK;
+        const PktShape sh = pkt_shape(d, run);
+        uint32_t Rmax = sh.R;
+        Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 16));
+        Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 32));
 
-    for (uint32_t grp = blockIdx.x * kWavesPerWG + wave; grp < ngroups; grp += gridDim.x * kWavesPerWG) {
+        // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
+        const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
+        const uint32_t c2 = bswap32((uint32_t)d.counter);
+        uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
+        for (uint32_t r = 0; r < Rmax; r++) {
+            if (r < sh.R) {
+                const uint4 X = gcm_lane_round<OPEN>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
+                A = (r == 0) ? X : gf_mul_full(A, X, lds.full);
+            }
+        }
+        if (run) {
+            // Σ_l A_l·H^(16-l): lane l's own power from the Shoup tables, then XOR over the 16 lanes
+            uint4 V = gf_mul_shoup(A, (15u - l) * 256u, lds.shoup);
+#pragma unroll
+            for (int s = 1; s < 16; s <<= 1) V = xor4(V, shfl_xor4(V, s));
+            if (gcm_finish<OPEN>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
+        }
+        if (valid && l == 15u) args.status[p] = (int32_t)st;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Mixed keys: per-packet key material staged in the wave's LDS slice.
+
+constexpr int kMultiWaves = 12;
+constexpr int kMultiThreads = kMultiWaves * kWave;
+constexpr int kMultiNT = 5;  // tables per packet: H, H^2, H^4, H^8, H^16 (lane powers H, H^2; tree H^2, H^4, H^8)
+__host__ __device__ constexpr int multi_pow(int t) { return t < 2 ? t + 1 : (2 << (t - 1)); }
+
+struct MultiPkt {
+    uint4 shoup[kMultiNT * 16];  // 1280 B (256-B aligned tables)
+    uint4 rk[16];                // 240 B used (15 round keys), padded to 256
+};
+struct MultiLds {
+    MultiPkt pkt[kMultiWaves][4];  // 96 KiB
+    uint2 ttab[256 * 32];          // 64 KiB
+};
+static_assert(sizeof(MultiLds) <= 163840, "LDS budget");
+
+template <bool OPEN>
+__global__ __launch_bounds__(kMultiThreads, 3) void gcm_multi_kernel(GcmArgs args) {
+    __shared__ MultiLds lds;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = tid >> 6;
+    const uint32_t q = lane >> 4;
+    const uint32_t l = lane & 15u;
+    const uint2 lb8 = ttab_lane_base(lane);
+
+    for (uint32_t i = tid; i < 256u * 32u; i += kMultiThreads) lds.ttab[i] = ttab_entry(i);
+    __syncthreads();
+    MultiPkt& mp = lds.pkt[wave][q];
+    const uint4* pbase = lds.pkt[0][0].shoup;
+    const uint32_t tabs = (uint32_t)((const char*)mp.shoup - (const char*)pbase);  // multiple of 256
+    const RkLds rk{mp.rk};
+
+    const uint32_t ngroups = (args.npkt + 3u) >> 2;
+    for (uint32_t grp = blockIdx.x * kMultiWaves + wave; grp < ngroups; grp += gridDim.x * kMultiWaves) {
         const uint32_t p = grp * 4u + q;
         const bool valid = p < args.npkt;
         neb_desc d = {};
         if (valid) d = args.desc[p];
         const uint32_t* rec = args.keys + (size_t)d.key_id * kKeyRecDwords;
         uint32_t st = NEB_STATUS_OK;
-        if (SINGLE) {
-            if (d.key_id != args.key_hint) st = NEB_STATUS_BAD_KEY;
-        } else {
-            if (d.key_id >= args.max_keys || ld_rec(rec, kRecAlg) != NEB_ALG_AESGCM) st = NEB_STATUS_BAD_KEY;
-        }
+        if (d.key_id >= args.max_keys || rec[kRecAlg] != NEB_ALG_AESGCM) st = NEB_STATUS_BAD_KEY;
         if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
         const bool run = valid && st == NEB_STATUS_OK;
-
-        const uint32_t na = (d.aad_len + 15u) >> 4;
-        const uint32_t m = (d.len + 15u) >> 4;
-        const uint32_t n = na + m + 1u;
-        const uint32_t R = run ? (n + 15u) >> 4 : 0u;
-        const uint32_t pad = 16u * R - n;
-        uint32_t Rmax = R;
+        const PktShape sh = pkt_shape(d, run);
+        uint32_t Rmax = sh.R;
         Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 16));
         Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 32));
 
-        if constexpr (!SINGLE) {
-            // stage this packet's round keys and GHASH tables in the wave's LDS slice
-            if (run) {
-                if (l < 15u) lds_st128(rkbase + 16u * l, ld_rec4(rec, kRecRoundKeys + 4u * l));
+        if (run) {  // stage round keys and the 5 Shoup tables of this packet's key
+            if (l < 15u) mp.rk[l] = ld_rec4(rec, kRecRoundKeys + 4u * l);
 #pragma unroll
-                for (int t = 0; t < G::NT; t++) {
-                    uint4 pw = ld_rec4(rec, kRecHPow + 4u * (uint32_t)(G::pw(t) - 1));
-                    lds_st128(tabbase + (uint32_t)t * kGhTabBytes + 16u * l, gf_tab_entry(pw, l));
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int t = 0; t < kMultiNT; t++)
+                mp.shoup[16 * t + l] = ld_rec4(rec, kRecShoup + 64u * (uint32_t)(multi_pow(t) - 1) + 4u * l);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
         const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
         const uint32_t c2 = bswap32((uint32_t)d.counter);
-        uint8_t* arena = args.arena;
-
-        uint4 A = make_uint4(0, 0, 0, 0);
-        uint4 ej0 = make_uint4(0, 0, 0, 0);
+        uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
         for (uint32_t r = 0; r < Rmax; r++) {
-            if (r < R) {
-                const int32_t g = (int32_t)(16u * r + l + 1u) - (int32_t)pad;  // 1-based GHASH index
-                const bool is_aad = g >= 1 && g <= (int32_t)na;
-                const bool is_ct = g > (int32_t)na && g <= (int32_t)(na + m);
-                const bool is_len = g == (int32_t)n;
-                const uint32_t k = (uint32_t)(g - (int32_t)na);  // ciphertext block index (1-based)
-                const uint32_t ctr = is_ct ? k + 1u : 1u;
-                uint4 ks;
-                if constexpr (SINGLE) ks = aes256_block(0u, c1, c2, bswap32(ctr), lb, RkRegs{rks});
-                else ks = aes256_block(0u, c1, c2, bswap32(ctr), lb, RkLds{rkbase});
-                uint4 X = make_uint4(0, 0, 0, 0);
-                if (is_aad) {
-                    uint32_t off = 16u * (uint32_t)(g - 1);
-                    X = bswap4(load_block(arena + d.aad_off + off, min(16u, d.aad_len - off)));
-                }
-                if (is_ct) {
-                    uint32_t off = 16u * (k - 1u);
-                    uint32_t nb = min(16u, d.len - off);
-                    uint4 in = load_block(arena + d.src_off + off, nb);
-                    uint4 out = xor4(in, mask_block(ks, nb));
-                    store_block(arena + d.dst_off + off, out, nb);
-                    X = bswap4(OPEN ? in : out);
-                }
-                if (is_len) {
-                    uint64_t abits = (uint64_t)d.aad_len * 8u, cbits = (uint64_t)d.len * 8u;
-                    X = make_uint4((uint32_t)(abits >> 32), (uint32_t)abits, (uint32_t)(cbits >> 32), (uint32_t)cbits);
-                    ej0 = ks;
-                }
-                A = (r == 0) ? X : xor4(gf_mul_tab(A, tabbase + G::kHorner * kGhTabBytes), X);
+            if (r < sh.R) {
+                const uint4 X = gcm_lane_round<OPEN>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
+                A = (r == 0) ? X : xor4(gf_mul_shoup(A, tabs + 4u * 256u, pbase), X);
             }
         }
-
         if (run) {
-            // Σ_l A_l·H^(16-l): per-lane powers inside NLP-lane groups, then a tree over the groups
-            uint4 V = gf_mul_tab(A, tabbase + (uint32_t)(NLP - 1 - (int)(l % NLP)) * kGhTabBytes);
+            // lane powers H^(2 - l mod 2), pair XOR, then tree levels H^2, H^4, H^8
+            uint4 V = gf_mul_shoup(A, tabs + (1u - (l & 1u)) * 256u, pbase);
+            V = xor4(V, shfl_xor4(V, 1));
 #pragma unroll
-            for (int s = 1; s < NLP; s <<= 1) V = xor4(V, shfl_xor4(V, s));
-#pragma unroll
-            for (int s = NLP; s < 16; s <<= 1) {
-                uint4 mv = gf_mul_tab(V, tabbase + (uint32_t)G::tree_tab(s) * kGhTabBytes);
-                uint4 pv = shfl_xor4(V, s), pm = shfl_xor4(mv, s);
+            for (int s = 2, t = 1; s < 16; s <<= 1, t++) {
+                const uint4 mv = gf_mul_shoup(V, tabs + (uint32_t)t * 256u, pbase);
+                const uint4 pv = shfl_xor4(V, s), pm = shfl_xor4(mv, s);
                 V = ((l / (uint32_t)s) & 1u) ? xor4(pm, V) : xor4(mv, pv);
             }
-            uint4 tag = xor4(ej0, bswap4(V));  // valid on lane 15
-            uint32_t fail = 0;
-            if (l == 15u) {
-                if constexpr (!OPEN) {
-                    store_block(arena + d.dst_off + d.len, tag, 16);
-                } else {
-                    uint4 rt = load_block(arena + d.src_off + d.len, 16);
-                    uint4 df = xor4(rt, tag);
-                    fail = (df.x | df.y | df.z | df.w) != 0u;
-                }
-            }
-            if constexpr (OPEN) {
-                fail = (uint32_t)__shfl((int)fail, (int)(lane | 15u));
-                if (fail) {
-                    for (uint32_t off = 16u * l; off < d.len; off += 256u)
-                        store_block(arena + d.dst_off + off, make_uint4(0, 0, 0, 0), min(16u, d.len - off));
-                }
-                if (fail) st = NEB_STATUS_AUTH_FAILED;
-            }
+            if (gcm_finish<OPEN>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
         }
         if (valid && l == 15u) args.status[p] = (int32_t)st;
-        if constexpr (!SINGLE) {
-            // the next group overwrites this wave's LDS slice
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // slice is rewritten next group
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
 // ------------------------------------------------------------------------------------------
-// Key install: AES-256 key expansion, H = E_K(0), H^1..H^16. One lane; runs once per tunnel key.
+// Key install: AES-256 key expansion, H = E_K(0), H^1..H^16, and the GHASH tables.
+// Runs once per tunnel key (one workgroup of 256 lanes).
 
 __device__ uint8_t sbox_b(uint32_t x) { return (uint8_t)(c_T0.t[x & 255u] >> 8); }
 __device__ uint8_t xtime_d(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
 
-__global__ void gcm_key_setup_kernel(const uint8_t* __restrict__ key, uint32_t* __restrict__ rec) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint8_t rk[240];
-    for (int i = 0; i < 32; i++) rk[i] = key[i];
-    uint8_t rcon = 1;
-    for (int i = 8; i < 60; i++) {
-        uint8_t t0 = rk[4 * i - 4], t1 = rk[4 * i - 3], t2 = rk[4 * i - 2], t3 = rk[4 * i - 1];
-        if (i % 8 == 0) {
-            uint8_t u = t0;
-            t0 = sbox_b(t1) ^ rcon; t1 = sbox_b(t2); t2 = sbox_b(t3); t3 = sbox_b(u);
-            rcon = xtime_d(rcon);
-        } else if (i % 8 == 4) {
-            t0 = sbox_b(t0); t1 = sbox_b(t1); t2 = sbox_b(t2); t3 = sbox_b(t3);
-        }
-        rk[4 * i] = rk[4 * i - 32] ^ t0; rk[4 * i + 1] = rk[4 * i - 31] ^ t1;
-        rk[4 * i + 2] = rk[4 * i - 30] ^ t2; rk[4 * i + 3] = rk[4 * i - 29] ^ t3;
-    }
-    for (int i = 0; i < 60; i++)
-        rec[kRecRoundKeys + i] = (uint32_t)rk[4 * i] | (uint32_t)rk[4 * i + 1] << 8 | (uint32_t)rk[4 * i + 2] << 16 |
-                                 (uint32_t)rk[4 * i + 3] << 24;
-    // H = E_K(0^128), byte-oriented FIPS-197 cipher
-    uint8_t s[16];
-    for (int i = 0; i < 16; i++) s[i] = rk[i];
-    for (int r = 1; r <= 14; r++) {
-        uint8_t t[16];
-        for (int c = 0; c < 4; c++)
-            for (int j = 0; j < 4; j++) t[4 * c + j] = sbox_b(s[4 * ((c + j) & 3) + j]);
-        if (r != 14) {
-            for (int c = 0; c < 4; c++) {
-                uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
-                uint8_t x = a0 ^ a1 ^ a2 ^ a3;
-                t[4 * c] = a0 ^ x ^ xtime_d(a0 ^ a1);
-                t[4 * c + 1] = a1 ^ x ^ xtime_d(a1 ^ a2);
-                t[4 * c + 2] = a2 ^ x ^ xtime_d(a2 ^ a3);
-                t[4 * c + 3] = a3 ^ x ^ xtime_d(a3 ^ a0);
+__global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __restrict__ key, uint32_t* __restrict__ rec) {
+    __shared__ uint4 hp[16];      // H^1..H^16
+    __shared__ uint4 basis[128];  // x^i · H^16
+    if (threadIdx.x == 0) {
+        uint8_t rk[240];
+        for (int i = 0; i < 32; i++) rk[i] = key[i];
+        uint8_t rcon = 1;
+        for (int i = 8; i < 60; i++) {
+            uint8_t t0 = rk[4 * i - 4], t1 = rk[4 * i - 3], t2 = rk[4 * i - 2], t3 = rk[4 * i - 1];
+            if (i % 8 == 0) {
+                uint8_t u = t0;
+                t0 = sbox_b(t1) ^ rcon; t1 = sbox_b(t2); t2 = sbox_b(t3); t3 = sbox_b(u);
+                rcon = xtime_d(rcon);
+            } else if (i % 8 == 4) {
+                t0 = sbox_b(t0); t1 = sbox_b(t1); t2 = sbox_b(t2); t3 = sbox_b(t3);
             }
+            rk[4 * i] = rk[4 * i - 32] ^ t0; rk[4 * i + 1] = rk[4 * i - 31] ^ t1;
+            rk[4 * i + 2] = rk[4 * i - 30] ^ t2; rk[4 * i + 3] = rk[4 * i - 29] ^ t3;
         }
-        for (int i = 0; i < 16; i++) s[i] = t[i] ^ rk[16 * r + i];
-    }
-    uint32_t h[4];
-    for (int i = 0; i < 4; i++)
-        h[i] = (uint32_t)s[4 * i] << 24 | (uint32_t)s[4 * i + 1] << 16 | (uint32_t)s[4 * i + 2] << 8 | s[4 * i + 3];
-    // powers by bit-serial multiply (SP 800-38D Algorithm 1)
-    uint32_t pw[4] = {h[0], h[1], h[2], h[3]};
-    for (int k = 0; k < (int)kNumHPow; k++) {
-        for (int i = 0; i < 4; i++) rec[kRecHPow + 4 * k + i] = pw[i];
-        uint32_t z[4] = {0, 0, 0, 0}, v[4] = {h[0], h[1], h[2], h[3]};
-        for (int b = 0; b < 128; b++) {
-            if ((pw[b >> 5] >> (31 - (b & 31))) & 1u)
-                for (int i = 0; i < 4; i++) z[i] ^= v[i];
-            uint32_t lsb = v[3] & 1u;
-            v[3] = (v[3] >> 1) | (v[2] << 31); v[2] = (v[2] >> 1) | (v[1] << 31);
-            v[1] = (v[1] >> 1) | (v[0] << 31); v[0] = (v[0] >> 1) ^ (lsb ? 0xE1000000u : 0u);
+        for (int i = 0; i < 60; i++)
+            rec[kRecRoundKeys + i] = (uint32_t)rk[4 * i] | (uint32_t)rk[4 * i + 1] << 8 |
+                                     (uint32_t)rk[4 * i + 2] << 16 | (uint32_t)rk[4 * i + 3] << 24;
+        // H = E_K(0^128), byte-oriented FIPS-197 cipher
+        uint8_t s[16];
+        for (int i = 0; i < 16; i++) s[i] = rk[i];
+        for (int r = 1; r <= 14; r++) {
+            uint8_t t[16];
+            for (int c = 0; c < 4; c++)
+                for (int j = 0; j < 4; j++) t[4 * c + j] = sbox_b(s[4 * ((c + j) & 3) + j]);
+            if (r != 14) {
+                for (int c = 0; c < 4; c++) {
+                    uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+                    uint8_t x = a0 ^ a1 ^ a2 ^ a3;
+                    t[4 * c] = a0 ^ x ^ xtime_d(a0 ^ a1);
+                    t[4 * c + 1] = a1 ^ x ^ xtime_d(a1 ^ a2);
+                    t[4 * c + 2] = a2 ^ x ^ xtime_d(a2 ^ a3);
+                    t[4 * c + 3] = a3 ^ x ^ xtime_d(a3 ^ a0);
+                }
+            }
+            for (int i = 0; i < 16; i++) s[i] = t[i] ^ rk[16 * r + i];
         }
-        for (int i = 0; i < 4; i++) pw[i] = z[i];
+        uint32_t h[4];
+        for (int i = 0; i < 4; i++)
+            h[i] = (uint32_t)s[4 * i] << 24 | (uint32_t)s[4 * i + 1] << 16 | (uint32_t)s[4 * i + 2] << 8 | s[4 * i + 3];
+        // powers by bit-serial multiply (SP 800-38D Algorithm 1)
+        uint32_t pw[4] = {h[0], h[1], h[2], h[3]};
+        for (int k = 0; k < (int)kNumHPow; k++) {
+            hp[k] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+            for (int i = 0; i < 4; i++) rec[kRecHPow + 4 * k + i] = pw[i];
+            uint32_t z[4] = {0, 0, 0, 0}, v[4] = {h[0], h[1], h[2], h[3]};
+            for (int b = 0; b < 128; b++) {
+                if ((pw[b >> 5] >> (31 - (b & 31))) & 1u)
+                    for (int i = 0; i < 4; i++) z[i] ^= v[i];
+                uint32_t lsb = v[3] & 1u;
+                v[3] = (v[3] >> 1) | (v[2] << 31); v[2] = (v[2] >> 1) | (v[1] << 31);
+                v[1] = (v[1] >> 1) | (v[0] << 31); v[0] = (v[0] >> 1) ^ (lsb ? 0xE1000000u : 0u);
+            }
+            for (int i = 0; i < 4; i++) pw[i] = z[i];
+        }
+        uint4 b = hp[15];
+        for (int i = 0; i < 128; i++) {
+            basis[i] = b;
+            b = gf_mulx(b);
+        }
+        rec[kRecAlg] = NEB_ALG_AESGCM;
     }
-    rec[kRecAlg] = NEB_ALG_AESGCM;
+    __syncthreads();
+    const uint32_t t = threadIdx.x;
+    // Shoup tables: entry (k, v) for k = 1..16
+    {
+        const uint32_t k = t >> 4, v = t & 15u;
+        const uint4 e = gf_tab_entry(hp[k], v);
+        uint32_t* o = rec + kRecShoup + 64u * k + 4u * v;
+        o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
+    }
+    // full table of H^16: F_p[v] = XOR of basis[4p + j] for the set bits of v (bit 3 ↔ j = 0)
+    for (uint32_t i = t; i < 512u; i += 256u) {
+        const uint32_t p = i >> 4, v = i & 15u;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        for (uint32_t j = 0; j < 4; j++)
+            if ((v >> (3 - j)) & 1u) e = xor4(e, basis[4 * p + j]);
+        uint32_t* o = rec + kRecFull16 + 4u * i;
+        o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
+    }
 }
 
 }  // namespace neb
@@ -463,30 +633,27 @@ __global__ void gcm_key_setup_kernel(const uint8_t* __restrict__ key, uint32_t* 
 // ------------------------------------------------------------------------------------------
 // Host-side launchers (called by engine.cpp)
 
+extern "C" hipError_t neb_gcm_probe(void) {
+    hipFuncAttributes attr;
+    return hipFuncGetAttributes(&attr, (const void*)neb::gcm_single_kernel<false>);
+}
+
 extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s) {
-    hipLaunchKernelGGL(neb::gcm_key_setup_kernel, dim3(1), dim3(64), 0, s, d_key, d_rec);
+    hipLaunchKernelGGL(neb::gcm_key_setup_kernel, dim3(1), dim3(256), 0, s, d_key, d_rec);
     return hipGetLastError();
 }
 
-template <bool OPEN, bool SINGLE>
-static hipError_t launch_gcm(const neb::GcmArgs& a, int cu_count, hipStream_t s) {
-    auto kern = neb::gcm_batch_kernel<OPEN, SINGLE>;
-    const uint32_t lds = SINGLE ? neb::kLdsSingle : neb::kLdsMulti;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+template <class K>
+static hipError_t launch_grid(K kern, const neb::GcmArgs& a, int threads, int waves, int cu_count, hipStream_t s) {
     int per_cu = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, neb::kThreads, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     const uint32_t groups = (a.npkt + 3u) / 4u;
-    uint32_t want = (groups + neb::kWavesPerWG - 1) / neb::kWavesPerWG;
-    uint32_t cap = (uint32_t)(per_cu * cu_count);
-    uint32_t grid = want < cap ? want : cap;
+    const uint32_t want = (groups + waves - 1) / waves;
+    const uint32_t cap = (uint32_t)(per_cu * cu_count);
+    const uint32_t grid = want < cap ? want : cap;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(neb::kThreads), lds, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, a);
     return hipGetLastError();
 }
 
@@ -494,7 +661,10 @@ extern "C" hipError_t neb_gcm_batch(int open, const neb_desc* d_desc, uint32_t n
                                     const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint, int32_t* d_status,
                                     int cu_count, hipStream_t s) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status};
-    const bool single = key_hint != NEB_KEYS_MIXED;
-    if (open) return single ? launch_gcm<true, true>(a, cu_count, s) : launch_gcm<true, false>(a, cu_count, s);
-    return single ? launch_gcm<false, true>(a, cu_count, s) : launch_gcm<false, false>(a, cu_count, s);
+    if (key_hint != NEB_KEYS_MIXED) {
+        return open ? launch_grid(neb::gcm_single_kernel<true>, a, neb::kSingleThreads, neb::kSingleWaves, cu_count, s)
+                    : launch_grid(neb::gcm_single_kernel<false>, a, neb::kSingleThreads, neb::kSingleWaves, cu_count, s);
+    }
+    return open ? launch_grid(neb::gcm_multi_kernel<true>, a, neb::kMultiThreads, neb::kMultiWaves, cu_count, s)
+                : launch_grid(neb::gcm_multi_kernel<false>, a, neb::kMultiThreads, neb::kMultiWaves, cu_count, s);
 }

@@ -19,6 +19,7 @@ extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, h
 extern "C" hipError_t neb_gcm_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                     const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint, int32_t* d_status,
                                     int cu_count, hipStream_t s);
+extern "C" hipError_t neb_gcm_probe(void);
 extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
@@ -70,10 +71,19 @@ struct neb_cipher {
     int alg;
 };
 
-#define HIP_TRY(x)                               \
-    do {                                         \
-        hipError_t err_ = (x);                   \
-        if (err_ != hipSuccess) return NEB_ERR_HIP; \
+static thread_local char g_last_error[256] = "";
+
+static void set_error(const char* where, hipError_t err) {
+    std::snprintf(g_last_error, sizeof g_last_error, "%s: %s (%d)", where, hipGetErrorString(err), (int)err);
+}
+
+#define HIP_TRY(x)                                  \
+    do {                                            \
+        hipError_t err_ = (x);                      \
+        if (err_ != hipSuccess) {                   \
+            set_error(#x, err_);                    \
+            return NEB_ERR_HIP;                     \
+        }                                           \
     } while (0)
 
 static int ensure_stage(neb_engine* e, size_t bytes) {
@@ -91,6 +101,8 @@ static int ensure_stage(neb_engine* e, size_t bytes) {
 }
 
 extern "C" {
+
+NEB_API const char* neb_last_error(void) { return g_last_error; }
 
 NEB_API const char* neb_strerror(int rc) {
     switch (rc) {
@@ -111,20 +123,36 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
     if (!out || max_keys == 0 || max_keys == NEB_KEYS_MIXED) return NEB_ERR_INVALID;
     *out = nullptr;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NEB_ERR_NO_DEVICE;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return NEB_ERR_NO_DEVICE;
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NEB_ERR_NO_DEVICE;
-    HIP_TRY(hipSetDevice(device));
+    hipError_t err = hipGetDeviceCount(&ndev);
+    if (err != hipSuccess) {
+        set_error("hipGetDeviceCount", err);
+        return NEB_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= ndev) {
+        std::snprintf(g_last_error, sizeof g_last_error, "device %d out of range (%d devices)", device, ndev);
+        return NEB_ERR_NO_DEVICE;
+    }
+    int cus = 0;
+    if ((err = hipSetDevice(device)) != hipSuccess ||
+        (err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess) {
+        set_error("hipSetDevice/hipDeviceGetAttribute", err);
+        return NEB_ERR_NO_DEVICE;
+    }
+    // the library carries gfx950 code objects only: a device they do not load on is refused
+    if ((err = neb_gcm_probe()) != hipSuccess) {
+        set_error("gfx950 code object not loadable on this device", err);
+        return NEB_ERR_NO_DEVICE;
+    }
     neb_engine* e = new (std::nothrow) neb_engine();
     if (!e) return NEB_ERR_INVALID;
     e->device = device;
-    e->cu_count = prop.multiProcessorCount;
+    e->cu_count = cus;
     e->max_keys = max_keys;
     e->slot_alg.assign(max_keys, 0);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess ||
         hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess) {
+        set_error("engine allocation", hipGetLastError());
         neb_engine_destroy(e);
         return NEB_ERR_HIP;
     }
@@ -333,7 +361,7 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
     if (n == 0) return NEB_OK;
     if (!d_desc || !d_arena || !d_status) return NEB_ERR_INVALID;
     hipSetDevice(e->device);
-    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream, as for any HIP launch
     return launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s) == hipSuccess ? NEB_OK : NEB_ERR_HIP;
 }
 
