@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libnebula_aead.so")
+# NEB_LIB_PATH selects an alternative build of the same library (e.g. an ablation build in tools/).
+LIB_PATH = os.environ.get("NEB_LIB_PATH") or os.path.join(PKG_DIR, "libnebula_aead.so")
 
 ALG_AESGCM = 1
 ALG_CHACHAPOLY = 2

@@ -321,17 +321,21 @@ __device__ __forceinline__ PktShape pkt_shape(const neb_desc& d, bool run) {
 }
 
 // One round of one packet lane: keystream, payload XOR, GHASH input block. Returns X (BE words).
-template <bool OPEN, class RK>
+template <bool OPEN, uint32_t LPP, class RK>
 __device__ __forceinline__ uint4 gcm_lane_round(const neb_desc& d, const PktShape& sh, uint32_t r, uint32_t l,
                                                 uint32_t c1, uint32_t c2, uint2 lb8, const uint2* ttab,
                                                 const RK& rk, uint8_t* arena, uint4& ej0) {
-    const int32_t g = (int32_t)(16u * r + l + 1u) - (int32_t)sh.pad;  // 1-based GHASH index
+    const int32_t g = (int32_t)(LPP * r + l + 1u) - (int32_t)sh.pad;  // 1-based GHASH index
     const bool is_aad = g >= 1 && g <= (int32_t)sh.na;
     const bool is_ct = g > (int32_t)sh.na && g <= (int32_t)(sh.na + sh.m);
     const bool is_len = g == (int32_t)sh.n;
     const uint32_t k = (uint32_t)(g - (int32_t)sh.na);  // ciphertext block index (1-based)
     const uint32_t ctr = is_ct ? k + 1u : 1u;
+#ifdef NEB_ABLATE_AES
+    const uint4 ks = make_uint4(c1 ^ ctr, c2, ctr * 0x9E3779B9u, lb8.x);
+#else
     const uint4 ks = aes256_block(0u, c1, c2, bswap32(ctr), lb8, ttab, rk);
+#endif
     uint4 X = make_uint4(0, 0, 0, 0);
     if (is_aad) {
         const uint32_t off = 16u * (uint32_t)(g - 1);
@@ -353,13 +357,14 @@ __device__ __forceinline__ uint4 gcm_lane_round(const neb_desc& d, const PktShap
     return X;
 }
 
-// Tag finish on lane 15 (seal: store; open: compare, zero the payload on mismatch).
-template <bool OPEN>
+// Tag finish on the packet's last lane, which holds E_K(J0) (seal: store; open: compare, zero
+// the payload on mismatch).
+template <bool OPEN, uint32_t LPP>
 __device__ __forceinline__ uint32_t gcm_finish(const neb_desc& d, uint4 S, uint4 ej0, uint32_t lane, uint32_t l,
                                                uint8_t* arena) {
-    const uint4 tag = xor4(ej0, bswap4(S));  // valid on lane 15
+    const uint4 tag = xor4(ej0, bswap4(S));  // valid on lane LPP-1
     uint32_t fail = 0;
-    if (l == 15u) {
+    if (l == LPP - 1u) {
         if constexpr (!OPEN) {
             store_block(arena + d.dst_off + d.len, tag, 16);
         } else {
@@ -369,9 +374,9 @@ __device__ __forceinline__ uint32_t gcm_finish(const neb_desc& d, uint4 S, uint4
         }
     }
     if constexpr (OPEN) {
-        fail = (uint32_t)__shfl((int)fail, (int)(lane | 15u));
+        fail = (uint32_t)__shfl((int)fail, (int)(lane | (LPP - 1u)));
         if (fail) {
-            for (uint32_t off = 16u * l; off < d.len; off += 256u)
+            for (uint32_t off = 16u * l; off < d.len; off += 16u * LPP)
                 store_block(arena + d.dst_off + off, make_uint4(0, 0, 0, 0), min(16u, d.len - off));
         }
     }
@@ -379,16 +384,34 @@ __device__ __forceinline__ uint32_t gcm_finish(const neb_desc& d, uint4 S, uint4
 }
 
 // ------------------------------------------------------------------------------------------
-// One tunnel key for the whole batch.
+// One tunnel key for the whole batch: 4 lanes per packet, 16 packets per wave.
+//
+// Lane l of a packet owns padded GHASH blocks g' = 4r + l + 1 (n' = 4·ceil(n/4); a 1300-byte
+// packet has n = 84, so nothing is padded). Horner stride H^4 through the full table (32
+// conflict-free ds_read_b128 per multiply). The final Σ_l A_l·H^(4-l) runs as a 4-step Horner over
+// the quad with H's Shoup table, which every lane of a ds_read_b128 group reads at once: no bank
+// conflicts (per-lane power tables conflicted on every lookup and cost 17%).
 
 constexpr int kSingleWaves = 8;
 constexpr int kSingleThreads = kSingleWaves * kWave;
+constexpr uint32_t kLpp = kFullPow;            // lanes per packet
+constexpr uint32_t kPpw = 64u / kLpp;          // packets per wave
 
 struct SingleLds {
-    uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^16 (first: its offsets fit the ds_read offset field)
-    uint4 shoup[16 * 16];    // 4 KiB  M_k[v] for H^1..H^16 (table k-1 at byte (k-1)*256)
-    uint2 ttab[256 * 32];    // 64 KiB (T0, T2) pairs, 32 copies
+    uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
+    uint4 shoup_h[16];       // 256 B  M[v] = v·H
+    uint2 ttab[256 * 32];    // 64 KiB T-table pairs, 32 copies
 };
+
+// broadcast lane j of each quad (DPP quad_perm)
+template <int J>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J | (J << 2) | (J << 4) | (J << 6), 0xF, 0xF, false);
+}
+template <int J>
+__device__ __forceinline__ uint4 quad_bcast4(uint4 v) {
+    return make_uint4(quad_bcast<J>(v.x), quad_bcast<J>(v.y), quad_bcast<J>(v.z), quad_bcast<J>(v.w));
+}
 
 template <bool OPEN>
 __global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs args) {
@@ -396,23 +419,23 @@ __global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs a
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    const uint32_t q = lane >> 4;
-    const uint32_t l = lane & 15u;
+    const uint32_t q = lane / kLpp;   // packet slot in the wave
+    const uint32_t l = lane % kLpp;   // lane within the packet
     const uint2 lb8 = ttab_lane_base(lane);
 
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
     for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
-    for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull16 + 4u * i);
-    for (uint32_t i = tid; i < 16u * 16u; i += kSingleThreads) lds.shoup[i] = ld_rec4(srec, kRecShoup + 4u * i);
+    for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull + 4u * i);
+    if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
     uint32_t rks[60];
 #pragma unroll
     for (int i = 0; i < 60; i++) rks[i] = __builtin_amdgcn_readfirstlane(srec[kRecRoundKeys + i]);
     __syncthreads();
     const RkRegs rk{rks};
 
-    const uint32_t ngroups = (args.npkt + 3u) >> 2;
+    const uint32_t ngroups = (args.npkt + kPpw - 1u) / kPpw;
     for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
-        const uint32_t p = grp * 4u + q;
+        const uint32_t p = grp * kPpw + q;
         const bool valid = p < args.npkt;
         neb_desc d = {};
         if (valid) d = args.desc[p];
@@ -420,10 +443,15 @@ __global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs a
         if (d.key_id != args.key_hint) st = NEB_STATUS_BAD_KEY;
         if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
         const bool run = valid && st == NEB_STATUS_OK;
-        const PktShape sh = pkt_shape(d, run);
+        PktShape sh;
+        sh.na = (d.aad_len + 15u) >> 4;
+        sh.m = (d.len + 15u) >> 4;
+        sh.n = sh.na + sh.m + 1u;
+        sh.R = run ? (sh.n + kLpp - 1u) / kLpp : 0u;
+        sh.pad = kLpp * sh.R - sh.n;
         uint32_t Rmax = sh.R;
-        Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 16));
-        Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 32));
+#pragma unroll
+        for (int s = (int)kLpp; s < 64; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, s));
 
         // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
         const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
@@ -431,18 +459,30 @@ __global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs a
         uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
         for (uint32_t r = 0; r < Rmax; r++) {
             if (r < sh.R) {
-                const uint4 X = gcm_lane_round<OPEN>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
-                A = (r == 0) ? X : gf_mul_full(A, X, lds.full);
+                // GHASH of the previous rounds (A·H^4) first, then this round's AES: one phase's
+                // registers at a time keeps the kernel at 4 waves/SIMD without spills
+#ifdef NEB_ABLATE_HORNER
+                const uint4 G = A;
+#else
+                const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gf_mul_full(A, make_uint4(0, 0, 0, 0), lds.full);
+#endif
+                __builtin_amdgcn_sched_barrier(0);
+                const uint4 X = gcm_lane_round<OPEN, kLpp>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
+                A = xor4(G, X);
             }
         }
         if (run) {
-            // Σ_l A_l·H^(16-l): lane l's own power from the Shoup tables, then XOR over the 16 lanes
-            uint4 V = gf_mul_shoup(A, (15u - l) * 256u, lds.shoup);
-#pragma unroll
-            for (int s = 1; s < 16; s <<= 1) V = xor4(V, shfl_xor4(V, s));
-            if (gcm_finish<OPEN>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
+            // GHASH = Σ_l A_l·H^(4-l) = (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, same table in every lane
+            uint4 V = quad_bcast4<0>(A);
+#ifndef NEB_ABLATE_FINAL
+            V = xor4(gf_mul_shoup(V, 0u, lds.shoup_h), quad_bcast4<1>(A));
+            V = xor4(gf_mul_shoup(V, 0u, lds.shoup_h), quad_bcast4<2>(A));
+            V = xor4(gf_mul_shoup(V, 0u, lds.shoup_h), quad_bcast4<3>(A));
+            V = gf_mul_shoup(V, 0u, lds.shoup_h);
+#endif
+            if (gcm_finish<OPEN, kLpp>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
         }
-        if (valid && l == 15u) args.status[p] = (int32_t)st;
+        if (valid && l == kLpp - 1u) args.status[p] = (int32_t)st;
     }
 }
 
@@ -512,7 +552,7 @@ __global__ __launch_bounds__(kMultiThreads, 3) void gcm_multi_kernel(GcmArgs arg
         uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
         for (uint32_t r = 0; r < Rmax; r++) {
             if (r < sh.R) {
-                const uint4 X = gcm_lane_round<OPEN>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
+                const uint4 X = gcm_lane_round<OPEN, 16u>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
                 A = (r == 0) ? X : xor4(gf_mul_shoup(A, tabs + 4u * 256u, pbase), X);
             }
         }
@@ -526,7 +566,7 @@ __global__ __launch_bounds__(kMultiThreads, 3) void gcm_multi_kernel(GcmArgs arg
                 const uint4 pv = shfl_xor4(V, s), pm = shfl_xor4(mv, s);
                 V = ((l / (uint32_t)s) & 1u) ? xor4(pm, V) : xor4(mv, pv);
             }
-            if (gcm_finish<OPEN>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
+            if (gcm_finish<OPEN, 16u>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
         }
         if (valid && l == 15u) args.status[p] = (int32_t)st;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // slice is rewritten next group
@@ -544,7 +584,7 @@ __device__ uint8_t xtime_d(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) 
 
 __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __restrict__ key, uint32_t* __restrict__ rec) {
     __shared__ uint4 hp[16];      // H^1..H^16
-    __shared__ uint4 basis[128];  // x^i · H^16
+    __shared__ uint4 basis[128];  // x^i · H^kFullPow
     if (threadIdx.x == 0) {
         uint8_t rk[240];
         for (int i = 0; i < 32; i++) rk[i] = key[i];
@@ -601,7 +641,7 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
             }
             for (int i = 0; i < 4; i++) pw[i] = z[i];
         }
-        uint4 b = hp[15];
+        uint4 b = hp[kFullPow - 1];
         for (int i = 0; i < 128; i++) {
             basis[i] = b;
             b = gf_mulx(b);
@@ -617,13 +657,13 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         uint32_t* o = rec + kRecShoup + 64u * k + 4u * v;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
-    // full table of H^16: F_p[v] = XOR of basis[4p + j] for the set bits of v (bit 3 ↔ j = 0)
+    // full table of H^kFullPow: F_p[v] = XOR of basis[4p + j] for the set bits of v (bit 3 ↔ j = 0)
     for (uint32_t i = t; i < 512u; i += 256u) {
         const uint32_t p = i >> 4, v = i & 15u;
         uint4 e = make_uint4(0, 0, 0, 0);
         for (uint32_t j = 0; j < 4; j++)
             if ((v >> (3 - j)) & 1u) e = xor4(e, basis[4 * p + j]);
-        uint32_t* o = rec + kRecFull16 + 4u * i;
+        uint32_t* o = rec + kRecFull + 4u * i;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
 }
@@ -644,11 +684,12 @@ extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, h
 }
 
 template <class K>
-static hipError_t launch_grid(K kern, const neb::GcmArgs& a, int threads, int waves, int cu_count, hipStream_t s) {
+static hipError_t launch_grid(K kern, const neb::GcmArgs& a, int threads, int waves, uint32_t ppw, int cu_count,
+                              hipStream_t s) {
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
-    const uint32_t groups = (a.npkt + 3u) / 4u;
+    const uint32_t groups = (a.npkt + ppw - 1u) / ppw;
     const uint32_t want = (groups + waves - 1) / waves;
     const uint32_t cap = (uint32_t)(per_cu * cu_count);
     const uint32_t grid = want < cap ? want : cap;
@@ -662,9 +703,11 @@ extern "C" hipError_t neb_gcm_batch(int open, const neb_desc* d_desc, uint32_t n
                                     int cu_count, hipStream_t s) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status};
     if (key_hint != NEB_KEYS_MIXED) {
-        return open ? launch_grid(neb::gcm_single_kernel<true>, a, neb::kSingleThreads, neb::kSingleWaves, cu_count, s)
-                    : launch_grid(neb::gcm_single_kernel<false>, a, neb::kSingleThreads, neb::kSingleWaves, cu_count, s);
+        return open ? launch_grid(neb::gcm_single_kernel<true>, a, neb::kSingleThreads, neb::kSingleWaves, neb::kPpw,
+                                  cu_count, s)
+                    : launch_grid(neb::gcm_single_kernel<false>, a, neb::kSingleThreads, neb::kSingleWaves, neb::kPpw,
+                                  cu_count, s);
     }
-    return open ? launch_grid(neb::gcm_multi_kernel<true>, a, neb::kMultiThreads, neb::kMultiWaves, cu_count, s)
-                : launch_grid(neb::gcm_multi_kernel<false>, a, neb::kMultiThreads, neb::kMultiWaves, cu_count, s);
+    return open ? launch_grid(neb::gcm_multi_kernel<true>, a, neb::kMultiThreads, neb::kMultiWaves, 4u, cu_count, s)
+                : launch_grid(neb::gcm_multi_kernel<false>, a, neb::kMultiThreads, neb::kMultiWaves, 4u, cu_count, s);
 }

@@ -16,10 +16,12 @@ constexpr uint32_t kRecHPow = 64;       // dwords [64,128): H^1..H^16, 4 big-end
 constexpr uint32_t kNumHPow = 16;
 // 4-bit tables M_k[v] = v·H^k for k = 1..16: 16 tables × 16 entries × 4 BE words (Shoup layout)
 constexpr uint32_t kRecShoup = 128;
-// full 4-bit table of H^16 over all 32 nibble positions: F_p[v] = (v·x^4p)·H^16 (reduced),
-// 32 × 16 entries × 4 BE words — a multiply by H^16 is 32 lookups and XORs, no shifts
-constexpr uint32_t kRecFull16 = kRecShoup + 16 * 16 * 4;
-static_assert(kRecFull16 + 32 * 16 * 4 == kKeyRecDwords, "record layout");
+// full 4-bit table of H^kFullPow over all 32 nibble positions: F_p[v] = (v·x^4p)·H^kFullPow
+// (reduced), 32 × 16 entries × 4 BE words — a multiply by it is 32 lookups and XORs, no shifts.
+// kFullPow = lanes per packet of the single-key kernel (its Horner stride).
+constexpr uint32_t kFullPow = 4;
+constexpr uint32_t kRecFull = kRecShoup + 16 * 16 * 4;
+static_assert(kRecFull + 32 * 16 * 4 == kKeyRecDwords, "record layout");
 
 // ChaCha20-Poly1305 record
 constexpr uint32_t kRecChaKey = 0;      // dwords [0,8): the 256-bit key as 8 little-endian words
