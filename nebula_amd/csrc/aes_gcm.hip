@@ -384,24 +384,17 @@ __device__ __forceinline__ uint32_t gcm_finish(const neb_desc& d, uint4 S, uint4
 }
 
 // ------------------------------------------------------------------------------------------
-// One tunnel key for the whole batch: 4 lanes per packet, 16 packets per wave.
+// Packet groups: 4 lanes per packet, 16 packets per wave.
 //
 // Lane l of a packet owns padded GHASH blocks g' = 4r + l + 1 (n' = 4·ceil(n/4); a 1300-byte
-// packet has n = 84, so nothing is padded). Horner stride H^4 through the full table (32
-// conflict-free ds_read_b128 per multiply). The final Σ_l A_l·H^(4-l) runs as a 4-step Horner over
-// the quad with H's Shoup table, which every lane of a ds_read_b128 group reads at once: no bank
-// conflicts (per-lane power tables conflicted on every lookup and cost 17%).
+// packet has n = 84, so nothing is padded). Horner stride H^4. The final Σ_l A_l·H^(4-l) runs as a
+// 4-step Horner over the quad with H's table, which every lane of a ds_read_b128 group reads at
+// once: no bank conflicts (per-lane power tables conflicted on every lookup and cost 17%).
+// The round keys are wave-uniform (scalar registers) in both kernels below: one key per batch, or
+// one key per chunk of a regrouped mixed-key batch (sched.hpp).
 
-constexpr int kSingleWaves = 8;
-constexpr int kSingleThreads = kSingleWaves * kWave;
-constexpr uint32_t kLpp = kFullPow;            // lanes per packet
-constexpr uint32_t kPpw = 64u / kLpp;          // packets per wave
-
-struct SingleLds {
-    uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
-    uint4 shoup_h[16];       // 256 B  M[v] = v·H
-    uint2 ttab[256 * 32];    // 64 KiB T-table pairs, 32 copies
-};
+constexpr uint32_t kLpp = kFullPow;    // lanes per packet
+constexpr uint32_t kPpw = 64u / kLpp;  // packets per wave
 
 // broadcast lane j of each quad (DPP quad_perm)
 template <int J>
@@ -413,14 +406,96 @@ __device__ __forceinline__ uint4 quad_bcast4(uint4 v) {
     return make_uint4(quad_bcast<J>(v.x), quad_bcast<J>(v.y), quad_bcast<J>(v.z), quad_bcast<J>(v.w));
 }
 
+// GHASH tables a packet group multiplies with.
+struct GhFull {  // one key per batch: reduction-free full table for H^4 + Shoup table for H
+    const uint4* full;
+    const uint4* shoup_h;
+    __device__ __forceinline__ uint4 horner(uint4 a) const { return gf_mul_full(a, make_uint4(0, 0, 0, 0), full); }
+    __device__ __forceinline__ uint4 mul_h(uint4 a) const { return gf_mul_shoup(a, 0u, shoup_h); }
+};
+struct GhShoup {  // one key per chunk: Shoup tables for H^4 and H staged in the wave's LDS slice
+    const uint4* base;  // table H at +0, H^4 at +256
+    __device__ __forceinline__ uint4 horner(uint4 a) const { return gf_mul_shoup(a, 256u, base); }
+    __device__ __forceinline__ uint4 mul_h(uint4 a) const { return gf_mul_shoup(a, 0u, base); }
+};
+
+// Seal or open packet `p` (lanes q*4 .. q*4+3 of the wave). `expect_key`: the key this wave's
+// round keys and tables belong to; key_ok: that key is installed with the right algorithm.
+template <bool OPEN, class GH>
+__device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
+                                                 bool key_ok, const RkRegs& rk, const GH& gh, const uint2* ttab,
+                                                 uint2 lb8, uint32_t lane) {
+    const uint32_t l = lane % kLpp;
+    neb_desc d = {};
+    if (valid) d = args.desc[p];
+    uint32_t st = NEB_STATUS_OK;
+    if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
+    if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
+    const bool run = valid && st == NEB_STATUS_OK;
+    PktShape sh;
+    sh.na = (d.aad_len + 15u) >> 4;
+    sh.m = (d.len + 15u) >> 4;
+    sh.n = sh.na + sh.m + 1u;
+    sh.R = run ? (sh.n + kLpp - 1u) / kLpp : 0u;
+    sh.pad = kLpp * sh.R - sh.n;
+    uint32_t Rmax = sh.R;
+#pragma unroll
+    for (int s = (int)kLpp; s < 64; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, s));
+
+    // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
+    const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
+    const uint32_t c2 = bswap32((uint32_t)d.counter);
+    uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
+    for (uint32_t r = 0; r < Rmax; r++) {
+        if (r < sh.R) {
+            // GHASH of the previous rounds (A·H^4) first, then this round's AES: one phase's
+            // registers at a time keeps the kernel at 4 waves/SIMD without spills
+#ifdef NEB_ABLATE_HORNER
+            const uint4 G = A;
+#else
+            const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+            const uint4 X = gcm_lane_round<OPEN, kLpp>(d, sh, r, l, c1, c2, lb8, ttab, rk, args.arena, ej0);
+            A = xor4(G, X);
+        }
+    }
+    if (run) {
+        // GHASH = Σ_l A_l·H^(4-l) = (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, same table in every lane
+        uint4 V = quad_bcast4<0>(A);
+#ifndef NEB_ABLATE_FINAL
+        V = xor4(gh.mul_h(V), quad_bcast4<1>(A));
+        V = xor4(gh.mul_h(V), quad_bcast4<2>(A));
+        V = xor4(gh.mul_h(V), quad_bcast4<3>(A));
+        V = gh.mul_h(V);
+#endif
+        if (gcm_finish<OPEN, kLpp>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
+    }
+    if (valid && l == kLpp - 1u) args.status[p] = (int32_t)st;
+}
+
+__device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rks[60]) {
+#pragma unroll
+    for (int i = 0; i < 60; i++) rks[i] = __builtin_amdgcn_readfirstlane(rec[kRecRoundKeys + i]);
+}
+
+// ---- one tunnel key for the whole batch -------------------------------------------------------
+
+constexpr int kSingleWaves = 8;
+constexpr int kSingleThreads = kSingleWaves * kWave;
+
+struct SingleLds {
+    uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
+    uint4 shoup_h[16];       // 256 B  M[v] = v·H
+    uint2 ttab[256 * 32];    // 64 KiB T-table pairs, 32 copies
+};
+
 template <bool OPEN>
 __global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs args) {
     __shared__ SingleLds lds;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    const uint32_t q = lane / kLpp;   // packet slot in the wave
-    const uint32_t l = lane % kLpp;   // lane within the packet
     const uint2 lb8 = ttab_lane_base(lane);
 
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
@@ -428,148 +503,68 @@ __global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs a
     for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull + 4u * i);
     if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
     uint32_t rks[60];
-#pragma unroll
-    for (int i = 0; i < 60; i++) rks[i] = __builtin_amdgcn_readfirstlane(srec[kRecRoundKeys + i]);
+    load_round_keys(srec, rks);
     __syncthreads();
     const RkRegs rk{rks};
+    const GhFull gh{lds.full, lds.shoup_h};
 
     const uint32_t ngroups = (args.npkt + kPpw - 1u) / kPpw;
     for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
-        const uint32_t p = grp * kPpw + q;
-        const bool valid = p < args.npkt;
-        neb_desc d = {};
-        if (valid) d = args.desc[p];
-        uint32_t st = NEB_STATUS_OK;
-        if (d.key_id != args.key_hint) st = NEB_STATUS_BAD_KEY;
-        if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
-        const bool run = valid && st == NEB_STATUS_OK;
-        PktShape sh;
-        sh.na = (d.aad_len + 15u) >> 4;
-        sh.m = (d.len + 15u) >> 4;
-        sh.n = sh.na + sh.m + 1u;
-        sh.R = run ? (sh.n + kLpp - 1u) / kLpp : 0u;
-        sh.pad = kLpp * sh.R - sh.n;
-        uint32_t Rmax = sh.R;
-#pragma unroll
-        for (int s = (int)kLpp; s < 64; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, s));
-
-        // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
-        const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
-        const uint32_t c2 = bswap32((uint32_t)d.counter);
-        uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
-        for (uint32_t r = 0; r < Rmax; r++) {
-            if (r < sh.R) {
-                // GHASH of the previous rounds (A·H^4) first, then this round's AES: one phase's
-                // registers at a time keeps the kernel at 4 waves/SIMD without spills
-#ifdef NEB_ABLATE_HORNER
-                const uint4 G = A;
-#else
-                const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gf_mul_full(A, make_uint4(0, 0, 0, 0), lds.full);
-#endif
-                __builtin_amdgcn_sched_barrier(0);
-                const uint4 X = gcm_lane_round<OPEN, kLpp>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
-                A = xor4(G, X);
-            }
-        }
-        if (run) {
-            // GHASH = Σ_l A_l·H^(4-l) = (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, same table in every lane
-            uint4 V = quad_bcast4<0>(A);
-#ifndef NEB_ABLATE_FINAL
-            V = xor4(gf_mul_shoup(V, 0u, lds.shoup_h), quad_bcast4<1>(A));
-            V = xor4(gf_mul_shoup(V, 0u, lds.shoup_h), quad_bcast4<2>(A));
-            V = xor4(gf_mul_shoup(V, 0u, lds.shoup_h), quad_bcast4<3>(A));
-            V = gf_mul_shoup(V, 0u, lds.shoup_h);
-#endif
-            if (gcm_finish<OPEN, kLpp>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
-        }
-        if (valid && l == kLpp - 1u) args.status[p] = (int32_t)st;
+        const uint32_t p = grp * kPpw + lane / kLpp;
+        gcm_packet_group<OPEN>(args, p, p < args.npkt, args.key_hint, true, rk, gh, lds.ttab, lb8, lane);
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// Mixed keys: per-packet key material staged in the wave's LDS slice.
+// ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------
 
-constexpr int kMultiWaves = 12;
-constexpr int kMultiThreads = kMultiWaves * kWave;
-constexpr int kMultiNT = 5;  // tables per packet: H, H^2, H^4, H^8, H^16 (lane powers H, H^2; tree H^2, H^4, H^8)
-__host__ __device__ constexpr int multi_pow(int t) { return t < 2 ? t + 1 : (2 << (t - 1)); }
+constexpr int kChunkWaves = 8;
+constexpr int kChunkThreads = kChunkWaves * kWave;
 
-struct MultiPkt {
-    uint4 shoup[kMultiNT * 16];  // 1280 B (256-B aligned tables)
-    uint4 rk[16];                // 240 B used (15 round keys), padded to 256
+struct ChunkLds {
+    uint4 shoup[kChunkWaves][2][16];  // per wave: M[v] for H (+0) and H^4 (+256)
+    uint2 ttab[256 * 32];             // 64 KiB T-table pairs, 32 copies
 };
-struct MultiLds {
-    MultiPkt pkt[kMultiWaves][4];  // 96 KiB
-    uint2 ttab[256 * 32];          // 64 KiB
+
+struct ChunkArgs {
+    const uint32_t* sorted;
+    const uint4* chunks;
+    const uint32_t* nchunks;  // device counter written by the scheduler
+    uint32_t max_chunks;
 };
-static_assert(sizeof(MultiLds) <= 163840, "LDS budget");
 
 template <bool OPEN>
-__global__ __launch_bounds__(kMultiThreads, 3) void gcm_multi_kernel(GcmArgs args) {
-    __shared__ MultiLds lds;
+__global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs args, ChunkArgs ca) {
+    __shared__ ChunkLds lds;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    const uint32_t q = lane >> 4;
-    const uint32_t l = lane & 15u;
     const uint2 lb8 = ttab_lane_base(lane);
-
-    for (uint32_t i = tid; i < 256u * 32u; i += kMultiThreads) lds.ttab[i] = ttab_entry(i);
+    for (uint32_t i = tid; i < 256u * 32u; i += kChunkThreads) lds.ttab[i] = ttab_entry(i);
     __syncthreads();
-    MultiPkt& mp = lds.pkt[wave][q];
-    const uint4* pbase = lds.pkt[0][0].shoup;
-    const uint32_t tabs = (uint32_t)((const char*)mp.shoup - (const char*)pbase);  // multiple of 256
-    const RkLds rk{mp.rk};
+    uint4* wtab = &lds.shoup[wave][0][0];
+    const GhShoup gh{wtab};
+    uint32_t nch = __builtin_amdgcn_readfirstlane(*ca.nchunks);
+    nch = nch < ca.max_chunks ? nch : ca.max_chunks;
 
-    const uint32_t ngroups = (args.npkt + 3u) >> 2;
-    for (uint32_t grp = blockIdx.x * kMultiWaves + wave; grp < ngroups; grp += gridDim.x * kMultiWaves) {
-        const uint32_t p = grp * 4u + q;
-        const bool valid = p < args.npkt;
-        neb_desc d = {};
-        if (valid) d = args.desc[p];
-        const uint32_t* rec = args.keys + (size_t)d.key_id * kKeyRecDwords;
-        uint32_t st = NEB_STATUS_OK;
-        if (d.key_id >= args.max_keys || rec[kRecAlg] != NEB_ALG_AESGCM) st = NEB_STATUS_BAD_KEY;
-        if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
-        const bool run = valid && st == NEB_STATUS_OK;
-        const PktShape sh = pkt_shape(d, run);
-        uint32_t Rmax = sh.R;
-        Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 16));
-        Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, 32));
-
-        if (run) {  // stage round keys and the 5 Shoup tables of this packet's key
-            if (l < 15u) mp.rk[l] = ld_rec4(rec, kRecRoundKeys + 4u * l);
-#pragma unroll
-            for (int t = 0; t < kMultiNT; t++)
-                mp.shoup[16 * t + l] = ld_rec4(rec, kRecShoup + 64u * (uint32_t)(multi_pow(t) - 1) + 4u * l);
-        }
+    for (uint32_t c = blockIdx.x * kChunkWaves + wave; c < nch; c += gridDim.x * kChunkWaves) {
+        const uint4 ch = ca.chunks[c];  // {start, count, key, class}, wave-uniform
+        const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
+        const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
+        const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
+        const uint32_t* rec = args.keys + (size_t)(key < args.max_keys ? key : 0u) * kKeyRecDwords;
+        const bool key_ok = key < args.max_keys && rec[kRecAlg] == NEB_ALG_AESGCM;
+        uint32_t rks[60];
+        load_round_keys(rec, rks);
+        // stage the chunk key's Shoup tables for H (table 0) and H^4 (table 3)
+        if (lane < 32u) wtab[lane] = ld_rec4(rec, kRecShoup + (lane < 16u ? 0u : 3u * 64u - 64u) + 4u * lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-        const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
-        const uint32_t c2 = bswap32((uint32_t)d.counter);
-        uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
-        for (uint32_t r = 0; r < Rmax; r++) {
-            if (r < sh.R) {
-                const uint4 X = gcm_lane_round<OPEN, 16u>(d, sh, r, l, c1, c2, lb8, lds.ttab, rk, args.arena, ej0);
-                A = (r == 0) ? X : xor4(gf_mul_shoup(A, tabs + 4u * 256u, pbase), X);
-            }
-        }
-        if (run) {
-            // lane powers H^(2 - l mod 2), pair XOR, then tree levels H^2, H^4, H^8
-            uint4 V = gf_mul_shoup(A, tabs + (1u - (l & 1u)) * 256u, pbase);
-            V = xor4(V, shfl_xor4(V, 1));
-#pragma unroll
-            for (int s = 2, t = 1; s < 16; s <<= 1, t++) {
-                const uint4 mv = gf_mul_shoup(V, tabs + (uint32_t)t * 256u, pbase);
-                const uint4 pv = shfl_xor4(V, s), pm = shfl_xor4(mv, s);
-                V = ((l / (uint32_t)s) & 1u) ? xor4(pm, V) : xor4(mv, pv);
-            }
-            if (gcm_finish<OPEN, 16u>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
-        }
-        if (valid && l == 15u) args.status[p] = (int32_t)st;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // slice is rewritten next group
+        const uint32_t q = lane / kLpp;
+        const bool valid = q < count;
+        const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, lds.ttab, lb8, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
@@ -683,31 +678,39 @@ extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, h
     return hipGetLastError();
 }
 
-template <class K>
-static hipError_t launch_grid(K kern, const neb::GcmArgs& a, int threads, int waves, uint32_t ppw, int cu_count,
-                              hipStream_t s) {
+template <class K, class... Extra>
+static hipError_t launch_grid(K kern, int threads, uint32_t work_waves, int cu_count, hipStream_t s, Extra... args) {
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
-    const uint32_t groups = (a.npkt + ppw - 1u) / ppw;
-    const uint32_t want = (groups + waves - 1) / waves;
+    const uint32_t waves = (uint32_t)threads / 64u;
+    const uint32_t want = (work_waves + waves - 1) / waves;
     const uint32_t cap = (uint32_t)(per_cu * cu_count);
     const uint32_t grid = want < cap ? want : cap;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, args...);
     return hipGetLastError();
 }
 
-extern "C" hipError_t neb_gcm_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
-                                    const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint, int32_t* d_status,
-                                    int cu_count, hipStream_t s) {
+// One tunnel key (key_hint) for every descriptor.
+extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                                           const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
+                                           int32_t* d_status, int cu_count, hipStream_t s) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status};
-    if (key_hint != NEB_KEYS_MIXED) {
-        return open ? launch_grid(neb::gcm_single_kernel<true>, a, neb::kSingleThreads, neb::kSingleWaves, neb::kPpw,
-                                  cu_count, s)
-                    : launch_grid(neb::gcm_single_kernel<false>, a, neb::kSingleThreads, neb::kSingleWaves, neb::kPpw,
-                                  cu_count, s);
-    }
-    return open ? launch_grid(neb::gcm_multi_kernel<true>, a, neb::kMultiThreads, neb::kMultiWaves, 4u, cu_count, s)
-                : launch_grid(neb::gcm_multi_kernel<false>, a, neb::kMultiThreads, neb::kMultiWaves, 4u, cu_count, s);
+    const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
+    return open ? launch_grid(neb::gcm_single_kernel<true>, neb::kSingleThreads, groups, cu_count, s, a)
+                : launch_grid(neb::gcm_single_kernel<false>, neb::kSingleThreads, groups, cu_count, s, a);
+}
+
+// Mixed keys: the batch has been regrouped into chunks by neb_sched_build.
+extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                                            const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
+                                            const uint32_t* d_sorted, const uint4* d_chunks,
+                                            const uint32_t* d_nchunks, uint32_t max_chunks, int cu_count,
+                                            hipStream_t s) {
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status};
+    neb::ChunkArgs ca{d_sorted, d_chunks, d_nchunks, max_chunks};
+    const uint32_t bound = (n + neb::kPpw - 1u) / neb::kPpw;  // enough waves for the typical chunk count
+    return open ? launch_grid(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, a, ca)
+                : launch_grid(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, a, ca);
 }

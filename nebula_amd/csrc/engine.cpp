@@ -14,11 +14,17 @@
 
 #include "../../include/nebula_aead.h"
 #include "layout.hpp"
+#include "sched.hpp"
 
 extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
-extern "C" hipError_t neb_gcm_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
-                                    const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint, int32_t* d_status,
-                                    int cu_count, hipStream_t s);
+extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                                           const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
+                                           int32_t* d_status, int cu_count, hipStream_t s);
+extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
+                                            const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
+                                            const uint32_t* d_sorted, const uint4* d_chunks,
+                                            const uint32_t* d_nchunks, uint32_t max_chunks, int cu_count,
+                                            hipStream_t s);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
@@ -47,6 +53,17 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
 
+// Device workspace of the mixed-key scheduler (sched.hpp). One per engine; a batch waits on the
+// previous user's event before reusing it, so batches on different streams never overlap in it.
+struct SchedSpace {
+    uint8_t* mem = nullptr;
+    size_t bytes = 0;
+    uint32_t n_cap = 0;
+    neb::SchedWs ws{};
+    hipEvent_t done = nullptr;
+    std::mutex mu;
+};
+
 struct neb_engine {
     int device = 0;
     int cu_count = 0;
@@ -63,6 +80,8 @@ struct neb_engine {
 
     std::mutex pipe_mu;
     PipeSlot pipe[kPipeStreams];
+
+    SchedSpace sched;
 };
 
 struct neb_cipher {
@@ -172,6 +191,8 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
         if (s.h_desc) hipHostFree(s.h_desc);
         if (s.h_status) hipHostFree(s.h_status);
     }
+    if (e->sched.done) { hipEventSynchronize(e->sched.done); hipEventDestroy(e->sched.done); }
+    if (e->sched.mem) hipFree(e->sched.mem);
     if (e->d_keys) hipFree(e->d_keys);
     if (e->h_stage) hipHostFree(e->h_stage);
     if (e->d_stage) hipFree(e->d_stage);
@@ -263,10 +284,63 @@ static void fill_nonce(int alg, uint64_t n, uint8_t* nb) {
     for (int i = 0; i < 8; i++) nb[4 + i] = alg == NEB_ALG_AESGCM ? (uint8_t)(n >> (56 - 8 * i)) : (uint8_t)(n >> (8 * i));
 }
 
+// Size the scheduler workspace for n packets (caller holds sched.mu).
+static hipError_t sched_reserve(neb_engine* e, uint32_t n) {
+    SchedSpace& sp = e->sched;
+    if (!sp.done) {
+        hipError_t err = hipEventCreateWithFlags(&sp.done, hipEventDisableTiming);
+        if (err != hipSuccess) return err;
+    }
+    if (n <= sp.n_cap && sp.mem) return hipSuccess;
+    const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
+    const uint32_t nb = neb::sched_nbins(e->max_keys);
+    const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys);
+    const size_t b_counters = align_up((2u + 2u * (size_t)nb) * 4u, 256), b_base = align_up((size_t)nb * 4u, 256);
+    const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = (size_t)mc * 16u;
+    const size_t bytes = b_counters + b_base + 2 * b_idx + b_chunks;
+    hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
+    if (err != hipSuccess) return err;
+    if (sp.mem) hipFree(sp.mem);
+    sp.mem = nullptr;
+    sp.n_cap = 0;
+    err = hipMalloc((void**)&sp.mem, bytes);
+    if (err != hipSuccess) return err;
+    uint8_t* m = sp.mem;
+    sp.ws.counters = (uint32_t*)m;
+    sp.ws.hist = sp.ws.counters + 2;
+    sp.ws.fill = sp.ws.hist + nb;
+    m += b_counters;
+    sp.ws.base = (uint32_t*)m;
+    m += b_base;
+    sp.ws.binof = (uint32_t*)m;
+    m += b_idx;
+    sp.ws.sorted = (uint32_t*)m;
+    m += b_idx;
+    sp.ws.chunks = (uint4*)m;
+    sp.ws.max_chunks = mc;
+    sp.bytes = bytes;
+    sp.n_cap = cap;
+    return hipSuccess;
+}
+
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                int32_t* d_status, uint32_t key_hint, hipStream_t s) {
-    if (alg == NEB_ALG_AESGCM)
-        return neb_gcm_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, e->cu_count, s);
+    if (alg == NEB_ALG_AESGCM) {
+        if (key_hint != NEB_KEYS_MIXED)
+            return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status,
+                                        e->cu_count, s);
+        // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
+        SchedSpace& sp = e->sched;
+        std::lock_guard<std::mutex> g(sp.mu);
+        hipError_t err = sched_reserve(e, n);
+        if (err == hipSuccess) err = hipStreamWaitEvent(s, sp.done, 0);
+        if (err == hipSuccess) err = neb_sched_build(d_desc, n, e->max_keys, 4u, &sp.ws, s);
+        if (err == hipSuccess)
+            err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
+                                        sp.ws.chunks, sp.ws.counters + 1, sp.ws.max_chunks, e->cu_count, s);
+        if (err == hipSuccess) err = hipEventRecord(sp.done, s);
+        return err;
+    }
     return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, e->cu_count, s);
 }
 
@@ -297,6 +371,7 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
     if (err == hipSuccess)
         err = launch_batch(e, c->alg, open, (const neb_desc*)(e->d_stage + o_desc), 1, e->d_stage + o_aad,
                            (int32_t*)(e->d_stage + o_status), c->key_id, e->stream);
+    if (err != hipSuccess) set_error("one_packet", err);
     const size_t out_len = open ? pay_len : pay_len + 16;
     if (err == hipSuccess) err = hipMemcpyAsync(h + o_status, e->d_stage + o_status, 4, hipMemcpyDeviceToHost, e->stream);
     if (err == hipSuccess && out_len)
@@ -362,7 +437,12 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
     if (!d_desc || !d_arena || !d_status) return NEB_ERR_INVALID;
     hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream, as for any HIP launch
-    return launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s) == hipSuccess ? NEB_OK : NEB_ERR_HIP;
+    hipError_t err = launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s);
+    if (err != hipSuccess) {
+        set_error("batch launch", err);
+        return NEB_ERR_HIP;
+    }
+    return NEB_OK;
 }
 
 NEB_API int neb_seal_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
