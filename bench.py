@@ -37,13 +37,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_env():
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return rank, world, local
-
-
 def cpu_share() -> int:
     try:
         n = len(os.sched_getaffinity(0))
@@ -98,12 +91,14 @@ def cpu_baseline(b, target_s: float = 6.0):
     }
 
 
-def pmc_traffic(kernel_tag: str):
-    """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/pmc_traffic.json)."""
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 counter passes
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
+    correction + WRITE_SIZE, KiB -> bytes). None when no pass for this kernel is committed."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
-        return d.get(kernel_tag, {}).get("hbm_bytes_per_launch")
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -118,6 +113,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    from nebula_amd.shard import Control, dist_env
+
     rank, world, local = dist_env()
     import torch
 
@@ -129,16 +126,9 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("gloo")  # control only (barrier / max of timings); no data-path collective
-        pg = dist
-
-    def barrier():
-        if pg is not None:
-            pg.barrier()
+    # control plane only (barrier / max of timings) over gloo; no data-path collective
+    ctrl = Control(world)
+    barrier = ctrl.barrier
 
     cfg = args.config
     t0 = time.time()
@@ -177,11 +167,7 @@ def main():
             st2 = host_batch(eng, b.alg, True, d, buf.array, hint)
         te = time.perf_counter()
         assert (st == 0).all() and (st2 == 0).all()
-        dt = te - ts
-        if pg is not None:
-            t = torch.tensor([dt], dtype=torch.float64)
-            pg.all_reduce(t, op=pg.ReduceOp.MAX)
-            dt = float(t[0])
+        dt = ctrl.max(te - ts)
         if rank == 0:
             print(json.dumps({
                 "metric": "GiB/s host-resident (pinned H2D + kernel + D2H) AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch",
@@ -223,18 +209,16 @@ def main():
     open_ms = float(np.mean([m.elapsed_time(z) for _, m, z in ev]))
     st = db.status_host()
     assert (st == 0).all(), "open failed inside the timed region"
-    if pg is not None:
-        t = torch.tensor([dt], dtype=torch.float64)
-        pg.all_reduce(t, op=pg.ReduceOp.MAX)
-        dt = float(t[0])
+    dt = ctrl.max(dt)
+    total_payload = ctrl.sum(2 * payload * args.steps)
 
     if rank != 0:
         return
-    total_payload = 2 * payload * args.steps * world
     value = total_payload / dt / GIB
     achieved = alg_bytes / (seal_ms * 1e-3) / 1e9  # GB/s, seal kernel
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
-    kern_tag = f"{'gcm' if b.alg == 1 else 'chacha'}_seal_{'single' if b.nkeys == 1 else 'mixed'}"
+    kern_tag = ("gcm_single_kernel<false>" if b.nkeys == 1 else "gcm_chunk_kernel<false>") if b.alg == 1 \
+        else "chacha_batch_kernel<false>"
     out = {
         "metric": "GiB/s device-resident AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch"
         if cfg == 1 else f"GiB/s device-resident {alg_name} seal+open ({workload_name})",
