@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
 #include "layout.hpp"
@@ -132,27 +134,30 @@ struct RkLds {  // per-packet round keys staged in LDS
     __device__ __forceinline__ uint4 get(int r) const { return base[r]; }
 };
 
-template <class RK>
-__device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint2 lb,
-                                              const uint2* ttab, const RK& rk) {
-    // volatile keeps the 8-byte ds_read_b64 (bank = (addr/4) mod 64, conflict-free over the 32
-    // copies); a narrowed ds_read_b32 would bank mod 32 and conflict 2-way between copies c, c+16
-    // lookups are single dwords (ds_read_b32, bank = (addr/4) mod 32): T0 via lb0, T2 via lb2
-    auto T0 = [&](uint32_t s, int k) -> uint32_t {
+// T-table lookups: T0[byte k of s], T2[byte k of s] (T1 = rotl8 T0, T3 = rotl8 T2).
+struct TLook {
+    const uint2* ttab;
+    uint2 lb;
+    __device__ __forceinline__ uint32_t t0(uint32_t s, int k) const {
         return lds_at<uint32_t>(ttab, perm(s, lb.x, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
-    };
-    auto T2 = [&](uint32_t s, int k) -> uint32_t {
+    }
+    __device__ __forceinline__ uint32_t t2(uint32_t s, int k) const {
         return lds_at<uint32_t>(ttab, perm(s, lb.y, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
-    };
-    uint4 k = rk.get(0);
-    s0 ^= k.x; s1 ^= k.y; s2 ^= k.z; s3 ^= k.w;
+    }
+};
+
+// AES-256 rounds FIRST..13 (full) and 14 (final) on the state s0..s3 (after round FIRST-1).
+template <int FIRST, class RK>
+__device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, const TLook& T,
+                                               const RK& rk) {
+    uint4 k;
 #pragma unroll
-    for (int r = 1; r < 14; r++) {
+    for (int r = FIRST; r < 14; r++) {
         k = rk.get(r);
-        const uint32_t a0 = T0(s0, 0), a1 = T0(s1, 1), a2 = T2(s2, 2), a3 = T2(s3, 3);
-        const uint32_t b0 = T0(s1, 0), b1 = T0(s2, 1), b2 = T2(s3, 2), b3 = T2(s0, 3);
-        const uint32_t c0 = T0(s2, 0), c1 = T0(s3, 1), c2 = T2(s0, 2), c3 = T2(s1, 3);
-        const uint32_t d0 = T0(s3, 0), d1 = T0(s0, 1), d2 = T2(s1, 2), d3 = T2(s2, 3);
+        const uint32_t a0 = T.t0(s0, 0), a1 = T.t0(s1, 1), a2 = T.t2(s2, 2), a3 = T.t2(s3, 3);
+        const uint32_t b0 = T.t0(s1, 0), b1 = T.t0(s2, 1), b2 = T.t2(s3, 2), b3 = T.t2(s0, 3);
+        const uint32_t c0 = T.t0(s2, 0), c1 = T.t0(s3, 1), c2 = T.t2(s0, 2), c3 = T.t2(s1, 3);
+        const uint32_t d0 = T.t0(s3, 0), d1 = T.t0(s0, 1), d2 = T.t2(s1, 2), d3 = T.t2(s2, 3);
         // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k, T1 = rotl8 T0, T3 = rotl8 T2
         if constexpr (RK::kUniform) {
             s0 = x3s(a0, a2, k.x) ^ rotl8(a1 ^ a3);
@@ -168,10 +173,10 @@ __device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t
     }
     k = rk.get(14);
     // last round: SubBytes+ShiftRows; S[x] is byte 1 of T0[x]
-    const uint32_t a0 = T0(s0, 0), a1 = T0(s1, 1), a2 = T0(s2, 2), a3 = T0(s3, 3);
-    const uint32_t b0 = T0(s1, 0), b1 = T0(s2, 1), b2 = T0(s3, 2), b3 = T0(s0, 3);
-    const uint32_t c0 = T0(s2, 0), c1 = T0(s3, 1), c2 = T0(s0, 2), c3 = T0(s1, 3);
-    const uint32_t d0 = T0(s3, 0), d1 = T0(s0, 1), d2 = T0(s1, 2), d3 = T0(s2, 3);
+    const uint32_t a0 = T.t0(s0, 0), a1 = T.t0(s1, 1), a2 = T.t0(s2, 2), a3 = T.t0(s3, 3);
+    const uint32_t b0 = T.t0(s1, 0), b1 = T.t0(s2, 1), b2 = T.t0(s3, 2), b3 = T.t0(s0, 3);
+    const uint32_t c0 = T.t0(s2, 0), c1 = T.t0(s3, 1), c2 = T.t0(s0, 2), c3 = T.t0(s1, 3);
+    const uint32_t d0 = T.t0(s3, 0), d1 = T.t0(s0, 1), d2 = T.t0(s1, 2), d3 = T.t0(s2, 3);
     uint4 o;
     if constexpr (RK::kUniform) {
         o.x = x3s(perm(a1, a0, 0x0C0C0501u), perm(a3, a2, 0x05010C0Cu), k.x);
@@ -185,6 +190,52 @@ __device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t
         o.w = x3(perm(d1, d0, 0x0C0C0501u), perm(d3, d2, 0x05010C0Cu), k.w);
     }
     return o;
+}
+
+template <class RK>
+__device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, const TLook& T,
+                                              const RK& rk) {
+    const uint4 k = rk.get(0);
+    return aes256_rounds<1>(s0 ^ k.x, s1 ^ k.y, s2 ^ k.z, s3 ^ k.w, T, rk);
+}
+
+// Counter-mode caching. A packet's counter blocks are 00000000 || BE64(n) || BE32(ctr): with
+// ctr < 2^16 they differ only in state bytes 14 and 15 (word 3, bytes 2 and 3). Round 1 then
+// varies only through T2[byte 14] in column 1 and T3[byte 15] in column 0, and round 2 only
+// through the two varying columns of round 1: per block 2 + 8 lookups instead of 32. K (round 1)
+// and L (round 2) hold the packet-constant parts, round keys folded in.
+struct CtrConst {
+    uint4 K, L;
+    uint32_t k0w;  // word 3 of round key 0
+};
+
+template <class RK>
+__device__ __forceinline__ CtrConst aes_ctr_prep(uint32_t c1, uint32_t c2, const TLook& T, const RK& rk) {
+    const uint4 k0 = rk.get(0), k1 = rk.get(1), k2 = rk.get(2);
+    const uint32_t s0 = k0.x, s1 = c1 ^ k0.y, s2 = c2 ^ k0.z, s3 = k0.w;  // counter bytes = 0
+    CtrConst c;
+    c.k0w = k0.w;
+    c.K.x = T.t0(s0, 0) ^ rotl8(T.t0(s1, 1)) ^ T.t2(s2, 2) ^ k1.x;                      // minus T3[b3 s3]
+    c.K.y = T.t0(s1, 0) ^ rotl8(T.t0(s2, 1)) ^ rotl8(T.t2(s0, 3)) ^ k1.y;               // minus T2[b2 s3]
+    c.K.z = T.t0(s2, 0) ^ rotl8(T.t0(s3, 1) ^ T.t2(s1, 3)) ^ T.t2(s0, 2) ^ k1.z;
+    c.K.w = T.t0(s3, 0) ^ rotl8(T.t0(s0, 1) ^ T.t2(s2, 3)) ^ T.t2(s1, 2) ^ k1.w;
+    c.L.x = T.t2(c.K.z, 2) ^ rotl8(T.t2(c.K.w, 3)) ^ k2.x;
+    c.L.y = rotl8(T.t0(c.K.z, 1)) ^ T.t2(c.K.w, 2) ^ k2.y;
+    c.L.z = T.t0(c.K.z, 0) ^ rotl8(T.t0(c.K.w, 1)) ^ k2.z;
+    c.L.w = T.t0(c.K.w, 0) ^ rotl8(T.t2(c.K.z, 3)) ^ k2.w;
+    return c;
+}
+
+template <class RK>
+__device__ __forceinline__ uint4 aes256_ctr_block(const CtrConst& c, uint32_t ctr, const TLook& T, const RK& rk) {
+    const uint32_t s3 = c.k0w ^ bswap32(ctr);
+    const uint32_t t0 = c.K.x ^ rotl8(T.t2(s3, 3));
+    const uint32_t t1 = c.K.y ^ T.t2(s3, 2);
+    const uint32_t u0 = x3(c.L.x, T.t0(t0, 0), rotl8(T.t0(t1, 1)));
+    const uint32_t u1 = x3(c.L.y, T.t0(t1, 0), rotl8(T.t2(t0, 3)));
+    const uint32_t u2 = x3(c.L.z, T.t2(t0, 2), rotl8(T.t2(t1, 3)));
+    const uint32_t u3 = x3(c.L.w, T.t2(t1, 2), rotl8(T.t0(t0, 1)));
+    return aes256_rounds<3>(u0, u1, u2, u3, T, rk);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -321,9 +372,9 @@ __device__ __forceinline__ PktShape pkt_shape(const neb_desc& d, bool run) {
 }
 
 // One round of one packet lane: keystream, payload XOR, GHASH input block. Returns X (BE words).
-template <bool OPEN, uint32_t LPP, class RK>
+template <bool OPEN, uint32_t LPP, bool CTRC, class RK>
 __device__ __forceinline__ uint4 gcm_lane_round(const neb_desc& d, const PktShape& sh, uint32_t r, uint32_t l,
-                                                uint32_t c1, uint32_t c2, uint2 lb8, const uint2* ttab,
+                                                uint32_t c1, uint32_t c2, const CtrConst& cc, const TLook& T,
                                                 const RK& rk, uint8_t* arena, uint4& ej0) {
     const int32_t g = (int32_t)(LPP * r + l + 1u) - (int32_t)sh.pad;  // 1-based GHASH index
     const bool is_aad = g >= 1 && g <= (int32_t)sh.na;
@@ -332,9 +383,11 @@ __device__ __forceinline__ uint4 gcm_lane_round(const neb_desc& d, const PktShap
     const uint32_t k = (uint32_t)(g - (int32_t)sh.na);  // ciphertext block index (1-based)
     const uint32_t ctr = is_ct ? k + 1u : 1u;
 #ifdef NEB_ABLATE_AES
-    const uint4 ks = make_uint4(c1 ^ ctr, c2, ctr * 0x9E3779B9u, lb8.x);
+    const uint4 ks = make_uint4(c1 ^ ctr, c2, ctr * 0x9E3779B9u, cc.k0w);
 #else
-    const uint4 ks = aes256_block(0u, c1, c2, bswap32(ctr), lb8, ttab, rk);
+    uint4 ks;
+    if constexpr (CTRC) ks = aes256_ctr_block(cc, ctr, T, rk);
+    else ks = aes256_block(0u, c1, c2, bswap32(ctr), T, rk);
 #endif
     uint4 X = make_uint4(0, 0, 0, 0);
     if (is_aad) {
@@ -445,21 +498,30 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
     const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
     const uint32_t c2 = bswap32((uint32_t)d.counter);
+    const TLook T{ttab, lb8};
     uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
-    for (uint32_t r = 0; r < Rmax; r++) {
-        if (r < sh.R) {
-            // GHASH of the previous rounds (A·H^4) first, then this round's AES: one phase's
-            // registers at a time keeps the kernel at 4 waves/SIMD without spills
+    auto rounds = [&](auto ctrc) {
+        constexpr bool CTRC = decltype(ctrc)::value;
+        CtrConst cc{};
+        if constexpr (CTRC) cc = aes_ctr_prep(c1, c2, T, rk);
+        for (uint32_t r = 0; r < Rmax; r++) {
+            if (r < sh.R) {
+                // GHASH of the previous rounds (A·H^4) first, then this round's AES: one phase's
+                // registers at a time keeps the kernel at 4 waves/SIMD without spills
 #ifdef NEB_ABLATE_HORNER
-            const uint4 G = A;
+                const uint4 G = A;
 #else
-            const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A);
+                const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A);
 #endif
-            __builtin_amdgcn_sched_barrier(0);
-            const uint4 X = gcm_lane_round<OPEN, kLpp>(d, sh, r, l, c1, c2, lb8, ttab, rk, args.arena, ej0);
-            A = xor4(G, X);
+                __builtin_amdgcn_sched_barrier(0);
+                const uint4 X = gcm_lane_round<OPEN, kLpp, CTRC>(d, sh, r, l, c1, c2, cc, T, rk, args.arena, ej0);
+                A = xor4(G, X);
+            }
         }
-    }
+    };
+    // counter caching needs every block counter of every packet in the wave below 2^16
+    if (__all(sh.m + 1u < 65536u)) rounds(std::true_type{});
+    else rounds(std::false_type{});
     if (run) {
         // GHASH = Σ_l A_l·H^(4-l) = (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, same table in every lane
         uint4 V = quad_bcast4<0>(A);
