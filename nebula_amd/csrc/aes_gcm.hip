@@ -102,7 +102,10 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) {
 
 template <class T>
 __device__ __forceinline__ T lds_at(const void* base, uint32_t byte_off) {
-    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+    // every table offset is a multiple of sizeof(T): say so, or 16-byte reads get split into
+    // ds_read2/b96 pieces that conflict
+    return *reinterpret_cast<const T*>(
+        __builtin_assume_aligned(reinterpret_cast<const char*>(base) + byte_off, sizeof(T)));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -372,42 +375,69 @@ __device__ __forceinline__ PktShape pkt_shape(const neb_desc& d, bool run) {
 }
 
 // One round of one packet lane: keystream, payload XOR, GHASH input block. Returns X (BE words).
-template <bool OPEN, uint32_t LPP, bool CTRC, class RK>
-__device__ __forceinline__ uint4 gcm_lane_round(const neb_desc& d, const PktShape& sh, uint32_t r, uint32_t l,
-                                                uint32_t c1, uint32_t c2, const CtrConst& cc, const TLook& T,
-                                                const RK& rk, uint8_t* arena, uint4& ej0) {
-    const int32_t g = (int32_t)(LPP * r + l + 1u) - (int32_t)sh.pad;  // 1-based GHASH index
-    const bool is_aad = g >= 1 && g <= (int32_t)sh.na;
-    const bool is_ct = g > (int32_t)sh.na && g <= (int32_t)(sh.na + sh.m);
-    const bool is_len = g == (int32_t)sh.n;
-    const uint32_t k = (uint32_t)(g - (int32_t)sh.na);  // ciphertext block index (1-based)
-    const uint32_t ctr = is_ct ? k + 1u : 1u;
-#ifdef NEB_ABLATE_AES
-    const uint4 ks = make_uint4(c1 ^ ctr, c2, ctr * 0x9E3779B9u, cc.k0w);
-#else
-    uint4 ks;
-    if constexpr (CTRC) ks = aes256_ctr_block(cc, ctr, T, rk);
-    else ks = aes256_block(0u, c1, c2, bswap32(ctr), T, rk);
-#endif
-    uint4 X = make_uint4(0, 0, 0, 0);
-    if (is_aad) {
-        const uint32_t off = 16u * (uint32_t)(g - 1);
-        X = bswap4(load_block(arena + d.aad_off + off, min(16u, d.aad_len - off)));
+// Block roles of lane l in round r: 1-based GHASH index g and, for a ciphertext block, its counter.
+struct LaneBlock {
+    int32_t g;
+    bool is_aad, is_ct, is_len;
+    uint32_t k, ctr;
+};
+template <uint32_t LPP>
+__device__ __forceinline__ LaneBlock lane_block(const PktShape& sh, uint32_t r, uint32_t l) {
+    LaneBlock b;
+    b.g = (int32_t)(LPP * r + l + 1u) - (int32_t)sh.pad;
+    b.is_aad = b.g >= 1 && b.g <= (int32_t)sh.na;
+    b.is_ct = b.g > (int32_t)sh.na && b.g <= (int32_t)(sh.na + sh.m);
+    b.is_len = b.g == (int32_t)sh.n;
+    b.k = (uint32_t)(b.g - (int32_t)sh.na);  // ciphertext block index (1-based)
+    b.ctr = b.is_ct ? b.k + 1u : 1u;          // the length lane computes E_K(J0)
+    return b;
+}
+
+// Input block of lane block b: the AAD block or the payload block (zero-padded), else zero.
+__device__ __forceinline__ uint4 gcm_lane_load(const neb_desc& d, const LaneBlock& b, const uint8_t* arena) {
+    uint4 in = make_uint4(0, 0, 0, 0);
+    if (b.is_aad) {
+        const uint32_t off = 16u * (uint32_t)(b.g - 1);
+        in = load_block(arena + d.aad_off + off, min(16u, d.aad_len - off));
     }
-    if (is_ct) {
-        const uint32_t off = 16u * (k - 1u);
+    if (b.is_ct) {
+        const uint32_t off = 16u * (b.k - 1u);
+        in = load_block(arena + d.src_off + off, min(16u, d.len - off));
+    }
+    return in;
+}
+
+// Payload XOR and GHASH input of one block given its input and keystream. Returns X (BE words).
+template <bool OPEN>
+__device__ __forceinline__ uint4 gcm_lane_io(const neb_desc& d, const LaneBlock& b, uint4 in, uint4 ks,
+                                             uint8_t* arena, uint4& ej0) {
+    uint4 X = make_uint4(0, 0, 0, 0);
+    if (b.is_aad) X = bswap4(in);
+    if (b.is_ct) {
+        const uint32_t off = 16u * (b.k - 1u);
         const uint32_t nb = min(16u, d.len - off);
-        const uint4 in = load_block(arena + d.src_off + off, nb);
         const uint4 out = xor4(in, mask_block(ks, nb));
         store_block(arena + d.dst_off + off, out, nb);
         X = bswap4(OPEN ? in : out);
     }
-    if (is_len) {
+    if (b.is_len) {
         const uint64_t abits = (uint64_t)d.aad_len * 8u, cbits = (uint64_t)d.len * 8u;
         X = make_uint4((uint32_t)(abits >> 32), (uint32_t)abits, (uint32_t)(cbits >> 32), (uint32_t)cbits);
         ej0 = ks;
     }
     return X;
+}
+
+// Keystream block of lane block b.
+template <bool CTRC, class RK>
+__device__ __forceinline__ uint4 gcm_lane_ks(const LaneBlock& b, uint32_t c1, uint32_t c2, const CtrConst& cc,
+                                             const TLook& T, const RK& rk) {
+#ifdef NEB_ABLATE_AES
+    return make_uint4(c1 ^ b.ctr, c2, b.ctr * 0x9E3779B9u, cc.k0w);
+#else
+    if constexpr (CTRC) return aes256_ctr_block(cc, b.ctr, T, rk);
+    else return aes256_block(0u, c1, c2, bswap32(b.ctr), T, rk);
+#endif
 }
 
 // Tag finish on the packet's last lane, which holds E_K(J0) (seal: store; open: compare, zero
@@ -506,6 +536,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         if constexpr (CTRC) cc = aes_ctr_prep(c1, c2, T, rk);
         for (uint32_t r = 0; r < Rmax; r++) {
             if (r < sh.R) {
+                const LaneBlock b = lane_block<kLpp>(sh, r, l);
                 // GHASH of the previous rounds (A·H^4) first, then this round's AES: one phase's
                 // registers at a time keeps the kernel at 4 waves/SIMD without spills
 #ifdef NEB_ABLATE_HORNER
@@ -514,8 +545,9 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
-                const uint4 X = gcm_lane_round<OPEN, kLpp, CTRC>(d, sh, r, l, c1, c2, cc, T, rk, args.arena, ej0);
-                A = xor4(G, X);
+                const uint4 ks = gcm_lane_ks<CTRC>(b, c1, c2, cc, T, rk);
+                const uint4 in = gcm_lane_load(d, b, args.arena);
+                A = xor4(G, gcm_lane_io<OPEN>(d, b, in, ks, args.arena, ej0));
             }
         }
     };
@@ -543,7 +575,13 @@ __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rk
 
 // ---- one tunnel key for the whole batch -------------------------------------------------------
 
-constexpr int kSingleWaves = 8;
+#ifndef NEB_SINGLE_WAVES
+#define NEB_SINGLE_WAVES 8  // waves per workgroup (2 workgroups per CU)
+#endif
+#ifndef NEB_SINGLE_WPE
+#define NEB_SINGLE_WPE 4    // launch bound: waves per SIMD
+#endif
+constexpr int kSingleWaves = NEB_SINGLE_WAVES;
 constexpr int kSingleThreads = kSingleWaves * kWave;
 
 struct SingleLds {
@@ -553,7 +591,7 @@ struct SingleLds {
 };
 
 template <bool OPEN>
-__global__ __launch_bounds__(kSingleThreads, 4) void gcm_single_kernel(GcmArgs args) {
+__global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_kernel(GcmArgs args) {
     __shared__ SingleLds lds;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;

@@ -1,11 +1,16 @@
 #!/bin/bash
-# Build ablation variants of the engine (results WRONG by design; timing/counter study only).
+# Build engine variants for A/B timing (tools/ablate_gpu.sh). Usage: tools/ablate.sh "NAME:-DFLAG -DFLAG2" ...
+# NEB_ABLATE_* variants compute WRONG results by design (timing/counter study only).
 set -e
 cd "$(dirname "$0")/../nebula_amd"
 mkdir -p ../build_abl
-for v in BASE HORNER FINAL AES; do
-  def=""; [ "$v" != BASE ] && def="-DNEB_ABLATE_$v"
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result $def \
-     -shared -x hip csrc/aes_gcm.hip -x hip csrc/chacha_poly.hip -x hip csrc/sched.hip -x hip csrc/engine.cpp -o ../build_abl/lib_$v.so
+[ $# -eq 0 ] && set -- "BASE:" "HORNER:-DNEB_ABLATE_HORNER" "FINAL:-DNEB_ABLATE_FINAL" "AES:-DNEB_ABLATE_AES"
+: > ../build_abl/variants.txt
+for spec in "$@"; do
+  name=${spec%%:*}; defs=${spec#*:}
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result -Wno-unused-value $defs \
+     -shared -x hip csrc/aes_gcm.hip -x hip csrc/chacha_poly.hip -x hip csrc/sched.hip -x hip csrc/engine.cpp -o ../build_abl/lib_$name.so &
+  echo $name >> ../build_abl/variants.txt
 done
-ls -la ../build_abl
+wait
+ls ../build_abl

@@ -5,8 +5,9 @@ import torch
 from nebula_amd import workload as W
 from nebula_amd.batch import DeviceBatch, install_keys
 from nebula_amd.noiseutil import Engine
-b = W.config(1)
-eng = Engine(0, 16)
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+b = W.config(cfg) if cfg != 4 else W.make_batch(1, 65536, 4096, sizes=(90, 576, 1300), ratio=(7, 4, 1))
+eng = Engine(0, 4096)
 db = DeviceBatch(eng, b, install_keys(eng, b))
 for _ in range(3): db.seal()
 torch.cuda.synchronize()
