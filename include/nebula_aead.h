@@ -24,6 +24,13 @@
  *                            (connection_state.go:121-148) is an open with len = 0
  *   neb_header_encode/parse  header.Encode header/header.go:102-110, (*H).Parse :143-156
  *   NEB_REJECT_AFTER_MESSAGES noiseutil/cipher_state.go:11-15
+ *   neb_window_*             nebula.Bits, the anti-replay window: NewBits bits.go:28-50,
+ *                            Check :134-150, Update :152-262, its lost / duplicate / out-of-window
+ *                            counters (:23-25, network.packets.{lost,duplicate,out_of_window})
+ *   neb_rx_open_batch_host   ConnectionState.Decrypt (connection_state.go:99-119) over a whole
+ *                            receive batch (the recvmmsg flush, interface.go:381-413): window
+ *                            Check → DecryptDanger → window Update, results identical to the
+ *                            per-packet loop in arrival order
  */
 #ifndef NEBULA_AEAD_H
 #define NEBULA_AEAD_H
@@ -62,6 +69,9 @@ extern "C" {
 #define NEB_STATUS_AUTH_FAILED 1 /* open: tag mismatch, payload destination zeroed */
 #define NEB_STATUS_EXHAUSTED 2   /* seal: counter >= NEB_REJECT_AFTER_MESSAGES, nothing written */
 #define NEB_STATUS_BAD_KEY 3     /* key_id not installed / wrong algorithm / violates the uniform-key hint */
+#define NEB_STATUS_REPLAY 4      /* receive: the replay window refused the counter — ErrAlreadySeen
+                                    (connection_state.go:103-105,114-116); nothing decrypted when
+                                    refused before decryption */
 
 typedef struct neb_engine neb_engine; /* one per GPU: stream, key table, staging */
 typedef struct neb_cipher neb_cipher; /* one installed tunnel key (a CipherState) */
@@ -159,6 +169,27 @@ NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, ui
 NEB_API int neb_host_alloc(size_t bytes, void** out);
 NEB_API int neb_host_free(void* p);
 
+/* ---- replay window + batched receive ---------------------------------------------------------- */
+typedef struct neb_window neb_window; /* one per tunnel (ConnectionState.window, ReplayWindow = 8192) */
+/* NewBits(length): length must be a power of two (NEB_ERR_INVALID otherwise; Go panics). */
+NEB_API int neb_window_create(uint64_t length, neb_window** out);
+NEB_API int neb_window_destroy(neb_window* w);
+/* Check(i) / Update(i): 1 = accepted, 0 = refused, < 0 = error. Each call is atomic (the window
+ * carries its own lock, ConnectionState.decryptLock). */
+NEB_API int neb_window_check(neb_window* w, uint64_t counter);
+NEB_API int neb_window_update(neb_window* w, uint64_t counter);
+/* current counter and {lost, duplicate, out_of_window} counts since creation / the last reset. */
+NEB_API int neb_window_state(const neb_window* w, uint64_t* current, int64_t counters[3]);
+NEB_API int neb_window_slot(const neb_window* w, uint64_t slot); /* bit of slot (slot mod length) */
+NEB_API int neb_window_reset_counters(neb_window* w);
+/* Receive a batch in arrival order: for every packet, windows[desc.key_id] (NULL or key_id >=
+ * nwindows → NEB_STATUS_BAD_KEY) is checked, the packet opened in place (host arena, as
+ * neb_open_batch_host) and the window updated — statuses OK / AUTH_FAILED / BAD_KEY / REPLAY,
+ * window contents and counters identical to calling Decrypt packet by packet. All packets that
+ * pass go to the GPU as one batch; a packet refused by its window is not decrypted. */
+NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* windows, uint32_t nwindows,
+                                   const neb_desc* desc, uint32_t n, uint8_t* arena, size_t arena_len,
+                                   int32_t* status, uint32_t key_hint);
 /* ---- header (the AAD) --------------------------------------------------------------------- */
 
 NEB_API void neb_header_encode(uint8_t b[16], uint8_t version, uint8_t type, uint8_t subtype, uint32_t remote_index,

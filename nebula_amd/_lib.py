@@ -32,6 +32,7 @@ STATUS_OK = 0
 STATUS_AUTH_FAILED = 1
 STATUS_EXHAUSTED = 2
 STATUS_BAD_KEY = 3
+STATUS_REPLAY = 4
 
 OVERHEAD = 16
 HEADER_LEN = 16
@@ -71,6 +72,14 @@ SIGNATURES = {
     "neb_header_encode": (None, [_u8p, C.c_uint8, C.c_uint8, C.c_uint8, _u32, _u64]),
     "neb_header_parse": (_i, [_u8p, _sz, _u8p, _u8p, _u8p, C.POINTER(C.c_uint16), C.POINTER(_u32),
                               C.POINTER(_u64)]),
+    "neb_window_create": (_i, [_u64, C.POINTER(_vp)]),
+    "neb_window_destroy": (_i, [_vp]),
+    "neb_window_check": (_i, [_vp, _u64]),
+    "neb_window_update": (_i, [_vp, _u64]),
+    "neb_window_state": (_i, [_vp, C.POINTER(_u64), C.POINTER(C.c_int64)]),
+    "neb_window_slot": (_i, [_vp, _u64]),
+    "neb_window_reset_counters": (_i, [_vp]),
+    "neb_rx_open_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _u32]),
 }
 
 _lib = None

@@ -1,0 +1,142 @@
+"""GPU: the batched receive path (neb_rx_open_batch_host — ConnectionState.Decrypt over a whole
+recvmmsg flush, connection_state.go:99-119) against the oracle's packet-by-packet receive loop
+(oracle/replay_oracle.py rx_sequential + oracle AEAD): statuses, every arena byte (refused packets
+untouched, forged ones zeroed, accepted ones decrypted in place), window state and counters."""
+import random
+
+import numpy as np
+import pytest
+
+from nebula_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+SLOT = 16 + 1400 + 16
+
+
+def _build(oracle_mod, alg, keys, arrivals, seed):
+    """arrivals: [(tunnel, counter, forged)] -> (arena, desc (tunnel index in key_id), payloads)."""
+    rng = random.Random(seed)
+    n = len(arrivals)
+    arena = np.zeros(n * SLOT, np.uint8)
+    desc = np.zeros(n, dtype=L.DESC_DTYPE)
+    pts = []
+    for i, (t, ctr, forged) in enumerate(arrivals):
+        ln = rng.choice([0, 1, 15, 16, 17, 100, 576, 1300, 1400]) if i % 5 else 1300
+        pt = bytes(rng.getrandbits(8) for _ in range(ln))
+        hdr = oracle_mod.header_encode(1, 1, 0, 0x1000 + t, ctr)
+        ct = bytearray(oracle_mod.seal(alg, keys[t], oracle_mod.nonce(alg, ctr), hdr, pt))
+        if forged:
+            ct[rng.randrange(len(ct))] ^= 1 << rng.randrange(8)
+        base = i * SLOT
+        arena[base:base + 16] = np.frombuffer(hdr, np.uint8)
+        arena[base + 16:base + 16 + len(ct)] = np.frombuffer(bytes(ct), np.uint8)
+        desc[i] = (base + 16, base + 16, base, ctr, ln, 16, t, 0)
+        pts.append(pt)
+    return arena, desc, pts
+
+
+def _expected(oracle_mod, R, alg, keys, arrivals, arena, pts, window_len, seeds, installed):
+    wins = {t: R.Bits(window_len) for t in range(len(keys)) if t in seeds}
+    for t, mi in seeds.items():
+        for i in range(1, mi + 1):
+            wins[t].update(i)
+    verdicts = [(L.STATUS_OK if not forged else L.STATUS_AUTH_FAILED) if t in installed else L.STATUS_BAD_KEY
+                for (t, _, forged) in arrivals]
+    st, dec = R.rx_sequential(wins, [a[0] for a in arrivals], [a[1] for a in arrivals], verdicts)
+    exp = arena.copy()
+    for i, ((t, ctr, forged), s, d) in enumerate(zip(arrivals, st, dec)):
+        if not d or verdicts[i] == L.STATUS_BAD_KEY:
+            continue
+        base = i * SLOT + 16
+        ln = len(pts[i])
+        exp[base:base + ln] = 0 if forged else np.frombuffer(pts[i], np.uint8)
+    return st, exp, wins
+
+
+def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=None, installed=None, seed=1):
+    import replay_oracle as R
+    from nebula_amd.connection_state import Bits, rx_open_batch
+    from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
+
+    rng = random.Random(seed * 31 + alg)
+    keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(ntunnels)]
+    seeds = {t: 2 for t in range(ntunnels)} if seeds is None else seeds
+    installed = set(range(ntunnels)) if installed is None else installed
+    cf = CipherAESGCM if alg == L.ALG_AESGCM else CipherChaChaPoly
+    ciphers = {t: cf.Cipher(engine, keys[t]) for t in installed}
+    # tunnels whose key is not installed get a slot id from the top of the table (never allocated here)
+    slot_of = {t: (ciphers[t].key_id if t in ciphers else engine.max_keys - 1 - t) for t in range(ntunnels)}
+    try:
+        arena, desc, pts = _build(oracle_mod, alg, keys, arrivals, seed)
+        exp_status, exp_arena, owins = _expected(oracle_mod, R, alg, keys, arrivals, arena, pts, window_len, seeds,
+                                                 installed)
+        windows = [None] * engine.max_keys
+        ewins = {}
+        for t, mi in seeds.items():
+            w = Bits(window_len)
+            for i in range(1, mi + 1):
+                w.Update(i)
+            ewins[t] = w
+            windows[slot_of[t]] = w
+        d = desc.copy()
+        d["key_id"] = [slot_of[int(t)] for t in desc["key_id"]]
+        got = rx_open_batch(engine, alg, windows, d, arena)
+        assert got.tolist() == exp_status
+        assert np.array_equal(arena, exp_arena)
+        for t, w in ewins.items():
+            o = owins[t]
+            assert (w.current, w.lost, w.dupe, w.out_of_window) == (o.current, o.lost, o.dupe, o.out_of_window)
+            assert [bool(x) for x in w.snapshot()] == o.snapshot()
+        return got
+    finally:
+        for c in ciphers.values():
+            c.destroy()
+
+
+ARRIVALS = [
+    (0, 3, False), (0, 4, False), (1, 3, False), (0, 5, False),
+    (0, 4, False),                      # duplicate inside the batch: refused, never decrypted
+    (1, 5, False), (1, 4, False),       # reorder inside the window: accepted
+    (0, 7, True), (0, 7, False),        # forged copy first, genuine second: forged zeroed, genuine accepted
+    (0, 6, False), (0, 6, False),       # duplicate
+    (2, 3, True), (2, 3, True), (2, 3, False),  # two forgeries then the genuine one
+    (1, 2, False),                      # handshake counter: pre-marked seen (connection_state.go:70-72)
+    (0, 9003, False), (0, 10, False),   # jump past the window, then a stale counter: out of window
+    (1, 4, False),                      # replay of an accepted packet
+    (0, 9002, False), (0, 9003, True),  # in-window backfill; forged duplicate of the current counter
+]
+
+
+@pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
+def test_rx_batch_matches_sequential_decrypt(engine, oracle_mod, alg):
+    st = _run(engine, oracle_mod, alg, ARRIVALS)
+    assert (st == L.STATUS_REPLAY).sum() >= 5 and (st == L.STATUS_AUTH_FAILED).sum() >= 3
+
+
+def test_rx_batch_missing_window_and_key(engine, oracle_mod):
+    """Tunnel 2 has no window (no ConnectionState): BAD_KEY, untouched. Tunnel 1's key is not
+    installed: its window passes the packet, the engine refuses the key, the window is not updated."""
+    arr = [(0, 3, False), (2, 3, False), (1, 3, False), (1, 4, False), (0, 4, False)]
+    st = _run(engine, oracle_mod, L.ALG_AESGCM, arr, seeds={0: 2, 1: 2}, installed={0, 2})
+    assert st.tolist() == [0, L.STATUS_BAD_KEY, L.STATUS_BAD_KEY, L.STATUS_BAD_KEY, 0]
+
+
+def test_rx_batch_random_traffic(engine, oracle_mod):
+    """A long random receive stream over 8 tunnels and a small window: loss, reordering, jumps,
+    replays and forgeries, checked packet by packet against the sequential oracle."""
+    rng = random.Random(7)
+    cur = [2] * 8
+    arr = []
+    for _ in range(3000):
+        t = rng.randrange(8)
+        r = rng.random()
+        if r < 0.6:
+            cur[t] += 1 + (rng.random() < 0.1) * rng.randrange(1, 40)
+            c = cur[t]
+        elif r < 0.85:
+            c = max(1, cur[t] - rng.randrange(0, 80))
+        else:
+            c = cur[t] + rng.randrange(1, 30)
+        arr.append((t, c, rng.random() < 0.05))
+    _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=8, window_len=64, seed=3)

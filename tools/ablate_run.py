@@ -6,7 +6,12 @@ from nebula_amd import workload as W
 from nebula_amd.batch import DeviceBatch, install_keys
 from nebula_amd.noiseutil import Engine
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 1
-b = W.config(cfg) if cfg != 4 else W.make_batch(1, 65536, 4096, sizes=(90, 576, 1300), ratio=(7, 4, 1))
+if cfg == 4:
+    b = W.make_batch(1, 65536, 4096, sizes=(90, 576, 1300), ratio=(7, 4, 1))
+elif cfg == 5:  # 61440 wave-groups: divides evenly over 16, 20 and 24 waves per CU
+    b = W.make_batch(1, 983040, 1)
+else:
+    b = W.config(cfg)
 eng = Engine(0, 4096)
 db = DeviceBatch(eng, b, install_keys(eng, b))
 for _ in range(3): db.seal()
@@ -15,4 +20,4 @@ s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True
 s.record()
 for _ in range(20): db.seal()
 e.record(); torch.cuda.synchronize()
-print(os.environ.get("NEB_LIB_PATH"), "seal ms", s.elapsed_time(e) / 20)
+print(os.environ.get("NEB_LIB_PATH"), "seal ms", s.elapsed_time(e) / 20, "pkts", b.n)
