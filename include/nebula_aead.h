@@ -27,6 +27,11 @@
  *   neb_window_*             nebula.Bits, the anti-replay window: NewBits bits.go:28-50,
  *                            Check :134-150, Update :152-262, its lost / duplicate / out-of-window
  *                            counters (:23-25, network.packets.{lost,duplicate,out_of_window})
+ *   neb_tx_seal_batch        sendInsideMessage (inside.go:154-240) over a batch of TUN reads:
+ *                            decodeRead (overlay/tio/tio_gso_linux.go:231-280), SegmentSuperpacket
+ *                            (overlay/tio/tun_linux_offload.go:46-60, virtio/segment_linux.go),
+ *                            sendInsideEncrypt (inside.go:123-146) into SendBatch slots
+ *                            (overlay/batch/tx_batch.go:15-59)
  *   neb_rx_open_batch_host   ConnectionState.Decrypt (connection_state.go:99-119) over a whole
  *                            receive batch (the recvmmsg flush, interface.go:381-413): window
  *                            Check → DecryptDanger → window Update, results identical to the
@@ -190,6 +195,68 @@ NEB_API int neb_window_reset_counters(neb_window* w);
 NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* windows, uint32_t nwindows,
                                    const neb_desc* desc, uint32_t n, uint8_t* arena, size_t arena_len,
                                    int32_t* status, uint32_t key_hint);
+/* ---- transmit: TUN reads (IP packets, TSO/USO superpackets) -> sealed wire packets ------------ */
+/* virtio_net_hdr values (linux/virtio_net.h), as the TUN hands them over (overlay/tio/virtio/header_linux.go) */
+#define NEB_VNET_F_NEEDS_CSUM 1
+#define NEB_VNET_F_RSC_INFO 4
+#define NEB_GSO_NONE 0
+#define NEB_GSO_TCPV4 1
+#define NEB_GSO_TCPV6 4
+#define NEB_GSO_UDP_L4 5
+#define NEB_GSO_ECN 0x80
+/* Per-packet status of a TX batch (besides NEB_STATUS_OK / NEB_STATUS_BAD_KEY = the tunnel has no
+ * key, `if ci.eKey == nil { return }`, inside.go:155-158). */
+#define NEB_STATUS_INVALID 5  /* virtio / IP header rejected (decodeRead, CheckValid, CorrectHdrLen,
+                                 SegmentTCP/UDP, FinishChecksum errors): dropped, no counter used */
+#define NEB_STATUS_NO_SPACE 6 /* the output arena or the wire array is full: dropped */
+/* One TUN read: an IP packet at in_off of the input arena with its virtio_net_hdr, bound for a tunnel. */
+typedef struct neb_tx_packet {
+    uint64_t in_off;
+    uint32_t len;
+    uint32_t tunnel;     /* index into the tunnel array */
+    uint8_t vnet_flags;  /* virtio_net_hdr.flags */
+    uint8_t gso_type;    /* virtio_net_hdr.gso_type (the ECN qualifier allowed) */
+    uint16_t hdr_len;    /* virtio_net_hdr.hdr_len (re-derived from the TCP header, CorrectHdrLen) */
+    uint16_t gso_size;
+    uint16_t csum_start;
+    uint16_t csum_offset;
+    uint16_t reserved;
+} neb_tx_packet;
+/* The sending side of one tunnel (ConnectionState + HostInfo fields the TX path reads). */
+typedef struct neb_tx_tunnel {
+    uint64_t message_counter; /* ConnectionState.messageCounter: the last counter used; the batch
+                                 advances it by one per segment, as inside.go:127 does */
+    uint32_t key_id;          /* the eKey's key_id (neb_cipher_key_id); NEB_KEYS_MIXED = no eKey */
+    uint32_t remote_index;    /* hostinfo.remoteIndexId, written into every header */
+} neb_tx_tunnel;
+/* One wire packet: header(16) || ct || tag(16) at out_off (16-byte aligned) of the output arena. */
+typedef struct neb_tx_wire {
+    uint64_t out_off;
+    uint64_t counter;
+    uint32_t len;     /* 16 + segment + 16 */
+    uint32_t packet;  /* index of the neb_tx_packet it came from */
+    uint32_t segment; /* segment index within that packet */
+    uint32_t reserved;
+} neb_tx_wire;
+/* sendInsideMessage (inside.go:154-240) for a whole batch of TUN reads: every packet is validated
+ * and segmented exactly as decodeRead + SegmentSuperpacket do (TSO: per-segment seq, CWR/FIN/PSH,
+ * IPv4 ID and lengths, IPv4 and TCP checksums; USO: lengths and UDP checksum; plain packets with
+ * NEEDS_CSUM get FinishChecksum), each segment takes the next counter of its tunnel in batch order,
+ * gets header.Encode(Message, remote_index, counter) and is sealed in place: wires[i] describes the
+ * i-th segment of the batch (packet order, then segment order), wire_status[i] is its seal status
+ * (NEB_STATUS_EXHAUSTED = dropped, inside.go:137-145, its counter still used). The segment count is
+ * written to *d_nwires. Device pointers; asynchronous on `stream`. tunnels[].message_counter is
+ * advanced on the device. */
+NEB_API int neb_tx_seal_batch(neb_engine* e, int alg, neb_tx_tunnel* d_tunnels, uint32_t ntunnels,
+                              const neb_tx_packet* d_packets, uint32_t npackets, const uint8_t* d_in,
+                              uint8_t* d_out, size_t out_cap, neb_tx_wire* d_wires, int32_t* d_wire_status,
+                              uint32_t max_wires, uint32_t* d_nwires, int32_t* d_packet_status, uint32_t key_hint,
+                              void* stream);
+/* The same over host memory (synchronous): the input span is uploaded, the outputs downloaded. */
+NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnels, uint32_t ntunnels,
+                                   const neb_tx_packet* packets, uint32_t npackets, const uint8_t* in, size_t in_len,
+                                   uint8_t* out, size_t out_cap, neb_tx_wire* wires, int32_t* wire_status,
+                                   uint32_t max_wires, uint32_t* nwires, int32_t* packet_status, uint32_t key_hint);
 /* ---- header (the AAD) --------------------------------------------------------------------- */
 
 NEB_API void neb_header_encode(uint8_t b[16], uint8_t version, uint8_t type, uint8_t subtype, uint32_t remote_index,

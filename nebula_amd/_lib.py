@@ -33,6 +33,8 @@ STATUS_AUTH_FAILED = 1
 STATUS_EXHAUSTED = 2
 STATUS_BAD_KEY = 3
 STATUS_REPLAY = 4
+STATUS_INVALID = 5
+STATUS_NO_SPACE = 6
 
 OVERHEAD = 16
 HEADER_LEN = 16
@@ -80,6 +82,9 @@ SIGNATURES = {
     "neb_window_slot": (_i, [_vp, _u64]),
     "neb_window_reset_counters": (_i, [_vp]),
     "neb_rx_open_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _u32]),
+    "neb_tx_seal_batch": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
+    "neb_tx_seal_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _vp, _u32, _vp, _vp,
+                                    _u32]),
 }
 
 _lib = None

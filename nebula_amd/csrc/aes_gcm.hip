@@ -382,6 +382,7 @@ struct GcmArgs {
     uint32_t max_keys;
     uint32_t key_hint;     // SINGLE: the one key_id
     int32_t* status;
+    const uint32_t* npkt_dev;  // optional: the batch's packet count in device memory (min with npkt)
 };
 
 struct PktShape {
@@ -632,10 +633,12 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     const RkRegs rk{rks};
     const GhFull gh{lds.full, lds.shoup_h};
 
-    const uint32_t ngroups = (args.npkt + kPpw - 1u) / kPpw;
+    uint32_t npkt = args.npkt;
+    if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
+    const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
     for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
         const uint32_t p = grp * kPpw + lane / kLpp;
-        gcm_packet_group<OPEN>(args, p, p < args.npkt, args.key_hint, true, rk, gh, lds.ttab, lb8, lane);
+        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, true, rk, gh, lds.ttab, lb8, lane);
     }
 }
 
@@ -819,8 +822,8 @@ static hipError_t launch_grid(K kern, int threads, uint32_t work_waves, int cu_c
 // One tunnel key (key_hint) for every descriptor.
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                           int32_t* d_status, int cu_count, hipStream_t s) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status};
+                                           int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s) {
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
     return open ? launch_grid(neb::gcm_single_kernel<true>, neb::kSingleThreads, groups, cu_count, s, a)
                 : launch_grid(neb::gcm_single_kernel<false>, neb::kSingleThreads, groups, cu_count, s, a);
@@ -832,7 +835,7 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_sorted, const uint4* d_chunks,
                                             const uint32_t* d_nchunks, uint32_t max_chunks, int cu_count,
                                             hipStream_t s) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status};
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr};
     neb::ChunkArgs ca{d_sorted, d_chunks, d_nchunks, max_chunks};
     const uint32_t bound = (n + neb::kPpw - 1u) / neb::kPpw;  // enough waves for the typical chunk count
     return open ? launch_grid(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, a, ca)

@@ -187,6 +187,7 @@ struct ChachaArgs {
     uint32_t max_keys;
     uint32_t key_hint;
     int32_t* status;
+    const uint32_t* npkt_dev;  // optional: the batch's packet count in device memory (min with npkt)
 };
 
 template <bool OPEN>
@@ -198,12 +199,14 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
     const uint32_t j = l >> 2;      // quad within the packet
     const uint32_t q = lane >> 4;   // packet slot within the wave
     const uint32_t pbase = lane & ~15u;  // first lane of this packet
-    const uint32_t ngroups = (args.npkt + 3u) >> 2;
+    uint32_t npkt = args.npkt;
+    if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
+    const uint32_t ngroups = (npkt + 3u) >> 2;
     constexpr uint32_t kConst[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
 
     for (uint32_t grp = blockIdx.x * kChWavesPerWG + wave; grp < ngroups; grp += gridDim.x * kChWavesPerWG) {
         const uint32_t p = grp * 4u + q;
-        const bool valid = p < args.npkt;
+        const bool valid = p < npkt;
         neb_desc d = {};
         if (valid) d = args.desc[p];
         uint32_t st = NEB_STATUS_OK;
@@ -342,7 +345,7 @@ static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStrea
 
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                       int32_t* d_status, int cu_count, hipStream_t s) {
-    neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status};
+                                       int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s) {
+    neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n};
     return open ? launch_chacha<true>(a, cu_count, s) : launch_chacha<false>(a, cu_count, s);
 }

@@ -15,11 +15,12 @@
 #include "../../include/nebula_aead.h"
 #include "layout.hpp"
 #include "sched.hpp"
+#include "tx.hpp"
 
 extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                           int32_t* d_status, int cu_count, hipStream_t s);
+                                           int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s);
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
@@ -29,7 +30,7 @@ extern "C" hipError_t neb_gcm_probe(void);
 extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                       int32_t* d_status, int cu_count, hipStream_t s);
+                                       int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s);
 
 namespace {
 
@@ -64,6 +65,18 @@ struct SchedSpace {
     std::mutex mu;
 };
 
+// Device workspace of the transmit batch (tx.hpp) plus device staging for its host-memory form.
+struct TxSpace {
+    uint8_t* mem = nullptr;
+    size_t bytes = 0;
+    uint32_t n_cap = 0, tun_cap = 0, wire_cap = 0;
+    neb::TxWs ws{};
+    hipEvent_t done = nullptr;
+    uint8_t* d_io = nullptr;  // neb_tx_seal_batch_host staging
+    size_t io_cap = 0;
+    std::mutex mu;
+};
+
 struct neb_engine {
     int device = 0;
     int cu_count = 0;
@@ -82,6 +95,7 @@ struct neb_engine {
     PipeSlot pipe[kPipeStreams];
 
     SchedSpace sched;
+    TxSpace tx;
 };
 
 struct neb_cipher {
@@ -193,6 +207,9 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
     }
     if (e->sched.done) { hipEventSynchronize(e->sched.done); hipEventDestroy(e->sched.done); }
     if (e->sched.mem) hipFree(e->sched.mem);
+    if (e->tx.done) { hipEventSynchronize(e->tx.done); hipEventDestroy(e->tx.done); }
+    if (e->tx.mem) hipFree(e->tx.mem);
+    if (e->tx.d_io) hipFree(e->tx.d_io);
     if (e->d_keys) hipFree(e->d_keys);
     if (e->h_stage) hipHostFree(e->h_stage);
     if (e->d_stage) hipFree(e->d_stage);
@@ -323,25 +340,28 @@ static hipError_t sched_reserve(neb_engine* e, uint32_t n) {
     return hipSuccess;
 }
 
+// d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
+// only known on the device, e.g. the segments of a TX batch).
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
-                               int32_t* d_status, uint32_t key_hint, hipStream_t s) {
+                               int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
-            return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status,
+            return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
                                         e->cu_count, s);
         // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
         SchedSpace& sp = e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
         hipError_t err = sched_reserve(e, n);
         if (err == hipSuccess) err = hipStreamWaitEvent(s, sp.done, 0);
-        if (err == hipSuccess) err = neb_sched_build(d_desc, n, e->max_keys, 4u, &sp.ws, s);
+        if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                         sp.ws.chunks, sp.ws.counters + 1, sp.ws.max_chunks, e->cu_count, s);
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
         return err;
     }
-    return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, e->cu_count, s);
+    return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n, e->cu_count,
+                            s);
 }
 
 // One packet through the device: [desc | status | aad | payload (+tag)] in one staging buffer.
@@ -534,6 +554,143 @@ NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, ui
 NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
                                 size_t arena_len, int32_t* status, uint32_t key_hint) {
     return batch_host(e, alg, 1, desc, n, arena, arena_len, status, key_hint);
+}
+
+// ---- transmit batch (tx.hip) ------------------------------------------------------------------
+
+static hipError_t tx_reserve(neb_engine* e, uint32_t n, uint32_t ntun, uint32_t max_wires) {
+    TxSpace& tx = e->tx;
+    if (!tx.done) {
+        hipError_t err = hipEventCreateWithFlags(&tx.done, hipEventDisableTiming);
+        if (err != hipSuccess) return err;
+    }
+    if (tx.mem && n <= tx.n_cap && ntun <= tx.tun_cap && max_wires <= tx.wire_cap) return hipSuccess;
+    const uint32_t nc = std::max({n, tx.n_cap, 1024u}), tc = std::max({ntun, tx.tun_cap, 64u});
+    const uint32_t wc = std::max({max_wires, tx.wire_cap, 1024u});
+    size_t cub = 0;
+    const size_t bytes = neb_tx_ws_bytes(nc, tc, wc, &cub);
+    hipError_t err = hipEventSynchronize(tx.done);  // the old workspace may still be in use
+    if (err != hipSuccess) return err;
+    if (tx.mem) hipFree(tx.mem);
+    tx.mem = nullptr;
+    tx.n_cap = tx.tun_cap = tx.wire_cap = 0;
+    err = hipMalloc((void**)&tx.mem, bytes);
+    if (err != hipSuccess) return err;
+    neb::tx_ws_layout(nc, tc, wc, cub, tx.mem, &tx.ws);
+    tx.bytes = bytes;
+    tx.n_cap = nc;
+    tx.tun_cap = tc;
+    tx.wire_cap = wc;
+    return hipSuccess;
+}
+
+// caller holds e->tx.mu
+static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, const neb_tx_packet* d_pk, uint32_t npk,
+                  const uint8_t* d_in, uint8_t* d_out, size_t out_cap, neb_tx_wire* d_wires, int32_t* d_wire_status,
+                  uint32_t max_wires, uint32_t* d_nwires, int32_t* d_pk_status, uint32_t key_hint, hipStream_t s) {
+    TxSpace& tx = e->tx;
+    HIP_TRY(tx_reserve(e, npk, ntun, max_wires));
+    HIP_TRY(hipStreamWaitEvent(s, tx.done, 0));
+    HIP_TRY(neb_tx_plan(d_pk, npk, d_in, d_tun, ntun, e->d_keys, e->max_keys, alg, &tx.ws, out_cap, max_wires,
+                        d_pk_status, d_nwires, s));
+    HIP_TRY(neb_tx_segment(d_pk, npk, d_in, d_tun, d_out, &tx.ws, d_wires, d_nwires, max_wires, e->cu_count, s));
+    HIP_TRY(launch_batch(e, alg, 0, tx.ws.seal_desc, max_wires, d_out, d_wire_status, key_hint, s, d_nwires));
+    HIP_TRY(neb_tx_finish(d_tun, ntun, &tx.ws, s));
+    HIP_TRY(hipEventRecord(tx.done, s));
+    return NEB_OK;
+}
+
+NEB_API int neb_tx_seal_batch(neb_engine* e, int alg, neb_tx_tunnel* d_tunnels, uint32_t ntunnels,
+                              const neb_tx_packet* d_packets, uint32_t npackets, const uint8_t* d_in,
+                              uint8_t* d_out, size_t out_cap, neb_tx_wire* d_wires, int32_t* d_wire_status,
+                              uint32_t max_wires, uint32_t* d_nwires, int32_t* d_packet_status, uint32_t key_hint,
+                              void* stream) {
+    int rc = check_batch(e, alg, key_hint);
+    if (rc != NEB_OK) return rc;
+    if (!d_nwires || (npackets && (!d_packets || !d_in || !d_packet_status || !d_tunnels)) ||
+        (max_wires && (!d_out || !d_wires || !d_wire_status)))
+        return NEB_ERR_INVALID;
+    hipSetDevice(e->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (npackets == 0) {
+        HIP_TRY(hipMemsetAsync(d_nwires, 0, sizeof(uint32_t), s));
+        return NEB_OK;
+    }
+    std::lock_guard<std::mutex> g(e->tx.mu);
+    return tx_run(e, alg, d_tunnels, ntunnels, d_packets, npackets, d_in, d_out, out_cap, d_wires, d_wire_status,
+                  max_wires, d_nwires, d_packet_status, key_hint, s);
+}
+
+NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnels, uint32_t ntunnels,
+                                   const neb_tx_packet* packets, uint32_t npackets, const uint8_t* in, size_t in_len,
+                                   uint8_t* out, size_t out_cap, neb_tx_wire* wires, int32_t* wire_status,
+                                   uint32_t max_wires, uint32_t* nwires, int32_t* packet_status, uint32_t key_hint) {
+    int rc = check_batch(e, alg, key_hint);
+    if (rc != NEB_OK) return rc;
+    if (!nwires || (npackets && (!packets || !in || !packet_status || (ntunnels && !tunnels))) ||
+        (max_wires && (!out || !wires || !wire_status)))
+        return NEB_ERR_INVALID;
+    *nwires = 0;
+    if (npackets == 0) return NEB_OK;
+    // the input span the packets touch, uploaded once
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t i = 0; i < npackets; i++) {
+        lo = std::min(lo, packets[i].in_off);
+        hi = std::max(hi, packets[i].in_off + packets[i].len);
+    }
+    if (hi > in_len) return NEB_ERR_INVALID;
+    lo &= ~(uint64_t)15;
+    const size_t span = (size_t)(hi - lo);
+    const size_t o_tun = 0, o_pk = align_up((size_t)ntunnels * sizeof(neb_tx_tunnel), 256);
+    const size_t o_in = o_pk + align_up((size_t)npackets * sizeof(neb_tx_packet), 256);
+    const size_t o_out = o_in + align_up(span, 256);
+    const size_t o_w = o_out + align_up(out_cap, 256);
+    const size_t o_ws = o_w + align_up((size_t)max_wires * sizeof(neb_tx_wire), 256);
+    const size_t o_ps = o_ws + align_up((size_t)max_wires * 4, 256);
+    const size_t o_n = o_ps + align_up((size_t)npackets * 4, 256);
+    const size_t total = o_n + 256;
+    std::vector<neb_tx_packet> rebased(packets, packets + npackets);
+    for (auto& p : rebased) p.in_off -= lo;
+    std::lock_guard<std::mutex> g(e->tx.mu);
+    hipSetDevice(e->device);
+    TxSpace& tx = e->tx;
+    hipStream_t s = e->stream;
+    if (total > tx.io_cap) {
+        if (tx.done) HIP_TRY(hipEventSynchronize(tx.done));
+        if (tx.d_io) hipFree(tx.d_io);
+        tx.d_io = nullptr;
+        tx.io_cap = 0;
+        const size_t cap = align_up(total, 1 << 20);
+        HIP_TRY(hipMalloc((void**)&tx.d_io, cap));
+        tx.io_cap = cap;
+    }
+    uint8_t* d = tx.d_io;
+    auto* d_tun = (neb_tx_tunnel*)(d + o_tun);
+    auto* d_pk = (neb_tx_packet*)(d + o_pk);
+    auto* d_wires = (neb_tx_wire*)(d + o_w);
+    auto* d_wst = (int32_t*)(d + o_ws);
+    auto* d_pst = (int32_t*)(d + o_ps);
+    auto* d_n = (uint32_t*)(d + o_n);
+    if (ntunnels) HIP_TRY(hipMemcpyAsync(d_tun, tunnels, ntunnels * sizeof(neb_tx_tunnel), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_pk, rebased.data(), npackets * sizeof(neb_tx_packet), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_in, in + lo, span, hipMemcpyHostToDevice, s));
+    rc = tx_run(e, alg, d_tun, ntunnels, d_pk, npackets, d + o_in, d + o_out, out_cap, d_wires, d_wst, max_wires, d_n,
+                d_pst, key_hint, s);
+    if (rc != NEB_OK) return rc;
+    unsigned long long tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(tot, tx.ws.totals, sizeof tot, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(packet_status, d_pst, npackets * 4, hipMemcpyDeviceToHost, s));
+    if (ntunnels) HIP_TRY(hipMemcpyAsync(tunnels, d_tun, ntunnels * sizeof(neb_tx_tunnel), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t nw = (uint32_t)tot[0];
+    if (nw) {
+        HIP_TRY(hipMemcpyAsync(wires, d_wires, nw * sizeof(neb_tx_wire), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(wire_status, d_wst, nw * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(out, d + o_out, (size_t)tot[1], hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    *nwires = nw;
+    return NEB_OK;
 }
 
 NEB_API int neb_host_alloc(size_t bytes, void** out) {

@@ -14,8 +14,9 @@ __device__ __forceinline__ uint32_t size_class(const neb_desc& d, uint32_t lpp) 
 }
 
 // pass 1: histogram of (size class, key) bins; keys outside the table go to key index max_keys
-__global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, uint32_t max_keys, uint32_t lpp,
-                                  SchedWs ws) {
+__global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn,
+                                  uint32_t max_keys, uint32_t lpp, SchedWs ws) {
+    if (dn) n = min(n, *dn);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const neb_desc d = desc[i];
         const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
@@ -42,7 +43,8 @@ __global__ void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
 }
 
 // pass 3: scatter packet indices into their bin's range
-__global__ void sched_scatter_kernel(uint32_t n, SchedWs ws) {
+__global__ void sched_scatter_kernel(uint32_t n, const uint32_t* dn, SchedWs ws) {
+    if (dn) n = min(n, *dn);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t b = ws.binof[i];
         const uint32_t pos = atomicAdd(&ws.fill[b], 1u);
@@ -52,8 +54,8 @@ __global__ void sched_scatter_kernel(uint32_t n, SchedWs ws) {
 
 }  // namespace neb
 
-extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, uint32_t max_keys, uint32_t lpp,
-                                      const neb::SchedWs* ws, hipStream_t s) {
+extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
+                                      uint32_t lpp, const neb::SchedWs* ws, hipStream_t s) {
     const uint32_t nb = neb::sched_nbins(max_keys);
     // counters, hist and fill are contiguous: one memset per batch
     hipError_t e = hipMemsetAsync(ws->counters, 0, (2u + 2u * nb) * sizeof(uint32_t), s);
@@ -61,8 +63,8 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, uint32
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
     const uint32_t gb = (nb + tpb - 1) / tpb < 4096u ? (nb + tpb - 1) / tpb : 4096u;
-    hipLaunchKernelGGL(neb::sched_hist_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, max_keys, lpp, *ws);
+    hipLaunchKernelGGL(neb::sched_hist_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp, *ws);
     hipLaunchKernelGGL(neb::sched_alloc_kernel, dim3(gb), dim3(tpb), 0, s, max_keys, *ws);
-    hipLaunchKernelGGL(neb::sched_scatter_kernel, dim3(gp), dim3(tpb), 0, s, n, *ws);
+    hipLaunchKernelGGL(neb::sched_scatter_kernel, dim3(gp), dim3(tpb), 0, s, n, d_n, *ws);
     return hipGetLastError();
 }

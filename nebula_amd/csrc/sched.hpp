@@ -38,5 +38,5 @@ __host__ __device__ inline uint32_t sched_max_chunks(uint32_t n, uint32_t max_ke
 }  // namespace neb
 
 // Host launcher (sched.hip): zero the counters and run the three binning passes on stream s.
-extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, uint32_t max_keys, uint32_t lpp,
-                                      const neb::SchedWs* ws, hipStream_t s);
+extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
+                                      uint32_t lpp, const neb::SchedWs* ws, hipStream_t s);

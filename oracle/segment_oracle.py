@@ -280,3 +280,79 @@ def segment_superpacket(pkt: bytes, flags: int, gso_type: int, hdr_len: int, gso
     if g == GSO_UDP_L4:
         return segment_udp(pkt, hl, csum_start, gso_size)
     raise SegmentError(f"unsupported virtio gso type: {gso_type}")
+
+
+REJECT_AFTER = (1 << 64) - 1 - (1 << 40)
+OK, BAD_KEY, EXHAUSTED, INVALID, NO_SPACE = 0, 3, 2, 5, 6
+
+
+def slot_bytes(seg_len: int) -> int:
+    return (seg_len + 32 + 15) & ~15
+
+
+def tx_batch(alg, tunnels, packets, out_cap, max_wires, seal, header_encode):
+    """The batch as sendInsideMessage would send it, packet by packet in order (inside.go:154-240),
+    laid out as the engine's TX batch returns it: wires in order, each at a 16-byte aligned slot.
+    tunnels: [dict(counter, remote_index, key or None)] (counter = messageCounter before the batch);
+    packets: [dict(data, tunnel, flags, gso_type, hdr_len, gso_size, csum_start, csum_offset)].
+    A packet refused at read time (decodeRead) is INVALID; one whose tunnel has no key BAD_KEY; then
+    segment-time errors INVALID. The output keeps its longest fitting prefix of packets; the rest
+    are NO_SPACE and use no counter. Returns (wires [(off, counter, len, packet, segment, status,
+    bytes)], packet statuses, final counters)."""
+    ctr = [t["counter"] for t in tunnels]
+    pst, plans = [], []
+    for p in packets:
+        g = p["gso_type"] & ~GSO_ECN
+        st, segs = OK, None
+        try:  # read time
+            if len(p["data"]) == 0:
+                raise SegmentError("short read")
+            if g == GSO_NONE:
+                if p["flags"] & F_NEEDS_CSUM:
+                    segs = [finish_checksum(p["data"], p["csum_start"], p["csum_offset"])]
+                else:
+                    segs = [bytes(p["data"])]
+            else:
+                check_valid(p["data"], p["flags"], p["gso_type"], p["gso_size"])
+                hl = correct_hdr_len(p["data"], p["gso_type"], p["csum_start"], p["csum_offset"])
+                if g not in (GSO_TCPV4, GSO_TCPV6, GSO_UDP_L4):
+                    raise SegmentError("unsupported gso type")
+        except SegmentError:
+            st = INVALID
+        if st == OK and (p["tunnel"] >= len(tunnels) or tunnels[p["tunnel"]]["key"] is None):
+            st = BAD_KEY
+        if st == OK and segs is None:
+            try:
+                fn = segment_tcp if g in (GSO_TCPV4, GSO_TCPV6) else segment_udp
+                segs = fn(p["data"], hl, p["csum_start"], p["gso_size"])
+            except SegmentError:
+                st = INVALID
+        pst.append(st)
+        plans.append(segs if st == OK else [])
+    # fitting prefix
+    nw = nb = 0
+    fit = len(packets)
+    for i, segs in enumerate(plans):
+        nw2 = nw + len(segs)
+        nb2 = nb + sum(slot_bytes(len(s)) for s in segs)
+        if nw2 > max_wires or nb2 > out_cap:
+            fit = i
+            break
+        nw, nb = nw2, nb2
+    wires, off = [], 0
+    for i, (p, segs) in enumerate(zip(packets, plans)):
+        if i >= fit:
+            if pst[i] == OK:
+                pst[i] = NO_SPACE
+            continue
+        t = p["tunnel"]
+        for j, seg in enumerate(segs):
+            ctr[t] = (ctr[t] + 1) & ((1 << 64) - 1)
+            c = ctr[t]
+            hdr = header_encode(1, 1, 0, tunnels[t]["remote_index"], c)
+            if c >= REJECT_AFTER:
+                wires.append((off, c, len(seg) + 32, i, j, EXHAUSTED, None))
+            else:
+                wires.append((off, c, len(seg) + 32, i, j, OK, hdr + seal(alg, tunnels[t]["key"], c, hdr, seg)))
+            off += slot_bytes(len(seg))
+    return wires, pst, ctr
