@@ -109,7 +109,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
-    ap.add_argument("--mode", choices=["device", "host"], default="device")
+    ap.add_argument("--mode", choices=["device", "host", "tx", "rx"], default="device",
+                    help="device: the headline; host: host-resident batch; tx: the device TX batch "
+                         "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -177,6 +179,11 @@ def main():
                 "config": {"workload": workload_name.replace("device-resident", "host-resident pinned")},
             }), flush=True)
         return
+
+    if args.mode == "tx":
+        return bench_tx(args, eng, ctrl, rank, world)
+    if args.mode == "rx":
+        return bench_rx(args, eng, b, ciphers, ctrl, rank, world)
 
     db = DeviceBatch(eng, b, ciphers)
     stream = torch.cuda.current_stream()
@@ -250,6 +257,116 @@ def main():
             log(f"cpu_baseline failed: {e!r}")
             out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
+
+
+def tso_superpackets(nseg_total: int, mss: int = 1448, seed: int = 7):
+    """IPv4/TCP TSO superpackets of 45 x 1448 B (64 KiB class) carrying nseg_total segments."""
+    import struct
+
+    rng = np.random.default_rng(seed)
+    per = 45  # 40 + 45 x 1448 = 65200 B <= 64 KiB
+    nsp = (nseg_total + per - 1) // per
+    size = 40 + per * mss
+    stride = (size + 15) & ~15
+    arena = np.zeros(nsp * stride + 64, np.uint8)
+    hdr = bytearray(40)
+    hdr[0] = 0x45
+    struct.pack_into(">H", hdr, 2, size)
+    hdr[8], hdr[9] = 64, 6
+    hdr[12:16], hdr[16:20] = bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2])
+    struct.pack_into(">HHII", hdr, 20, 40000, 443, 1, 1)
+    hdr[32], hdr[33] = 0x50, 0x18
+    for i in range(nsp):
+        o = i * stride
+        arena[o:o + 40] = np.frombuffer(bytes(hdr), np.uint8)
+        arena[o + 40:o + size] = rng.integers(0, 256, size - 40, dtype=np.uint8)
+    return arena, nsp, size, stride, per
+
+
+def bench_tx(args, eng, ctrl, rank, world):
+    import torch
+
+    from nebula_amd import _lib as L
+    from nebula_amd.inside import TX_PACKET_DTYPE, TX_TUNNEL_DTYPE, DeviceTxBatch, slot_bytes
+    from nebula_amd.noiseutil import CipherAESGCM
+
+    mss = 1448
+    arena, nsp, size, stride, per = tso_superpackets(65536, mss)
+    key = CipherAESGCM.Cipher(eng, bytes(range(32)))
+    tun = np.zeros(1, TX_TUNNEL_DTYPE)
+    tun[0] = (2, key.key_id, 0xBEEF)
+    pk = np.zeros(nsp, TX_PACKET_DTYPE)
+    for i in range(nsp):
+        pk[i] = (i * stride, size, 0, 1, 1, 40, mss, 20, 16, 0)
+    nwire = nsp * per
+    db = DeviceTxBatch(eng, L.ALG_AESGCM, tun, pk, arena, nwire * slot_bytes(40 + mss), nwire, key.key_id)
+    db.seal()
+    torch.cuda.synchronize()
+    r = db.result()
+    assert len(r.wires) == nwire and (r.wire_status == 0).all() and (r.packet_status == 0).all()
+    for _ in range(args.warmup):
+        db.seal()
+    torch.cuda.synchronize()
+    ctrl.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        db.seal()
+    torch.cuda.synchronize()
+    dt = ctrl.max(time.perf_counter() - t0)
+    if rank == 0:
+        tun_bytes = float(nsp * size) * args.steps * world
+        print(json.dumps({
+            "metric": "GiB/s TUN bytes in, device TX batch (TSO 64 KiB superpackets -> segment + checksum + "
+                      "header + AES-256-GCM seal)",
+            "value": round(tun_bytes / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "dtype": "u8", "data": "synthetic",
+            "wire_packets_per_s": round(nwire * args.steps * world / dt, 1),
+            "config": {"workload": f"{nsp} IPv4/TCP TSO superpackets x {per} segments of {mss} B "
+                                   f"({nwire} wire packets), 1 tunnel, device-resident"},
+        }), flush=True)
+
+
+def bench_rx(args, eng, b, ciphers, ctrl, rank, world):
+    """Batched receive (host arena, replay windows) vs the plain host-resident open of the same batch."""
+    from nebula_amd import _lib as L
+    from nebula_amd.batch import PinnedBuffer, host_batch, slot_desc
+    from nebula_amd.connection_state import Bits, ReplayWindow, rx_open_batch
+
+    d = slot_desc(b, ciphers)
+    buf = PinnedBuffer(b.arena.nbytes)
+    buf.array[:] = b.arena
+    hint = int(d["key_id"][0]) if b.nkeys == 1 else L.KEYS_MIXED
+    st = host_batch(eng, b.alg, False, d, buf.array, hint)
+    assert (st == 0).all()
+    sealed = buf.array.copy()
+    nkeys = eng.max_keys
+    times = {"rx": 0.0, "open": 0.0}
+    for it in range(args.warmup + args.steps):
+        for mode in ("rx", "open"):
+            buf.array[:] = sealed
+            wins = [None] * nkeys
+            if mode == "rx":
+                for c in ciphers:
+                    wins[c.key_id] = Bits(ReplayWindow)
+            t0 = time.perf_counter()
+            if mode == "rx":
+                st = rx_open_batch(eng, b.alg, wins, d, buf.array, hint)
+            else:
+                st = host_batch(eng, b.alg, True, d, buf.array, hint)
+            el = time.perf_counter() - t0
+            assert (st == 0).all(), mode
+            if it >= args.warmup:
+                times[mode] += el
+    if rank == 0:
+        payload = float(b.payload_bytes) * args.steps
+        print(json.dumps({
+            "metric": "GiB/s host-resident batched receive (replay window Check -> GPU open -> Update)",
+            "value": round(payload / times["rx"] / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+            "open_only_gibs": round(payload / times["open"] / GIB, 3),
+            "config": {"workload": f"{b.name}: {b.n} packets, {b.nkeys} tunnel(s), host pinned arena"},
+        }), flush=True)
 
 
 if __name__ == "__main__":

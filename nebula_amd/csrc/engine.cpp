@@ -32,6 +32,17 @@ extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s);
 
+// Device workspace of the mixed-key scheduler (sched.hpp). One per engine; a batch waits on the
+// previous user's event before reusing it, so batches on different streams never overlap in it.
+struct SchedSpace {
+    uint8_t* mem = nullptr;
+    size_t bytes = 0;
+    uint32_t n_cap = 0;
+    neb::SchedWs ws{};
+    hipEvent_t done = nullptr;
+    std::mutex mu;
+};
+
 namespace {
 
 constexpr size_t kStageMin = 1 << 16;
@@ -48,22 +59,12 @@ struct PipeSlot {
     int32_t* h_status = nullptr; // pinned
     int32_t* user_status = nullptr;
     uint32_t user_begin = 0, count = 0;
+    SchedSpace* sched = nullptr;  // own mixed-key workspace: the two pipeline streams never wait on each other
 };
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
-
-// Device workspace of the mixed-key scheduler (sched.hpp). One per engine; a batch waits on the
-// previous user's event before reusing it, so batches on different streams never overlap in it.
-struct SchedSpace {
-    uint8_t* mem = nullptr;
-    size_t bytes = 0;
-    uint32_t n_cap = 0;
-    neb::SchedWs ws{};
-    hipEvent_t done = nullptr;
-    std::mutex mu;
-};
 
 // Device workspace of the transmit batch (tx.hpp) plus device staging for its host-memory form.
 struct TxSpace {
@@ -204,6 +205,11 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
         if (s.d_status) hipFree(s.d_status);
         if (s.h_desc) hipHostFree(s.h_desc);
         if (s.h_status) hipHostFree(s.h_status);
+        if (s.sched) {
+            if (s.sched->done) { hipEventSynchronize(s.sched->done); hipEventDestroy(s.sched->done); }
+            if (s.sched->mem) hipFree(s.sched->mem);
+            delete s.sched;
+        }
     }
     if (e->sched.done) { hipEventSynchronize(e->sched.done); hipEventDestroy(e->sched.done); }
     if (e->sched.mem) hipFree(e->sched.mem);
@@ -302,8 +308,7 @@ static void fill_nonce(int alg, uint64_t n, uint8_t* nb) {
 }
 
 // Size the scheduler workspace for n packets (caller holds sched.mu).
-static hipError_t sched_reserve(neb_engine* e, uint32_t n) {
-    SchedSpace& sp = e->sched;
+static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     if (!sp.done) {
         hipError_t err = hipEventCreateWithFlags(&sp.done, hipEventDisableTiming);
         if (err != hipSuccess) return err;
@@ -343,15 +348,16 @@ static hipError_t sched_reserve(neb_engine* e, uint32_t n) {
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
 // only known on the device, e.g. the segments of a TX batch).
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
-                               int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr) {
+                               int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr,
+                               SchedSpace* sched = nullptr) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
             return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
                                         e->cu_count, s);
         // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
-        SchedSpace& sp = e->sched;
+        SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
-        hipError_t err = sched_reserve(e, n);
+        hipError_t err = sched_reserve(e, sp, n);
         if (err == hipSuccess) err = hipStreamWaitEvent(s, sp.done, 0);
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)
@@ -493,6 +499,10 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
             HIP_TRY(hipHostMalloc((void**)&s.h_desc, kPipeChunkPkts * sizeof(neb_desc), hipHostMallocDefault));
             HIP_TRY(hipHostMalloc((void**)&s.h_status, kPipeChunkPkts * sizeof(int32_t), hipHostMallocDefault));
         }
+        if (!s.sched) {
+            s.sched = new (std::nothrow) SchedSpace;
+            if (!s.sched) return NEB_ERR_INVALID;
+        }
         s.count = 0;
     }
     int slot = 0;
@@ -529,7 +539,7 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         }
         HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s.stream));
         HIP_TRY(hipMemcpyAsync(s.d_buf, arena + lo, span, hipMemcpyHostToDevice, s.stream));
-        HIP_TRY(launch_batch(e, alg, open, s.d_desc, cnt, s.d_buf, s.d_status, key_hint, s.stream));
+        HIP_TRY(launch_batch(e, alg, open, s.d_desc, cnt, s.d_buf, s.d_status, key_hint, s.stream, nullptr, s.sched));
         HIP_TRY(hipMemcpyAsync(arena + lo, s.d_buf, span, hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
         s.user_status = status;

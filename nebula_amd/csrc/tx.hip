@@ -33,6 +33,18 @@ namespace neb {
 __device__ __forceinline__ uint32_t rd8(const uint8_t* p) { return p[0]; }
 __device__ __forceinline__ uint32_t rd16be(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 __device__ __forceinline__ uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+// two end-around folds of a 32-bit partial sum (the reference's `s = s&0xffff + s>>16` twice)
+__device__ __forceinline__ uint32_t fold2(uint32_t s) {
+    s = (s & 0xFFFFu) + (s >> 16);
+    return (s & 0xFFFFu) + (s >> 16);
+}
+// checksum.Checksum(p[lo:hi], 0): big-endian words paired from lo, odd tail byte high, folded
+__device__ uint32_t csum_range(const uint8_t* p, uint32_t lo, uint32_t hi) {
+    uint32_t s = 0;
+    for (uint32_t k = lo; k < hi; k++) s += ((k - lo) & 1u) ? (uint32_t)p[k] : (uint32_t)p[k] << 8;
+    while (s >> 16) s = (s & 0xFFFFu) + (s >> 16);
+    return s;
+}
 
 // ---- stage 1: per-packet checks and sizes ---------------------------------------------------
 
@@ -109,6 +121,27 @@ __global__ void tx_parse_kernel(const neb_tx_packet* __restrict__ pk, uint32_t n
                 plan.hdr_len = hl;
                 plan.v4 = v4;
                 plan.full_slot = align16(hl + gso + 32u);
+                // the constants of every segment header, from the pristine superpacket header
+                const uint32_t pseudo = (v4 ? csum_range(b, 12, 20) : csum_range(b, 8, 40)) +
+                                        (plan.kind == kTxTcp ? 6u : 17u);  // basePseudoSum
+                if (v4) {  // baseIPv4HdrSum
+                    plan.id0 = rd16be(b + 4);
+                    uint32_t sum = csum_range(b, 0, (rd8(b) & 15u) * 4u);
+                    sum += (~rd16be(b + 2) & 0xFFFFu) + (~rd16be(b + 10) & 0xFFFFu) + (~plan.id0 & 0xFFFFu);
+                    plan.ip_base = fold2(sum);
+                }
+                if (plan.kind == kTxTcp) {  // baseTCPHdrSum
+                    plan.seq0 = (rd16be(b + cs + 4u) << 16) | rd16be(b + cs + 6u);
+                    plan.fl0 = (uint8_t)rd8(b + cs + 13u);
+                    uint32_t sum = csum_range(b, cs, hl);
+                    sum += (~(plan.seq0 >> 16)) & 0xFFFFu;
+                    sum += (~plan.seq0) & 0xFFFFu;
+                    sum += (~(uint32_t)plan.fl0) & 0xFFFFu;
+                    sum += (~rd16be(b + cs + 16u)) & 0xFFFFu;
+                    plan.l4_base = fold2(sum) + pseudo;
+                } else {
+                    plan.l4_base = pseudo;
+                }
             }
         }
     }
@@ -131,6 +164,16 @@ __global__ void tx_parse_kernel(const neb_tx_packet* __restrict__ pk, uint32_t n
     pk_status[i] = st;
 }
 
+// wire -> packet map of the fitting prefix, one wave per packet
+__global__ void tx_segmap_kernel(uint32_t n, uint32_t max_wires, uint64_t out_cap, TxWs ws) {
+    const uint32_t p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (p >= n) return;
+    const uint64_t pre = ws.scan_out[p], own = ws.scan_in[p];
+    const uint64_t end_seg = (pre >> 40) + (own >> 40), end_bytes = (pre & kTxBytesMask) + (own & kTxBytesMask);
+    if (end_seg > max_wires || end_bytes > out_cap) return;
+    for (uint32_t k = (uint32_t)(pre >> 40) + (threadIdx.x & 63u); k < (uint32_t)end_seg; k += 64u) ws.seg_pkt[k] = p;
+}
+
 __global__ void tx_gather_kernel(uint32_t n, TxWs ws) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) ws.nseg_sorted[i] = ws.plan[ws.idx_sorted[i]].nseg;
@@ -146,10 +189,19 @@ __global__ void tx_scatter_kernel(uint32_t n, uint32_t ntun, uint64_t out_cap, u
     const uint64_t pre = ws.scan_out[p], own = ws.scan_in[p];
     const uint64_t end_seg = (pre >> 40) + (own >> 40);
     const uint64_t end_bytes = (pre & kTxBytesMask) + (own & kTxBytesMask);
-    const uint32_t t = ws.tun_key[p];
+    const uint32_t t = ws.tun_key_sorted[i];
+    const bool fits = end_seg <= max_wires && end_bytes <= out_cap;
     if (t < ntun) {
-        if (end_seg <= max_wires && end_bytes <= out_cap) {
-            atomicAdd(&ws.tun_total[t], (unsigned long long)(own >> 40));
+        if (fits) {
+            // the last fitting packet of its tunnel's run (sorted by tunnel, then batch order) writes
+            // the tunnel's segment total: its exclusive offset plus its own segments
+            bool last = i + 1u == n || ws.tun_key_sorted[i + 1u] != t;
+            if (!last) {
+                const uint32_t q = ws.idx_sorted[i + 1u];
+                const uint64_t e = ws.scan_out[q] + ws.scan_in[q];
+                last = !((e >> 40) <= max_wires && (e & kTxBytesMask) <= out_cap);
+            }
+            if (last) ws.tun_total[t] = ws.ctr_sorted[i] + (own >> 40);
         } else {
             pk_status[p] = NEB_STATUS_NO_SPACE;  // outside the fitting prefix
         }
@@ -212,17 +264,6 @@ __device__ __forceinline__ uint32_t put_be(uint32_t w, uint32_t lane, uint32_t o
     return w;
 }
 
-// RFC 1071 contribution of this lane's 4 header bytes to checksum(hdr[lo:hi]) (pairing from lo).
-__device__ __forceinline__ uint32_t lane_sum(uint32_t w, uint32_t lane, uint32_t lo, uint32_t hi) {
-    uint32_t s = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t k = 4u * lane + j;
-        if (k >= lo && k < hi) s += ((k - lo) & 1u) ? byte_at(w, j) : byte_at(w, j) << 8;
-    }
-    return s;
-}
-
 // Σ of 16-bit little-endian words of a 16-byte unit (pairing from the unit start).
 __device__ __forceinline__ uint32_t unit_le_sum(uint4 v) {
     return (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) + (v.z >> 16) +
@@ -250,168 +291,214 @@ __device__ __forceinline__ uint4 put_be_unit(uint4 v, uint32_t base, uint32_t of
 }
 
 constexpr int kTxWaves = 4;
+#ifndef NEB_TX_GROUP
+#define NEB_TX_GROUP 16     // measured (64 KiB TSO batch): 16 lanes x 6 units 308 GiB/s, 32 x 3 303,
+#define NEB_TX_REGUNITS 6  // 64 x 2 279; 6 blocks/CU (80 VGPRs) spills: 241
+#define NEB_TX_MINBLOCKS 4
+#endif
+constexpr uint32_t kTxGroup = NEB_TX_GROUP;        // lanes per segment: 64 / kTxGroup segments per wave
+constexpr uint32_t kTxRegUnits = NEB_TX_REGUNITS;  // payload units per lane kept in registers (16 x 6 x 16 B = 1.5 KiB)
 
-__global__ __launch_bounds__(kTxWaves * 64) void tx_segment_kernel(const neb_tx_packet* __restrict__ pk, uint32_t n,
+__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
+#pragma unroll
+    for (int o = kTxGroup / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, (int)kTxGroup);
+    return v;
+}
+
+__global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_kernel(const neb_tx_packet* __restrict__ pk,
                                                                      const uint8_t* __restrict__ in,
                                                                      const neb_tx_tunnel* __restrict__ tun,
                                                                      uint8_t* __restrict__ out, TxWs ws,
                                                                      neb_tx_wire* __restrict__ wires,
                                                                      const uint32_t* __restrict__ d_nwires) {
-    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = threadIdx.x & (kTxGroup - 1u);  // lane within the segment's group
     const uint32_t nw = __builtin_amdgcn_readfirstlane(*d_nwires);
-    for (uint32_t s = blockIdx.x * kTxWaves + (threadIdx.x >> 6); s < nw; s += gridDim.x * kTxWaves) {
-        // packet of segment s: the last packet whose first segment index is <= s
-        uint32_t lo = 0, hi = n;
-        while (hi - lo > 1u) {
-            const uint32_t m = (lo + hi) >> 1;
-            if ((ws.scan_out[m] >> 40) <= s) lo = m;
-            else hi = m;
-        }
-        const uint32_t p = lo;
-        const uint64_t pre = ws.scan_out[p];
+    const uint32_t groups_per_block = blockDim.x / kTxGroup;
+    const uint32_t first = blockIdx.x * groups_per_block + threadIdx.x / kTxGroup;
+    const uint32_t rounds = (nw + gridDim.x * groups_per_block - 1u) / (gridDim.x * groups_per_block);
+    for (uint32_t r = 0; r < rounds; r++) {  // uniform trip count: every lane reaches the shuffles
+        const uint32_t s = first + r * gridDim.x * groups_per_block;
+        const bool live = s < nw;
+        const uint32_t p = live ? ws.seg_pkt[s] : 0u;
+        const uint64_t pre = live ? ws.scan_out[p] : 0u;
         const uint32_t j = s - (uint32_t)(pre >> 40);
-        const TxPlan plan = ws.plan[p];
-        const neb_tx_packet P = pk[p];
-        const neb_tx_tunnel T = tun[P.tunnel];
-        const uint64_t counter = T.message_counter + ws.ctr_off[p] + j + 1u;
+        TxPlan plan{};
+        neb_tx_packet P{};
+        neb_tx_tunnel T{};
+        uint32_t ctr_off = 0;
+        if (live) {
+            plan = ws.plan[p];
+            P = pk[p];
+            ctr_off = ws.ctr_off[p];
+        }
+        if (live) T = tun[P.tunnel];
+        const uint64_t counter = T.message_counter + ctr_off + j + 1u;
         const uint64_t slot = (pre & kTxBytesMask) + (uint64_t)j * plan.full_slot;
         const uint8_t* src = in + P.in_off;
         const uint32_t hl = plan.hdr_len, cs = P.csum_start, co = P.csum_offset;
         const bool gsok = plan.kind == kTxTcp || plan.kind == kTxUdp;
         const uint32_t a = gsok ? j * P.gso_size : 0u;
-        const uint32_t pl = gsok ? min((uint32_t)P.gso_size, P.len - hl - a) : P.len;
+        const uint32_t pl = !live ? 0u : gsok ? min((uint32_t)P.gso_size, P.len - hl - a) : P.len;
         const uint32_t seg_len = hl + pl;
         uint8_t* dst = out + slot;
+        const bool work = live && counter < kRejectAfterMessages;  // an exhausted one keeps only its header
 
-        if (lane == 0) {
+        if (live && g == 0) {
             wires[s] = neb_tx_wire{slot, counter, seg_len + 32u, p, j, 0u};
             ws.seal_desc[s] = neb_desc{slot + 16u, slot + 16u, slot, counter, seg_len, 16u, T.key_id, 0u};
             // header.Encode(Version 1, Message 1, subtype 0, remote index, counter)
-            const uint32_t ri = T.remote_index;
-            *reinterpret_cast<uint4*>(dst) = make_uint4(0x00000011u, bswap32(ri), bswap32((uint32_t)(counter >> 32)),
-                                                        bswap32((uint32_t)counter));
+            *reinterpret_cast<uint4*>(dst) = make_uint4(0x00000011u, bswap32(T.remote_index),
+                                                        bswap32((uint32_t)(counter >> 32)), bswap32((uint32_t)counter));
         }
-        if (counter >= kRejectAfterMessages) continue;  // sendInsideEncrypt drops it; nothing but the header
 
-        // ---- header image (superpacket segments) ----
-        uint32_t hw = 0;  // this lane's dword of the segment's L3+L4 header
-        uint32_t l4_seed = 0;
+        // ---- the segment's L3+L4 header: dwords g and g + 16 of it (superpackets) ----
+        uint32_t hw[2] = {0, 0};
+        uint32_t le = 0;  // this lane's Σ of 16-bit words of the L4 checksum range, paired from its start, swapped
         uint64_t tcp_wide = 0;
-        if (gsok) {
-            uint32_t h0 = 0;  // pristine header bytes [4 lane, 4 lane + 4)
-            if (4u * lane < hl) {
+        uint32_t udp_seed = 0;
+        if (work && gsok) {
 #pragma unroll
-                for (uint32_t k = 0; k < 4; k++)
-                    if (4u * lane + k < hl) h0 |= (uint32_t)src[4u * lane + k] << (8u * k);
+            for (uint32_t h = 0; h < 2; h++) {
+                const uint32_t d = g + kTxGroup * h;
+                if (4u * d < hl) {
+                    const uint8_t* hp = src + 4u * d;
+                    if (((P.in_off & 3u) == 0u) && 4u * d + 4u <= hl) {
+                        hw[h] = *reinterpret_cast<const uint32_t*>(hp);
+                    } else {
+#pragma unroll
+                        for (uint32_t k = 0; k < 4; k++)
+                            if (4u * d + k < hl) hw[h] |= (uint32_t)hp[k] << (8u * k);
+                    }
+                }
             }
-            auto hb = [&](uint32_t pos) { return byte_at((uint32_t)__shfl((int)h0, (int)(pos >> 2)), pos & 3u); };
-            const bool v4 = plan.v4;
-            const bool tcp = plan.kind == kTxTcp;
-            // base sums over the pristine header (segment_linux.go:166-208)
-            const uint32_t pseudo =
-                fold16(wave_sum(v4 ? lane_sum(h0, lane, 12, 20) : lane_sum(h0, lane, 8, 40))) + (tcp ? 6u : 17u);
-            uint32_t ip_base = 0, id0 = 0;
-            if (v4) {
-                const uint32_t ihl = (hb(0) & 15u) * 4u;
-                uint32_t sum = fold16(wave_sum(lane_sum(h0, lane, 0, ihl)));
-                id0 = (hb(4) << 8) | hb(5);
-                sum += (~((hb(2) << 8) | hb(3)) & 0xFFFFu) + (~((hb(10) << 8) | hb(11)) & 0xFFFFu) + (~id0 & 0xFFFFu);
-                sum = (sum & 0xFFFFu) + (sum >> 16);
-                sum = (sum & 0xFFFFu) + (sum >> 16);
-                ip_base = sum;
-            }
-            uint32_t tcp_base = 0, seq0 = 0, fl0 = 0;
-            if (tcp) {
-                seq0 = (hb(cs + 4u) << 24) | (hb(cs + 5u) << 16) | (hb(cs + 6u) << 8) | hb(cs + 7u);
-                fl0 = hb(cs + 13u);
-                const uint32_t ck0 = (hb(cs + 16u) << 8) | hb(cs + 17u);
-                uint32_t sum = fold16(wave_sum(lane_sum(h0, lane, cs, hl)));
-                sum += (~(seq0 >> 16)) & 0xFFFFu;
-                sum += (~seq0) & 0xFFFFu;
-                sum += (~fl0) & 0xFFFFu;
-                sum += (~ck0) & 0xFFFFu;
-                sum = (sum & 0xFFFFu) + (sum >> 16);
-                sum = (sum & 0xFFFFu) + (sum >> 16);
-                tcp_base = sum;
-            }
-            // the per-segment fields, in the reference's write order
-            hw = h0;
-            if (v4) {
-                const uint32_t total = seg_len, id = (id0 + j) & 0xFFFFu;
-                hw = put_be(hw, lane, 2, 2, total);
-                hw = put_be(hw, lane, 4, 2, id);
-                hw = put_be(hw, lane, 10, 2, fold_complement(ip_base + total + id));
-            } else {
-                hw = put_be(hw, lane, 4, 2, hl - 40u + pl);
-            }
-            if (tcp) {
-                const uint32_t seq = seq0 + a;
-                uint32_t fl = fl0;
+            const uint32_t total = seg_len, id = (plan.id0 + j) & 0xFFFFu;
+            const uint32_t ipck = fold_complement(plan.ip_base + total + id);
+            uint32_t seq = 0, fl = 0, udp_len = 8u + pl;
+            if (plan.kind == kTxTcp) {
+                seq = plan.seq0 + a;
+                fl = plan.fl0;
                 if (j != 0) fl &= ~0x80u;               // CWR only on the first segment
                 if (j != plan.nseg - 1u) fl &= ~0x09u;  // FIN|PSH only on the last
-                hw = put_be(hw, lane, cs + 4u, 4, seq);
-                hw = put_be(hw, lane, cs + 13u, 1, fl);
-                tcp_wide = (uint64_t)tcp_base + pseudo + seq + fl + ((hl - cs) + pl);  // + the payload sum
-            } else {  // UDP: length, checksum zeroed, then ~checksum(seg[cs:], pseudo + udp length)
-                const uint32_t udp_len = 8u + pl;
-                hw = put_be(hw, lane, cs + 4u, 2, udp_len);
-                hw = put_be(hw, lane, cs + 6u, 2, 0u);
-                uint32_t ps = pseudo + udp_len;
-                ps = (ps & 0xFFFFu) + (ps >> 16);
-                ps = (ps & 0xFFFFu) + (ps >> 16);
-                l4_seed = ps + fold16(wave_sum(lane_sum(hw, lane, cs, hl)));
+                tcp_wide = (uint64_t)plan.l4_base + seq + fl + ((hl - cs) + pl);  // + the payload sum
+            } else {
+                udp_seed = fold2(plan.l4_base + udp_len);
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < 2; h++) {
+                const uint32_t d = g + kTxGroup * h;
+                uint32_t w = hw[h];
+                if (plan.v4) {  // the reference's write order: total length, ID, checksum
+                    w = put_be(w, d, 2, 2, total);
+                    w = put_be(w, d, 4, 2, id);
+                    w = put_be(w, d, 10, 2, ipck);
+                } else {
+                    w = put_be(w, d, 4, 2, hl - 40u + pl);
+                }
+                if (plan.kind == kTxTcp) {
+                    w = put_be(w, d, cs + 4u, 4, seq);
+                    w = put_be(w, d, cs + 13u, 1, fl);
+                } else {  // UDP: length and a zeroed checksum enter the sum over seg[cs:]
+                    w = put_be(w, d, cs + 4u, 2, udp_len);
+                    w = put_be(w, d, cs + 6u, 2, 0u);
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; k++) {
+                        const uint32_t pos = 4u * d + k;
+                        if (pos >= cs && pos < hl) le += ((pos - cs) & 1u) ? byte_at(w, k) << 8 : byte_at(w, k);
+                    }
+                }
+                hw[h] = w;
             }
         }
 
-        // ---- pass 1: the checksum over the payload units ----
-        // image positions hl + 16u; the sum runs over [sum_lo, seg_len) with bytes [zlo, zhi) as zero
-        const bool need_sum = plan.kind != kTxPass;
+        // ---- payload units: image positions hl + 16u; the L4 checksum covers [sum_lo, seg_len) ----
+        const bool need_sum = work && plan.kind != kTxPass;
         const uint32_t sum_lo = plan.kind == kTxFinish ? cs : hl;
         const uint32_t zlo = plan.kind == kTxFinish ? cs + co : 0u, zhi = plan.kind == kTxFinish ? cs + co + 2u : 0u;
         const uint8_t* psrc = src + hl + a;
-        uint32_t partial = 0;
-        if (plan.kind == kTxFinish) partial = rd16be(src + cs + co);
-        uint32_t csum = 0;
-        if (need_sum) {
-            uint32_t acc = 0;
-            for (uint32_t u = lane; 16u * u < pl; u += 64u) {
-                const uint32_t base = hl + 16u * u;
+        const uint32_t nunits = work ? (pl + 15u) >> 4 : 0u;
+        const bool in_regs = nunits <= kTxGroup * kTxRegUnits;
+        const bool flip = ((hl ^ sum_lo) & 1u) != 0u;  // units start at the parity of hl
+        uint4 keep[kTxRegUnits];
+        if (in_regs) {
+#pragma unroll
+            for (uint32_t k = 0; k < kTxRegUnits; k++) {
+                const uint32_t u = g + kTxGroup * k;
+                keep[k] = make_uint4(0, 0, 0, 0);
+                if (u < nunits) keep[k] = load_block(psrc + 16u * u, min(16u, pl - 16u * u));
+            }
+            if (need_sum) {
+#pragma unroll
+                for (uint32_t k = 0; k < kTxRegUnits; k++) {
+                    const uint32_t u = g + kTxGroup * k;
+                    if (u < nunits) {
+                        uint4 v = keep[k];
+                        if (plan.kind == kTxFinish) {  // only FinishChecksum sums part of its units
+                            v = zero_range(v, hl + 16u * u, 0u, sum_lo);
+                            v = zero_range(v, hl + 16u * u, zlo, zhi);
+                        }
+                        const uint32_t su = unit_le_sum(v);
+                        le += flip ? bswap16(fold16(su)) : su;
+                    }
+                }
+            }
+        } else if (need_sum) {
+            for (uint32_t u = g; u < nunits; u += kTxGroup) {
                 uint4 v = load_block(psrc + 16u * u, min(16u, pl - 16u * u));
-                v = zero_range(v, base, 0u, sum_lo);
-                if (zhi) v = zero_range(v, base, zlo, zhi);
-                acc += unit_le_sum(v);
+                if (plan.kind == kTxFinish) {
+                    v = zero_range(v, hl + 16u * u, 0u, sum_lo);
+                    v = zero_range(v, hl + 16u * u, zlo, zhi);
+                }
+                const uint32_t su = unit_le_sum(v);
+                le += flip ? bswap16(fold16(su)) : su;
             }
-            const uint32_t le = fold16(wave_sum(acc));
-            // pairing from sum_lo: unit starts have the parity of hl
-            const uint32_t rel = ((hl ^ sum_lo) & 1u) ? le : bswap16(le);
-            if (plan.kind == kTxTcp) {
-                uint64_t w = tcp_wide + rel;
-                w = (w & 0xFFFFFFFFull) + (w >> 32);
-                w = (w & 0xFFFFFFFFull) + (w >> 32);
-                csum = fold_complement((uint32_t)w);
-            } else if (plan.kind == kTxUdp) {
-                csum = ~fold16((uint64_t)l4_seed + rel) & 0xFFFFu;
-                if (csum == 0u) csum = 0xFFFFu;  // RFC 768: a computed zero goes out as all ones
-            } else {  // FinishChecksum
-                csum = ~fold16((uint64_t)partial + rel) & 0xFFFFu;
-                if (co == 6u && csum == 0u) csum = 0xFFFFu;
-            }
+        }
+        // the group total, folded and byte-swapped, is the big-endian RFC 1071 sum
+        const uint32_t rel = bswap16(fold16(group_sum(le)));
+        uint32_t csum = 0;
+        if (plan.kind == kTxTcp) {
+            uint64_t w = tcp_wide + rel;
+            w = (w & 0xFFFFFFFFull) + (w >> 32);
+            w = (w & 0xFFFFFFFFull) + (w >> 32);
+            csum = fold_complement((uint32_t)w);
+        } else if (plan.kind == kTxUdp) {
+            csum = ~fold16((uint64_t)udp_seed + rel) & 0xFFFFu;
+            if (csum == 0u) csum = 0xFFFFu;  // RFC 768: a computed zero goes out as all ones
+        } else if (plan.kind == kTxFinish && work) {  // seeded with the partial sum left in the field
+            csum = ~fold16((uint64_t)rd16be(src + cs + co) + rel) & 0xFFFFu;
+            if (co == 6u && csum == 0u) csum = 0xFFFFu;
         }
 
-        // ---- pass 2: store the image ----
+        // ---- store the image ----
         uint8_t* ddst = dst + 16u;
-        if (gsok && 4u * lane < hl) {
-            hw = put_be(hw, lane, plan.kind == kTxTcp ? cs + 16u : cs + 6u, 2, csum);
-            const uint32_t nb = min(4u, hl - 4u * lane);
-            if (nb == 4u) *reinterpret_cast<uint32_t*>(ddst + 4u * lane) = hw;
-            else for (uint32_t k = 0; k < nb; k++) ddst[4u * lane + k] = (uint8_t)(hw >> (8u * k));
+        if (work && gsok) {
+#pragma unroll
+            for (uint32_t h = 0; h < 2; h++) {
+                const uint32_t d = g + kTxGroup * h;
+                if (4u * d < hl) {
+                    const uint32_t w = put_be(hw[h], d, plan.kind == kTxTcp ? cs + 16u : cs + 6u, 2, csum);
+                    const uint32_t nb = min(4u, hl - 4u * d);
+                    if (nb == 4u) *reinterpret_cast<uint32_t*>(ddst + 4u * d) = w;
+                    else for (uint32_t k = 0; k < nb; k++) ddst[4u * d + k] = (uint8_t)(w >> (8u * k));
+                }
+            }
         }
-        for (uint32_t u = lane; 16u * u < pl; u += 64u) {
-            const uint32_t base = hl + 16u * u;
-            const uint32_t nb = min(16u, pl - 16u * u);
-            uint4 v = load_block(psrc + 16u * u, nb);
-            if (plan.kind == kTxFinish) v = put_be_unit(v, base, cs + co, csum);
-            store_block(ddst + base, v, nb);
+        if (in_regs) {
+#pragma unroll
+            for (uint32_t k = 0; k < kTxRegUnits; k++) {
+                const uint32_t u = g + kTxGroup * k;
+                if (u < nunits) {
+                    uint4 v = keep[k];
+                    if (plan.kind == kTxFinish) v = put_be_unit(v, hl + 16u * u, cs + co, csum);
+                    store_block(ddst + hl + 16u * u, v, min(16u, pl - 16u * u));
+                }
+            }
+        } else {
+            for (uint32_t u = g; u < nunits; u += kTxGroup) {
+                const uint32_t nb = min(16u, pl - 16u * u);
+                uint4 v = load_block(psrc + 16u * u, nb);
+                if (plan.kind == kTxFinish) v = put_be_unit(v, hl + 16u * u, cs + co, csum);
+                store_block(ddst + hl + 16u * u, v, nb);
+            }
         }
     }
 }
@@ -462,6 +549,7 @@ extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const u
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(neb::tx_scatter_kernel, dim3(grid), dim3(tpb), 0, s, n, ntun, out_cap, max_wires, *ws,
                        d_pk_status, d_nwires);
+    hipLaunchKernelGGL(neb::tx_segmap_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, max_wires, out_cap, *ws);
     return hipGetLastError();
 }
 
@@ -469,11 +557,13 @@ extern "C" hipError_t neb_tx_segment(const neb_tx_packet* d_pk, uint32_t n, cons
                                      const neb_tx_tunnel* d_tun, uint8_t* d_out, const neb::TxWs* ws,
                                      neb_tx_wire* d_wires, const uint32_t* d_nwires, uint32_t max_wires, int cu_count,
                                      hipStream_t s) {
-    const uint32_t want = (max_wires + neb::kTxWaves - 1) / neb::kTxWaves;
+    (void)n;
+    const uint32_t per_block = neb::kTxWaves * 64u / neb::kTxGroup;
+    const uint32_t want = (max_wires + per_block - 1) / per_block;
     const uint32_t cap = (uint32_t)cu_count * 8u;
     const uint32_t grid = want < cap ? want : cap;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(neb::tx_segment_kernel, dim3(grid), dim3(neb::kTxWaves * 64), 0, s, d_pk, n, d_in, d_tun, d_out,
+    hipLaunchKernelGGL(neb::tx_segment_kernel, dim3(grid), dim3(neb::kTxWaves * 64), 0, s, d_pk, d_in, d_tun, d_out,
                        *ws, d_wires, d_nwires);
     return hipGetLastError();
 }

@@ -16,7 +16,12 @@ struct TxPlan {          // per packet (tx_parse_kernel)
     uint32_t nseg;       // 0 = dropped
     uint32_t hdr_len;    // superpackets: the corrected L3+L4 header length
     uint32_t full_slot;  // output bytes of one full-size segment (16-aligned)
-    uint8_t kind, v4, pad0, pad1;
+    uint8_t kind, v4, fl0, pad0;
+    // per-superpacket constants of the segment headers (segment_linux.go:166-208), computed once
+    uint32_t ip_base;    // baseIPv4HdrSum
+    uint32_t l4_base;    // TCP: baseTCPHdrSum + basePseudoSum; UDP: basePseudoSum
+    uint32_t seq0;       // TCP sequence number
+    uint32_t id0;        // IPv4 ID
 };
 
 struct TxWs {
@@ -30,6 +35,7 @@ struct TxWs {
     uint32_t* nseg_sorted;
     uint32_t* ctr_sorted;
     uint32_t* ctr_off;           // per packet: segments of its tunnel earlier in the batch
+    uint32_t* seg_pkt;           // per wire: its packet
     unsigned long long* tun_total;  // per tunnel: segments in this batch
     unsigned long long* totals;     // [0] segments, [1] bytes of the fitting prefix
     neb_desc* seal_desc;         // per wire
@@ -61,6 +67,7 @@ inline size_t tx_ws_layout(uint32_t n, uint32_t ntun, uint32_t max_wires, size_t
     w.tun_total = (unsigned long long*)take((size_t)(ntun ? ntun : 1) * 8);
     w.totals = (unsigned long long*)take(16);
     w.seal_desc = (neb_desc*)take((size_t)(max_wires ? max_wires : 1) * sizeof(neb_desc));
+    w.seg_pkt = (uint32_t*)take((size_t)(max_wires ? max_wires : 1) * 4);
     w.cub_tmp = take(cub_bytes);
     w.cub_bytes = cub_bytes;
     if (ws) *ws = w;

@@ -24,7 +24,6 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/nebula_aead.h"
@@ -185,44 +184,46 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
                                    int32_t* status, uint32_t key_hint) {
     if (!e || (n && (!desc || !arena || !status || !windows))) return NEB_ERR_INVALID;
     if (n == 0) return NEB_OK;
-    enum : uint8_t { kToGpu, kHeld, kNoWindow };
-    std::vector<uint8_t> plan(n);
-    std::vector<neb_desc> sub;
-    std::vector<uint32_t> sub_of;  // packet index -> position in `sub`
-    sub.reserve(n);
-    sub_of.assign(n, 0);
-
-    // 1. simulation on private copies: which packets would the sequential receive path decrypt?
+    // Windows are independent: group the batch by window (stable, so each window sees its packets
+    // in arrival order) and run each window's sequence under one lock acquisition.
+    std::vector<uint32_t> start(nwindows + 2, 0), order(n);
+    auto group_of = [&](const neb_desc& d) -> uint32_t {
+        return (d.key_id < nwindows && windows[d.key_id]) ? d.key_id : nwindows;  // nwindows: no window
+    };
+    for (uint32_t i = 0; i < n; i++) start[group_of(desc[i]) + 1]++;
+    for (uint32_t g = 0; g <= nwindows; g++) start[g + 1] += start[g];
     {
-        std::unordered_map<const neb_window*, WindowCore> sim;
-        const neb_window* last = nullptr;
-        WindowCore* cur = nullptr;
-        for (uint32_t i = 0; i < n; i++) {
-            const neb_desc& d = desc[i];
-            const neb_window* w = d.key_id < nwindows ? windows[d.key_id] : nullptr;
-            if (!w) {
-                plan[i] = kNoWindow;
-                continue;
-            }
-            if (w != last) {
-                auto it = sim.find(w);
-                if (it == sim.end()) {
-                    std::lock_guard<std::mutex> g(w->mu);
-                    it = sim.emplace(w, w->core).first;
-                }
-                cur = &it->second;
-                last = w;
-            }
-            if (cur->check(d.counter)) {
-                cur->update(d.counter);
+        std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+        for (uint32_t i = 0; i < n; i++) order[fill[group_of(desc[i])]++] = i;
+    }
+    enum : uint8_t { kToGpu, kHeld };
+    std::vector<uint8_t> plan(n, kHeld);
+    std::vector<neb_desc> sub;
+    std::vector<uint32_t> sub_of(n, 0);
+    sub.reserve(n);
+
+    // 1. simulation on a private copy of each window: which packets would the sequential receive
+    //    path decrypt? (the GPU batch keeps arrival order inside each window's run)
+    WindowCore sim;
+    for (uint32_t g = 0; g < nwindows; g++) {
+        if (start[g] == start[g + 1]) continue;
+        {
+            std::lock_guard<std::mutex> lk(windows[g]->mu);
+            sim = windows[g]->core;
+        }
+        for (uint32_t k = start[g]; k < start[g + 1]; k++) {
+            const uint32_t i = order[k];
+            if (sim.check(desc[i].counter)) {
+                sim.update(desc[i].counter);
                 plan[i] = kToGpu;
-                sub_of[i] = (uint32_t)sub.size();
-                sub.push_back(d);
-            } else {
-                plan[i] = kHeld;
             }
         }
     }
+    for (uint32_t i = 0; i < n; i++)
+        if (plan[i] == kToGpu) {
+            sub_of[i] = (uint32_t)sub.size();
+            sub.push_back(desc[i]);
+        }
 
     // 2. one GPU open for everything the simulation lets through
     std::vector<int32_t> sub_status(sub.size(), NEB_STATUS_BAD_KEY);
@@ -232,45 +233,38 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
         if (rc != NEB_OK) return rc;
     }
 
-    // 3. the real windows in arrival order: Check → tag verdict → Update
-    neb_window* locked = nullptr;
-    std::unique_lock<std::mutex> lk;
-    for (uint32_t i = 0; i < n; i++) {
-        const neb_desc& d = desc[i];
-        if (plan[i] == kNoWindow) {
-            status[i] = NEB_STATUS_BAD_KEY;
-            continue;
-        }
-        neb_window* w = windows[d.key_id];
-        if (w != locked) {
-            if (lk.owns_lock()) lk.unlock();
-            lk = std::unique_lock<std::mutex>(w->mu);
-            locked = w;
-        }
-        if (!w->core.check(d.counter)) {
-            status[i] = NEB_STATUS_REPLAY;
-            continue;
-        }
-        int32_t st;
-        if (plan[i] == kToGpu) {
-            st = sub_status[sub_of[i]];
-        } else {  // held back, yet the real window accepts it: an earlier copy failed its tag
-            lk.unlock();
-            locked = nullptr;
-            const int rc = neb_open_batch_host(e, alg, &d, 1, arena, arena_len, &st, key_hint);
-            if (rc != NEB_OK) return rc;
-            lk = std::unique_lock<std::mutex>(w->mu);
-            locked = w;
-            if (st == NEB_STATUS_OK && !w->core.check(d.counter)) {  // moved by another thread meanwhile
+    // 3. the real windows, each in arrival order: Check → tag verdict → Update
+    for (uint32_t k = start[nwindows]; k < start[nwindows + 1]; k++) status[order[k]] = NEB_STATUS_BAD_KEY;
+    for (uint32_t g = 0; g < nwindows; g++) {
+        if (start[g] == start[g + 1]) continue;
+        neb_window* w = windows[g];
+        std::unique_lock<std::mutex> lk(w->mu);
+        for (uint32_t k = start[g]; k < start[g + 1]; k++) {
+            const uint32_t i = order[k];
+            const neb_desc& d = desc[i];
+            if (!w->core.check(d.counter)) {
                 status[i] = NEB_STATUS_REPLAY;
                 continue;
             }
+            int32_t st;
+            if (plan[i] == kToGpu) {
+                st = sub_status[sub_of[i]];
+            } else {  // held back, yet the real window accepts it: an earlier copy failed its tag
+                lk.unlock();
+                const int rc = neb_open_batch_host(e, alg, &d, 1, arena, arena_len, &st, key_hint);
+                if (rc != NEB_OK) return rc;
+                lk.lock();
+                if (st == NEB_STATUS_OK && !w->core.check(d.counter)) {  // moved by another thread meanwhile
+                    status[i] = NEB_STATUS_REPLAY;
+                    continue;
+                }
+            }
+            if (st != NEB_STATUS_OK) {
+                status[i] = st;
+                continue;
+            }
+            status[i] = w->core.update(d.counter) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
         }
-        if (st != NEB_STATUS_OK) {
-            status[i] = st;
-            continue;
-        }
-        status[i] = w->core.update(d.counter) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
     }
     return NEB_OK;
 }
