@@ -178,6 +178,17 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
         __builtin_amdgcn_s_setprio(0);
 #endif
         // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k, T1 = rotl8 T0, T3 = rotl8 T2
+#ifdef NEB_DUMMY_VALU
+        {  // experiment: extra VALU work per round that feeds nothing but a final register
+            uint32_t d0 = s0 ^ 0x1234u, d1 = s1 ^ 0x5678u;
+#pragma unroll
+            for (int q = 0; q < NEB_DUMMY_VALU / 2; q++) {
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(d0) : "v"(d1), "v"(s2));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(d1) : "v"(d0), "v"(s3));
+            }
+            asm volatile("" ::"v"(d0), "v"(d1));
+        }
+#endif
         if constexpr (RK::kUniform) {
             s0 = x3s(a0, a2, k.x) ^ rotl8(a1 ^ a3);
             s1 = x3s(b0, b2, k.y) ^ rotl8(b1 ^ b3);
@@ -571,6 +582,18 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
 #endif
                 __builtin_amdgcn_sched_barrier(0);
                 const uint4 ks = gcm_lane_ks<CTRC>(b, c1, c2, cc, T, rk);
+#ifndef NEB_NO_FASTIO
+                // the common round: every active lane holds a full, 16-B aligned payload block
+                const uint32_t off = 16u * (b.k - 1u);
+                const bool full = b.is_ct && off + 16u <= d.len && ((d.src_off | d.dst_off) & 15u) == 0u;
+                if (__all(full)) {
+                    const uint4 in = *reinterpret_cast<const uint4*>(args.arena + d.src_off + off);
+                    const uint4 out = xor4(in, ks);
+                    *reinterpret_cast<uint4*>(args.arena + d.dst_off + off) = out;
+                    A = xor4(G, bswap4(OPEN ? in : out));
+                    continue;
+                }
+#endif
                 const uint4 in = gcm_lane_load(d, b, args.arena);
                 A = xor4(G, gcm_lane_io<OPEN>(d, b, in, ks, args.arena, ej0));
             }

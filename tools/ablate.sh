@@ -3,7 +3,7 @@
 # NEB_ABLATE_* variants compute WRONG results by design (timing/counter study only).
 set -e
 cd "$(dirname "$0")/../nebula_amd"
-mkdir -p ../build_abl
+mkdir -p ../build_abl && rm -f ../build_abl/lib_*.so
 [ $# -eq 0 ] && set -- "BASE:" "HORNER:-DNEB_ABLATE_HORNER" "FINAL:-DNEB_ABLATE_FINAL" "AES:-DNEB_ABLATE_AES"
 : > ../build_abl/variants.txt
 for spec in "$@"; do
