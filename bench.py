@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E peak
 GIB = float(1 << 30)
+EV_EVERY = 4  # kernel-timing events bracket every 4th step (see the timed loop)
 
 
 def log(*a):
@@ -46,7 +47,8 @@ def cpu_share() -> int:
 
 
 def cpu_baseline(b, target_s: float = 6.0):
-    """OpenSSL-EVP port (oracle/evp_baseline.c) on a bounded sample: seal then open."""
+    """OpenSSL-EVP port (oracle/evp_baseline.c) on a bounded sample: seal then open, each timed
+    for about target_s seconds (about 2 x target_s of CPU wall time in all)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
@@ -55,9 +57,10 @@ def cpu_baseline(b, target_s: float = 6.0):
     desc = b.desc[:n].copy()
     arena = b.arena[: n * b.stride].copy()
     keys = b.keys
-    # calibrate
-    t1, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=1)
-    iters = max(1, int(target_s / max(t1, 1e-4)))
+    # calibrate on a warm pool (the first pass pays thread start-up)
+    oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=1)
+    t1, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=8)
+    iters = max(1, int(target_s / max(t1 / 8, 1e-5)))
     sealed = arena.copy()
     ts, st = oracle.evp_batch(b.alg, 0, keys, desc, sealed, threads=threads, iters=1)
     assert (st == 0).all()
@@ -197,23 +200,32 @@ def main():
         db.seal()
         db.open()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # Kernel durations come from HIP events on the launch stream inside the timed region. A timing
+    # event is a queue marker the GPU processes between the kernels (several µs each), so events
+    # bracket the seal and open kernels of every EV_EVERY-th step only: the other steps run
+    # back-to-back as in deployment. A bracket includes its marker gap: kernel_ms is an upper bound.
+    timed = [i for i in range(args.steps) if i % EV_EVERY == 0]
+    ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+              torch.cuda.Event(enable_timing=True)) for i in timed}
     barrier()
     torch.cuda.synchronize()
     ts = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
+        e = ev.get(i)
+        if e:
+            e[0].record(stream)
         db.seal()
-        ev[i][1].record(stream)
+        if e:
+            e[1].record(stream)
         db.open()
-        ev[i][2].record(stream)
+        if e:
+            e[2].record(stream)
     torch.cuda.synchronize()
     barrier()
     te = time.perf_counter()
     dt = te - ts
-    seal_ms = float(np.mean([a.elapsed_time(m) for a, m, _ in ev]))
-    open_ms = float(np.mean([m.elapsed_time(z) for _, m, z in ev]))
+    seal_ms = float(np.mean([a.elapsed_time(m) for a, m, _ in ev.values()]))
+    open_ms = float(np.mean([m.elapsed_time(z) for _, m, z in ev.values()]))
     st = db.status_host()
     assert (st == 0).all(), "open failed inside the timed region"
     dt = ctrl.max(dt)

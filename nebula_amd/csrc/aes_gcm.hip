@@ -276,6 +276,31 @@ __device__ __forceinline__ uint4 aes256_ctr_block(const CtrConst& c, uint32_t ct
     return aes256_rounds<3>(u0, u1, u2, u3, T, rk);
 }
 
+// The same with every counter below 2^8 (packets under 4 KiB): byte 14 is zero too, so round 1
+// varies only through T3[byte 15] in column 0, and round 2 through the 4 bytes of that column,
+// one per output column: 1 + 4 lookups per block instead of 2 + 8.
+template <class RK>
+__device__ __forceinline__ CtrConst aes_ctr_prep8(uint32_t c1, uint32_t c2, const TLook& T, const RK& rk) {
+    CtrConst c = aes_ctr_prep(c1, c2, T, rk);
+    const uint4 k2 = rk.get(2);
+    c.K.y ^= T.t2(c.k0w, 2);  // round 1 column 1 is constant now
+    c.L.x = rotl8(T.t0(c.K.y, 1)) ^ T.t2(c.K.z, 2) ^ rotl8(T.t2(c.K.w, 3)) ^ k2.x;
+    c.L.y = T.t0(c.K.y, 0) ^ rotl8(T.t0(c.K.z, 1)) ^ T.t2(c.K.w, 2) ^ k2.y;
+    c.L.z = T.t0(c.K.z, 0) ^ rotl8(T.t0(c.K.w, 1) ^ T.t2(c.K.y, 3)) ^ k2.z;
+    c.L.w = T.t0(c.K.w, 0) ^ T.t2(c.K.y, 2) ^ rotl8(T.t2(c.K.z, 3)) ^ k2.w;
+    return c;
+}
+
+template <class RK>
+__device__ __forceinline__ uint4 aes256_ctr8_block(const CtrConst& c, uint32_t ctr, const TLook& T, const RK& rk) {
+    const uint32_t t0 = c.K.x ^ rotl8(T.t2(c.k0w ^ (ctr << 24), 3));
+    const uint32_t u0 = c.L.x ^ T.t0(t0, 0);
+    const uint32_t u1 = c.L.y ^ rotl8(T.t2(t0, 3));
+    const uint32_t u2 = c.L.z ^ T.t2(t0, 2);
+    const uint32_t u3 = c.L.w ^ rotl8(T.t0(t0, 1));
+    return aes256_rounds<3>(u0, u1, u2, u3, T, rk);
+}
+
 // ------------------------------------------------------------------------------------------
 // GF(2^128), GCM bit order. An element is 4 big-endian words w0..w3; the coefficient of x^j is
 // bit 31 - (j mod 32) of w[j / 32], so multiplying by x is a 128-bit logical right shift.
@@ -464,14 +489,16 @@ __device__ __forceinline__ uint4 gcm_lane_io(const neb_desc& d, const LaneBlock&
     return X;
 }
 
-// Keystream block of lane block b.
-template <bool CTRC, class RK>
+// Keystream block of lane block b. CM: counter-mode caching level — 0 none, 1 every counter of
+// the wave below 2^16, 2 below 2^8.
+template <int CM, class RK>
 __device__ __forceinline__ uint4 gcm_lane_ks(const LaneBlock& b, uint32_t c1, uint32_t c2, const CtrConst& cc,
                                              const TLook& T, const RK& rk) {
 #ifdef NEB_ABLATE_AES
     return make_uint4(c1 ^ b.ctr, c2, b.ctr * 0x9E3779B9u, cc.k0w);
 #else
-    if constexpr (CTRC) return aes256_ctr_block(cc, b.ctr, T, rk);
+    if constexpr (CM == 2) return aes256_ctr8_block(cc, b.ctr, T, rk);
+    else if constexpr (CM == 1) return aes256_ctr_block(cc, b.ctr, T, rk);
     else return aes256_block(0u, c1, c2, bswap32(b.ctr), T, rk);
 #endif
 }
@@ -566,10 +593,11 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     const uint32_t c2 = bswap32((uint32_t)d.counter);
     const TLook T{ttab, lb8};
     uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
-    auto rounds = [&](auto ctrc) {
-        constexpr bool CTRC = decltype(ctrc)::value;
+    auto rounds = [&](auto cm) {
+        constexpr int CM = decltype(cm)::value;
         CtrConst cc{};
-        if constexpr (CTRC) cc = aes_ctr_prep(c1, c2, T, rk);
+        if constexpr (CM == 2) cc = aes_ctr_prep8(c1, c2, T, rk);
+        else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
         for (uint32_t r = 0; r < Rmax; r++) {
             if (r < sh.R) {
                 const LaneBlock b = lane_block<kLpp>(sh, r, l);
@@ -581,7 +609,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
-                const uint4 ks = gcm_lane_ks<CTRC>(b, c1, c2, cc, T, rk);
+                const uint4 ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
 #ifndef NEB_NO_FASTIO
                 // the common round: every active lane holds a full, 16-B aligned payload block
                 const uint32_t off = 16u * (b.k - 1u);
@@ -599,9 +627,13 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
             }
         }
     };
-    // counter caching needs every block counter of every packet in the wave below 2^16
-    if (__all(sh.m + 1u < 65536u)) rounds(std::true_type{});
-    else rounds(std::false_type{});
+    // counter caching needs every block counter of every packet in the wave below 2^8 / 2^16
+#ifndef NEB_NO_CTR8
+    if (__all(sh.m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
+    else
+#endif
+    if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
+    else rounds(std::integral_constant<int, 0>{});
     if (run) {
         // GHASH = Σ_l A_l·H^(4-l) = (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, same table in every lane
         uint4 V = quad_bcast4<0>(A);

@@ -133,6 +133,24 @@ def test_edge_shapes(engine, oracle_mod, alg):
     assert np.array_equal(got_o, ref_o)
 
 
+@pytest.mark.parametrize("nkeys", [1, 2])
+@pytest.mark.parametrize("lens", [[1300, 4064, 17], [4065, 1300], [1048545, 100], [1048544, 0]])
+def test_counter_cache_tiers(engine, oracle_mod, nkeys, lens):
+    """The AES-CTR round-1/2 caching tiers are chosen per wave by the largest block counter:
+    below 2^8 (payload <= 4064 B), below 2^16 (<= 1048544 B), else the full cipher. Each batch
+    puts packets on both sides of a boundary into one wave; nkeys 1 = single-key kernel,
+    2 = the chunked mixed-key kernel."""
+    b = _edge_batch(L.ALG_AESGCM, lens, [16] * len(lens), nkeys=nkeys, seed=len(lens) * 7 + lens[0])
+    ref, _ = oracle_seal(oracle_mod, b)
+    got, st = run_device(engine, b, seal=True)
+    assert (st == 0).all()
+    assert np.array_equal(got, ref)
+    ref_o, _ = oracle_open(oracle_mod, b, ref)
+    got_o, st_o = run_device(engine, b, seal=False, arena=ref)
+    assert (st_o == 0).all()
+    assert np.array_equal(got_o, ref_o)
+
+
 @pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
 def test_unaligned_offsets(engine, oracle_mod, alg):
     """Descriptors may point anywhere (Go slices): odd AAD / payload offsets, out-of-place."""

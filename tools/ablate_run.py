@@ -1,4 +1,5 @@
-"""Time the seal kernel of the library at NEB_LIB_PATH on the C2 batch (ablation study only)."""
+"""Time the seal kernel of the library at NEB_LIB_PATH on a config batch (ablation study only):
+20 back-to-back seals, then 20 seal+open steps as bench.py runs them (kernel boundaries included)."""
 import sys, os, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -20,4 +21,16 @@ s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True
 s.record()
 for _ in range(20): db.seal()
 e.record(); torch.cuda.synchronize()
-print(os.environ.get("NEB_LIB_PATH"), "seal ms", s.elapsed_time(e) / 20, "pkts", b.n)
+seal_ms = s.elapsed_time(e) / 20
+db.open()
+for _ in range(3):
+    db.seal(); db.open()
+torch.cuda.synchronize()
+s.record()
+for _ in range(20):
+    db.seal(); db.open()
+e.record(); torch.cuda.synchronize()
+step_ms = s.elapsed_time(e) / 20
+assert (db.status_host() == 0).all()
+print(os.path.basename(os.environ.get("NEB_LIB_PATH", "default")), "seal ms %.4f" % seal_ms,
+      "step ms %.4f" % step_ms, "pkts", b.n)
