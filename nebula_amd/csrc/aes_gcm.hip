@@ -32,6 +32,7 @@
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
 #include "layout.hpp"
+#include "sched.hpp"
 
 namespace neb {
 
@@ -442,10 +443,9 @@ struct LaneBlock {
     bool is_aad, is_ct, is_len;
     uint32_t k, ctr;
 };
-template <uint32_t LPP>
-__device__ __forceinline__ LaneBlock lane_block(const PktShape& sh, uint32_t r, uint32_t l) {
+__device__ __forceinline__ LaneBlock lane_block(const PktShape& sh, uint32_t r, uint32_t l, uint32_t lg) {
     LaneBlock b;
-    b.g = (int32_t)(LPP * r + l + 1u) - (int32_t)sh.pad;
+    b.g = (int32_t)((r << lg) + l + 1u) - (int32_t)sh.pad;
     b.is_aad = b.g >= 1 && b.g <= (int32_t)sh.na;
     b.is_ct = b.g > (int32_t)sh.na && b.g <= (int32_t)(sh.na + sh.m);
     b.is_len = b.g == (int32_t)sh.n;
@@ -505,9 +505,9 @@ __device__ __forceinline__ uint4 gcm_lane_ks(const LaneBlock& b, uint32_t c1, ui
 
 // Tag finish on the packet's last lane, which holds E_K(J0) (seal: store; open: compare, zero
 // the payload on mismatch).
-template <bool OPEN, uint32_t LPP>
+template <bool OPEN>
 __device__ __forceinline__ uint32_t gcm_finish(const neb_desc& d, uint4 S, uint4 ej0, uint32_t lane, uint32_t l,
-                                               uint8_t* arena) {
+                                               uint32_t LPP, uint8_t* arena) {
     const uint4 tag = xor4(ej0, bswap4(S));  // valid on lane LPP-1
     uint32_t fail = 0;
     if (l == LPP - 1u) {
@@ -530,17 +530,20 @@ __device__ __forceinline__ uint32_t gcm_finish(const neb_desc& d, uint4 S, uint4
 }
 
 // ------------------------------------------------------------------------------------------
-// Packet groups: 4 lanes per packet, 16 packets per wave.
+// Packet groups: LPP = 2^lg lanes per packet (4 in the single-key kernel; 4, 8 or 16 per chunk in
+// the mixed-key kernel), 64 / LPP packets per wave.
 //
-// Lane l of a packet owns padded GHASH blocks g' = 4r + l + 1 (n' = 4·ceil(n/4); a 1300-byte
-// packet has n = 84, so nothing is padded). Horner stride H^4. The final Σ_l A_l·H^(4-l) runs as a
-// 4-step Horner over the quad with H's table, which every lane of a ds_read_b128 group reads at
-// once: no bank conflicts (per-lane power tables conflicted on every lookup and cost 17%).
+// Lane l of a packet owns padded GHASH blocks g' = LPP·r + l + 1 (n' = LPP·ceil(n/LPP); a
+// 1300-byte packet has n = 84, so at LPP 4 nothing is padded). Horner stride H^LPP. The final
+// Σ_l A_l·H^(LPP-l) multiplies with one table shared by every lane of a ds_read_b128 group at a
+// time: no bank conflicts (per-lane power tables conflicted on every lookup and cost 17%).
 // The round keys are wave-uniform (scalar registers) in both kernels below: one key per batch, or
 // one key per chunk of a regrouped mixed-key batch (sched.hpp).
 
-constexpr uint32_t kLpp = kFullPow;    // lanes per packet
-constexpr uint32_t kPpw = 64u / kLpp;  // packets per wave
+constexpr uint32_t kLg = 2;             // single-key kernel: log2 lanes per packet
+constexpr uint32_t kLpp = 1u << kLg;    // = kFullPow, the full table's power
+constexpr uint32_t kPpw = 64u / kLpp;   // packets per wave
+static_assert(kLpp == kFullPow, "the single-key Horner stride is the full table's power");
 
 // broadcast lane j of each quad (DPP quad_perm)
 template <int J>
@@ -551,27 +554,57 @@ template <int J>
 __device__ __forceinline__ uint4 quad_bcast4(uint4 v) {
     return make_uint4(quad_bcast<J>(v.x), quad_bcast<J>(v.y), quad_bcast<J>(v.z), quad_bcast<J>(v.w));
 }
+__device__ __forceinline__ uint4 shfl4(uint4 v, uint32_t src) {
+    return make_uint4(__shfl(v.x, (int)src), __shfl(v.y, (int)src), __shfl(v.z, (int)src), __shfl(v.w, (int)src));
+}
+__device__ __forceinline__ uint4 shfl_down4(uint4 v, uint32_t d) {
+    return make_uint4(__shfl_down(v.x, d), __shfl_down(v.y, d), __shfl_down(v.z, d), __shfl_down(v.w, d));
+}
 
-// GHASH tables a packet group multiplies with.
-struct GhFull {  // one key per batch: reduction-free full table for H^4 + Shoup table for H
+// GHASH tables a packet group multiplies with: horner(A) = A·H^LPP, and final(A) = the packet's
+// Σ_l A_l·H^(LPP-l), valid at least on the packet's last lane (the one holding E_K(J0)).
+struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 + Shoup table for H
     const uint4* full;
     const uint4* shoup_h;
-    __device__ __forceinline__ uint4 horner(uint4 a) const { return gf_mul_full(a, make_uint4(0, 0, 0, 0), full); }
-    __device__ __forceinline__ uint4 mul_h(uint4 a) const { return gf_mul_shoup(a, 0u, shoup_h); }
+    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const {
+        return gf_mul_full(a, make_uint4(0, 0, 0, 0), full);
+    }
+    // (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, computed identically in the 4 lanes of the quad
+    __device__ __forceinline__ uint4 final(uint4 A, uint32_t, uint32_t) const {
+        uint4 V = quad_bcast4<0>(A);
+#ifndef NEB_ABLATE_FINAL
+        V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<1>(A));
+        V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<2>(A));
+        V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<3>(A));
+        V = gf_mul_shoup(V, 0u, shoup_h);
+#endif
+        return V;
+    }
 };
-struct GhShoup {  // one key per chunk: Shoup tables for H^4 and H staged in the wave's LDS slice
-    const uint4* base;  // table H at +0, H^4 at +256
-    __device__ __forceinline__ uint4 horner(uint4 a) const { return gf_mul_shoup(a, 256u, base); }
-    __device__ __forceinline__ uint4 mul_h(uint4 a) const { return gf_mul_shoup(a, 0u, base); }
+constexpr uint32_t kChunkTables = 5;  // Shoup tables H, H^2, H^4, H^8, H^16 (table i = H^(2^i))
+struct GhShoup {  // one key per chunk: its Shoup tables staged in the wave's LDS slice
+    const uint4* base;
+    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t lg) const { return gf_mul_shoup(a, lg * 256u, base); }
+    // Pairwise tree over the packet's lanes: level i folds V_l·H^(2^i) ⊕ V_(l+2^i) into the lanes
+    // l ≡ 0 mod 2^(i+1); after lg levels lane 0 holds Z with Σ_l A_l·H^(LPP-l) = Z·H.
+    // lg + 1 multiplies instead of a Horner's LPP.
+    __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
+        uint4 V = A;
+        for (uint32_t i = 0; i < lg; i++) V = xor4(gf_mul_shoup(V, i * 256u, base), shfl_down4(V, 1u << i));
+        V = gf_mul_shoup(V, 0u, base);
+        return shfl4(V, lane & ~((1u << lg) - 1u));
+    }
 };
 
-// Seal or open packet `p` (lanes q*4 .. q*4+3 of the wave). `expect_key`: the key this wave's
-// round keys and tables belong to; key_ok: that key is installed with the right algorithm.
+// Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
+// this wave's round keys and tables belong to; key_ok: that key is installed with the right
+// algorithm. lg is wave-uniform.
 template <bool OPEN, class GH>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const uint2* ttab,
-                                                 uint2 lb8, uint32_t lane) {
-    const uint32_t l = lane % kLpp;
+                                                 uint2 lb8, uint32_t lane, uint32_t lg) {
+    const uint32_t LPP = 1u << lg;
+    const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
     if (valid) d = args.desc[p];
     uint32_t st = NEB_STATUS_OK;
@@ -582,11 +615,10 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     sh.na = (d.aad_len + 15u) >> 4;
     sh.m = (d.len + 15u) >> 4;
     sh.n = sh.na + sh.m + 1u;
-    sh.R = run ? (sh.n + kLpp - 1u) / kLpp : 0u;
-    sh.pad = kLpp * sh.R - sh.n;
+    sh.R = run ? (sh.n + LPP - 1u) >> lg : 0u;
+    sh.pad = (sh.R << lg) - sh.n;
     uint32_t Rmax = sh.R;
-#pragma unroll
-    for (int s = (int)kLpp; s < 64; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, s));
+    for (uint32_t s = LPP; s < 64u; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, (int)s));
 
     // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
     const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
@@ -600,13 +632,13 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
         for (uint32_t r = 0; r < Rmax; r++) {
             if (r < sh.R) {
-                const LaneBlock b = lane_block<kLpp>(sh, r, l);
-                // GHASH of the previous rounds (A·H^4) first, then this round's AES: one phase's
+                const LaneBlock b = lane_block(sh, r, l, lg);
+                // GHASH of the previous rounds (A·H^LPP) first, then this round's AES: one phase's
                 // registers at a time keeps the kernel at 4 waves/SIMD without spills
 #ifdef NEB_ABLATE_HORNER
                 const uint4 G = A;
 #else
-                const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A);
+                const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A, lg);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
                 const uint4 ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
@@ -634,18 +666,9 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
 #endif
     if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
     else rounds(std::integral_constant<int, 0>{});
-    if (run) {
-        // GHASH = Σ_l A_l·H^(4-l) = (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, same table in every lane
-        uint4 V = quad_bcast4<0>(A);
-#ifndef NEB_ABLATE_FINAL
-        V = xor4(gh.mul_h(V), quad_bcast4<1>(A));
-        V = xor4(gh.mul_h(V), quad_bcast4<2>(A));
-        V = xor4(gh.mul_h(V), quad_bcast4<3>(A));
-        V = gh.mul_h(V);
-#endif
-        if (gcm_finish<OPEN, kLpp>(d, V, ej0, lane, l, args.arena)) st = NEB_STATUS_AUTH_FAILED;
-    }
-    if (valid && l == kLpp - 1u) args.status[p] = (int32_t)st;
+    const uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
+    if (run && gcm_finish<OPEN>(d, V, ej0, lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
+    if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
 }
 
 __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rks[60]) {
@@ -693,7 +716,7 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
     for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
         const uint32_t p = grp * kPpw + lane / kLpp;
-        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, true, rk, gh, lds.ttab, lb8, lane);
+        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, true, rk, gh, lds.ttab, lb8, lane, kLg);
     }
 }
 
@@ -703,17 +726,19 @@ constexpr int kChunkWaves = 8;
 constexpr int kChunkThreads = kChunkWaves * kWave;
 
 struct ChunkLds {
-    uint4 shoup[kChunkWaves][2][16];  // per wave: M[v] for H (+0) and H^4 (+256)
-    uint2 ttab[256 * 32];             // 64 KiB T-table pairs, 32 copies
+    uint4 shoup[kChunkWaves][kChunkTables][16];  // per wave: M[v] for H, H^2, H^4, H^8, H^16 (10 KiB)
+    uint2 ttab[256 * 32];                        // 64 KiB T-table pairs, 32 copies
 };
 
 struct ChunkArgs {
     const uint32_t* sorted;
     const uint4* chunks;
-    const uint32_t* nchunks;  // device counter written by the scheduler
+    uint32_t* counters;  // the scheduler's counters (sched.hpp kCnt*)
     uint32_t max_chunks;
 };
 
+// Chunks come from a work cursor, full ones first (chunks[0, F)), then the tails stored from the
+// end of the array: waves that drew cheap chunks draw again, and the cheap chunks run last.
 template <bool OPEN>
 __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs args, ChunkArgs ca) {
     __shared__ ChunkLds lds;
@@ -721,34 +746,49 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
     const uint2 lb8 = ttab_lane_base(lane);
+    const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
+    const uint32_t nback = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
+    const uint32_t nch = nfront + nback;
+    if (blockIdx.x * (uint32_t)kChunkWaves >= nch) return;  // uniform over the workgroup
     for (uint32_t i = tid; i < 256u * 32u; i += kChunkThreads) lds.ttab[i] = ttab_entry(i);
     __syncthreads();
     uint4* wtab = &lds.shoup[wave][0][0];
     const GhShoup gh{wtab};
-    uint32_t nch = __builtin_amdgcn_readfirstlane(*ca.nchunks);
-    nch = nch < ca.max_chunks ? nch : ca.max_chunks;
 
-    for (uint32_t c = blockIdx.x * kChunkWaves + wave; c < nch; c += gridDim.x * kChunkWaves) {
-        const uint4 ch = ca.chunks[c];  // {start, count, key, class}, wave-uniform
+    // First chunk: the wave's own index; later ones from the work cursor once a chunk is done, so
+    // waves that drew short chunks draw again (longest first: front, then back). Every wave
+    // pulling its first chunk off one atomic word at launch would serialise ~4096 dequeues at
+    // ≈88/µs (MI355X_MICROARCH.md, dequeue).
+    const uint32_t nwaves = gridDim.x * kChunkWaves;
+    for (uint32_t c = blockIdx.x * kChunkWaves + wave; c < nch;) {
+        const uint4 ch = ca.chunks[c < nfront ? c : ca.max_chunks - 1u - (c - nfront)];  // wave-uniform
         const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
         const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
         const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
+        const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);
         const uint32_t* rec = args.keys + (size_t)(key < args.max_keys ? key : 0u) * kKeyRecDwords;
         const bool key_ok = key < args.max_keys && rec[kRecAlg] == NEB_ALG_AESGCM;
         uint32_t rks[60];
         load_round_keys(rec, rks);
-        // stage the chunk key's Shoup tables for H (table 0) and H^4 (table 3)
-        if (lane < 32u) wtab[lane] = ld_rec4(rec, kRecShoup + (lane < 16u ? 0u : 3u * 64u - 64u) + 4u * lane);
+        // stage the chunk key's Shoup tables H^(2^i), i = 0..4 (record tables 0, 1, 3, 7, 15)
+        wtab[lane] = ld_rec4(rec, kRecShoup + 64u * ((1u << (lane >> 4)) - 1u) + 4u * (lane & 15u));
+        if (lane < 16u) wtab[64u + lane] = ld_rec4(rec, kRecShoup + 64u * 15u + 4u * lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t q = lane / kLpp;
+        const uint32_t q = lane >> lg;
         const bool valid = q < count;
         const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, lds.ttab, lb8, lane);
+        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, lds.ttab, lb8, lane, lg);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t next = nch;
+        if (nch > nwaves) {
+            if (lane == 0u) next = atomicAdd(&ca.counters[kCntWork], 1u);
+            next = nwaves + __builtin_amdgcn_readfirstlane(next);
+        }
+        c = next;
     }
 }
 
@@ -888,11 +928,13 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
-                                            const uint32_t* d_nchunks, uint32_t max_chunks, int cu_count,
+                                            uint32_t* d_counters, uint32_t max_chunks, int cu_count,
                                             hipStream_t s) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr};
-    neb::ChunkArgs ca{d_sorted, d_chunks, d_nchunks, max_chunks};
-    const uint32_t bound = (n + neb::kPpw - 1u) / neb::kPpw;  // enough waves for the typical chunk count
+    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks};
+    // one wave per chunk up to the occupancy cap (tails make chunks outnumber n / 16); the chunk
+    // count is only known on the device: workgroups past it exit before filling their tables
+    const uint32_t bound = max_chunks;
     return open ? launch_grid(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, a, ca)
                 : launch_grid(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, a, ca);
 }

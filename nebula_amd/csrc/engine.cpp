@@ -24,7 +24,7 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
-                                            const uint32_t* d_nchunks, uint32_t max_chunks, int cu_count,
+                                            uint32_t* d_counters, uint32_t max_chunks, int cu_count,
                                             hipStream_t s);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
@@ -317,7 +317,8 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
     const uint32_t nb = neb::sched_nbins(e->max_keys);
     const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys);
-    const size_t b_counters = align_up((2u + 2u * (size_t)nb) * 4u, 256), b_base = align_up((size_t)nb * 4u, 256);
+    const size_t b_counters = align_up((neb::kSchedCounters + 2u * (size_t)nb) * 4u, 256);
+    const size_t b_base = align_up((size_t)nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = (size_t)mc * 16u;
     const size_t bytes = b_counters + b_base + 2 * b_idx + b_chunks;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
@@ -329,7 +330,7 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     if (err != hipSuccess) return err;
     uint8_t* m = sp.mem;
     sp.ws.counters = (uint32_t*)m;
-    sp.ws.hist = sp.ws.counters + 2;
+    sp.ws.hist = sp.ws.counters + neb::kSchedCounters;
     sp.ws.fill = sp.ws.hist + nb;
     m += b_counters;
     sp.ws.base = (uint32_t*)m;
@@ -362,7 +363,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                        sp.ws.chunks, sp.ws.counters + 1, sp.ws.max_chunks, e->cu_count, s);
+                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count, s);
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
         return err;
     }

@@ -32,13 +32,30 @@ __global__ void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
     for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x) {
         const uint32_t c = ws.hist[b];
         if (c == 0u) continue;
-        const uint32_t base = atomicAdd(&ws.counters[0], c);
+        const uint32_t base = atomicAdd(&ws.counters[kCntPackets], c);
         ws.base[b] = base;
-        const uint32_t nch = (c + kChunkPkts - 1u) / kChunkPkts;
-        const uint32_t cb = atomicAdd(&ws.counters[1], nch);
         const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
-        for (uint32_t j = 0; j < nch && cb + j < ws.max_chunks; j++)
-            ws.chunks[cb + j] = make_uint4(base + j * kChunkPkts, min(kChunkPkts, c - j * kChunkPkts), key, cls);
+        const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
+        // chunks at 4 lanes per packet (the long ones) from the front, the short tails from the
+        // back: the crypto kernel takes them in that order. Front <= n/16 + bins, back <= bins and
+        // front + back <= n/16 + min(n, bins): the ranges never meet inside max_chunks
+        // (sched_max_chunks).
+        if (nfull) {
+            const uint32_t cb = atomicAdd(&ws.counters[kCntFrontChunks], nfull);
+            for (uint32_t j = 0; j < nfull && cb + j < ws.max_chunks; j++)
+                ws.chunks[cb + j] = make_uint4(base + j * kChunkPkts, kChunkPkts, key, cls | (2u << kChunkLgShift));
+        }
+        if (tail) {
+            const uint32_t lg = sched_tail_lg(tail, cls);
+            const uint4 ch = make_uint4(base + nfull * kChunkPkts, tail, key, cls | (lg << kChunkLgShift));
+            if (lg == 2u) {
+                const uint32_t t = atomicAdd(&ws.counters[kCntFrontChunks], 1u);
+                if (t < ws.max_chunks) ws.chunks[t] = ch;
+            } else {
+                const uint32_t t = atomicAdd(&ws.counters[kCntBackChunks], 1u);
+                if (t < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - t] = ch;
+            }
+        }
     }
 }
 
@@ -58,7 +75,7 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
                                       uint32_t lpp, const neb::SchedWs* ws, hipStream_t s) {
     const uint32_t nb = neb::sched_nbins(max_keys);
     // counters, hist and fill are contiguous: one memset per batch
-    hipError_t e = hipMemsetAsync(ws->counters, 0, (2u + 2u * nb) * sizeof(uint32_t), s);
+    hipError_t e = hipMemsetAsync(ws->counters, 0, (neb::kSchedCounters + 2u * nb) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;

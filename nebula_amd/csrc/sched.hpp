@@ -15,17 +15,39 @@
 
 namespace neb {
 
-constexpr uint32_t kChunkPkts = 16;   // packets per wavefront (4 lanes each)
-constexpr uint32_t kSizeClasses = 8;  // round-count classes: 1, 2, 3-4, 5-8, 9-16, 17-32, 33-64, 65+
+constexpr uint32_t kChunkPkts = 16;   // packets per full chunk (4 lanes each)
+constexpr uint32_t kSizeClasses = 8;  // round-count classes at 4 lanes per packet: 1, 2, 3-4, 5-8, 9-16, 17-32, 33-64, 65+
+
+// A bin of c packets becomes c / 16 full chunks of 16 packets at 4 lanes per packet, and one tail
+// chunk of the c mod 16 others at 2^lg lanes per packet: lg 4 (16 lanes) for up to 4 packets, 3
+// for up to 8, else 2 — capped for short packets so that no lane idles on a block that does not
+// exist (size class 0: <= 4 blocks, lg 2; class 1: <= 8 blocks, lg 3). A wave then runs a tail of
+// 1-4 packets in a quarter of the rounds instead of leaving 48-60 of its lanes idle.
+constexpr uint32_t kChunkLgShift = 8;  // chunk.w = size class | lg << kChunkLgShift
+__host__ __device__ inline uint32_t sched_tail_lg(uint32_t count, uint32_t cls) {
+    const uint32_t fit = count <= 4u ? 4u : (count <= 8u ? 3u : 2u);
+    const uint32_t size = cls == 0u ? 2u : (cls == 1u ? 3u : 4u);
+#ifdef NEB_TAIL_LG_MAX  // ablation: cap the tail chunks' lanes per packet
+    if (fit > NEB_TAIL_LG_MAX) return NEB_TAIL_LG_MAX;
+#endif
+    return fit < size ? fit : size;
+}
+
+// counters[] slots
+constexpr uint32_t kCntPackets = 0;      // cursor into sorted[]
+constexpr uint32_t kCntFrontChunks = 1;  // chunks at 4 lanes per packet (full or 9-15 packets), chunks[0, F)
+constexpr uint32_t kCntBackChunks = 2;   // tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
+constexpr uint32_t kCntWork = 3;         // the crypto kernel's chunk cursor (front chunks first)
+constexpr uint32_t kSchedCounters = 4;
 
 struct SchedWs {          // device workspace, sized for n packets and nbins bins
-    uint32_t* counters;   // [0] packet cursor, [1] chunk count, then hist[nbins], fill[nbins]
+    uint32_t* counters;   // [kSchedCounters] counters, then hist[nbins], fill[nbins]
     uint32_t* hist;
     uint32_t* fill;
     uint32_t* base;       // [nbins] output offset of each non-empty bin
     uint32_t* binof;      // [n] bin of each packet
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
-    uint4* chunks;        // [max_chunks] {start in sorted, count, key_id, size class}
+    uint4* chunks;        // [max_chunks] {start in sorted, count, key_id, size class | lg << 8}
     uint32_t max_chunks;
 };
 

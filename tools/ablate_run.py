@@ -2,6 +2,7 @@
 20 back-to-back seals, then 20 seal+open steps as bench.py runs them (kernel boundaries included)."""
 import sys, os, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
 import torch
 from nebula_amd import workload as W
 from nebula_amd.batch import DeviceBatch, install_keys
@@ -11,6 +12,10 @@ if cfg == 4:
     b = W.make_batch(1, 65536, 4096, sizes=(90, 576, 1300), ratio=(7, 4, 1))
 elif cfg == 5:  # 61440 wave-groups: divides evenly over 16, 20 and 24 waves per CU
     b = W.make_batch(1, 983040, 1)
+elif cfg in (6, 7):  # exactly 4 (6) or 16 (7) packets per key, 4096 keys: all tail / all full chunks
+    per = 4 if cfg == 6 else 16
+    b = W.make_batch(1, 4096 * per, 4096)
+    b.desc["key_id"] = np.arange(b.n, dtype=np.uint32) % 4096
 else:
     b = W.config(cfg)
 eng = Engine(0, 4096)
