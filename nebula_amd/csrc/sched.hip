@@ -2,6 +2,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include "sched.hpp"
 
 namespace neb {
@@ -26,35 +28,50 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
     }
 }
 
-// pass 2: every non-empty bin reserves its range of `sorted` and its chunks
-__global__ void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
+// pass 2: every non-empty bin reserves its range of `sorted` and its chunks. The reservations are
+// aggregated per workgroup (block scans, then one atomic per counter and workgroup): one atomic per
+// bin put ~4096 returning atomics on a single word for a 4096-tunnel batch.
+constexpr int kAllocThreads = 256;
+__global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
+    using Scan = hipcub::BlockScan<uint32_t, kAllocThreads>;
+    __shared__ typename Scan::TempStorage tmp;
+    __shared__ uint32_t wg_base[3];
     const uint32_t nb = sched_nbins(max_keys);
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x) {
-        const uint32_t c = ws.hist[b];
-        if (c == 0u) continue;
-        const uint32_t base = atomicAdd(&ws.counters[kCntPackets], c);
-        ws.base[b] = base;
-        const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
-        const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
-        // chunks at 4 lanes per packet (the long ones) from the front, the short tails from the
-        // back: the crypto kernel takes them in that order. Front <= n/16 + bins, back <= bins and
-        // front + back <= n/16 + min(n, bins): the ranges never meet inside max_chunks
-        // (sched_max_chunks).
-        if (nfull) {
-            const uint32_t cb = atomicAdd(&ws.counters[kCntFrontChunks], nfull);
-            for (uint32_t j = 0; j < nfull && cb + j < ws.max_chunks; j++)
-                ws.chunks[cb + j] = make_uint4(base + j * kChunkPkts, kChunkPkts, key, cls | (2u << kChunkLgShift));
-        }
-        if (tail) {
-            const uint32_t lg = sched_tail_lg(tail, cls);
-            const uint4 ch = make_uint4(base + nfull * kChunkPkts, tail, key, cls | (lg << kChunkLgShift));
-            if (lg == 2u) {
-                const uint32_t t = atomicAdd(&ws.counters[kCntFrontChunks], 1u);
-                if (t < ws.max_chunks) ws.chunks[t] = ch;
-            } else {
-                const uint32_t t = atomicAdd(&ws.counters[kCntBackChunks], 1u);
-                if (t < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - t] = ch;
-            }
+    const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
+    const uint32_t c = b < nb ? ws.hist[b] : 0u;
+    const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
+    const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
+    const uint32_t lg = tail ? sched_tail_lg(tail, cls) : 2u;
+    // chunks at 4 lanes per packet (the long ones) go to the front, the short tails to the back:
+    // the crypto kernel takes them in that order. Front <= n/16 + bins, back <= bins and
+    // front + back <= n/16 + min(n, bins): the ranges never meet inside max_chunks
+    // (sched_max_chunks).
+    const uint32_t nfront = nfull + (tail && lg == 2u ? 1u : 0u), nback = tail && lg != 2u ? 1u : 0u;
+    uint32_t off_p, off_f, off_b, tot_p, tot_f, tot_b;
+    Scan(tmp).ExclusiveSum(c, off_p, tot_p);
+    __syncthreads();
+    Scan(tmp).ExclusiveSum(nfront, off_f, tot_f);
+    __syncthreads();
+    Scan(tmp).ExclusiveSum(nback, off_b, tot_b);
+    if (threadIdx.x == 0) {
+        wg_base[0] = tot_p ? atomicAdd(&ws.counters[kCntPackets], tot_p) : 0u;
+        wg_base[1] = tot_f ? atomicAdd(&ws.counters[kCntFrontChunks], tot_f) : 0u;
+        wg_base[2] = tot_b ? atomicAdd(&ws.counters[kCntBackChunks], tot_b) : 0u;
+    }
+    __syncthreads();
+    if (c == 0u) return;
+    const uint32_t base = wg_base[0] + off_p;
+    ws.base[b] = base;
+    const uint32_t cf = wg_base[1] + off_f;
+    for (uint32_t j = 0; j < nfull && cf + j < ws.max_chunks; j++)
+        ws.chunks[cf + j] = make_uint4(base + j * kChunkPkts, kChunkPkts, key, cls | (2u << kChunkLgShift));
+    if (tail) {
+        const uint4 ch = make_uint4(base + nfull * kChunkPkts, tail, key, cls | (lg << kChunkLgShift));
+        if (lg == 2u) {
+            if (cf + nfull < ws.max_chunks) ws.chunks[cf + nfull] = ch;
+        } else {
+            const uint32_t t = wg_base[2] + off_b;
+            if (t < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - t] = ch;
         }
     }
 }
@@ -79,9 +96,9 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     if (e != hipSuccess) return e;
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
-    const uint32_t gb = (nb + tpb - 1) / tpb < 4096u ? (nb + tpb - 1) / tpb : 4096u;
     hipLaunchKernelGGL(neb::sched_hist_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp, *ws);
-    hipLaunchKernelGGL(neb::sched_alloc_kernel, dim3(gb), dim3(tpb), 0, s, max_keys, *ws);
+    hipLaunchKernelGGL(neb::sched_alloc_kernel, dim3((nb + neb::kAllocThreads - 1) / neb::kAllocThreads),
+                       dim3(neb::kAllocThreads), 0, s, max_keys, *ws);
     hipLaunchKernelGGL(neb::sched_scatter_kernel, dim3(gp), dim3(tpb), 0, s, n, d_n, *ws);
     return hipGetLastError();
 }
