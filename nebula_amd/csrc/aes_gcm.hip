@@ -148,6 +148,44 @@ struct TLook {
     __device__ __forceinline__ uint32_t t2(uint32_t s, int k) const {
         return lds_at<uint32_t>(ttab, perm(s, lb.y, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
     }
+    __device__ __forceinline__ uint32_t t1(uint32_t s, int k) const { return rotl8(t0(s, k)); }
+    __device__ __forceinline__ uint32_t t3(uint32_t s, int k) const { return rotl8(t2(s, k)); }
+    // the round's row-1/row-3 lookups before their rotation (one rotate per column, below)
+    __device__ __forceinline__ uint32_t t1r(uint32_t s, int k) const { return t0(s, k); }
+    __device__ __forceinline__ uint32_t t3r(uint32_t s, int k) const { return t2(s, k); }
+    static constexpr bool kFour = false;
+};
+
+// Four T-tables (T0..T3) in LDS, 128 KiB: region A (byte offset 0) holds the pairs (T0[x], T1[x]),
+// region B (offset 64 KiB) the pairs (T2[x], T3[x]), each laid out and swizzled like TLook's
+// (32 copies, copy c of entry x at x*256 + c*8, the two dwords swapped for c >= 16). A round then
+// combines each column with two XOR3s and no rotates (8 VALU per round fewer than TLook), at
+// the price of one 1024-lane workgroup per CU. One lane base serves all four tables: byte 0 =
+// the lane's row-0/row-2 dword offset in its 256-byte row, byte 3 = its row-1/row-3 dword offset,
+// byte 2 = 1 (region B); each lookup's v_perm picks byte 0 or 3 and zero or byte 2.
+__device__ __forceinline__ uint32_t ttab4_lane_base(uint32_t lane) {
+    const uint32_t c = lane & 31u, hi = c >> 4;
+    return ((c << 3) | (hi << 2)) | (1u << 16) | (((c << 3) | ((hi ^ 1u) << 2)) << 24);
+}
+__device__ __forceinline__ uint2 ttab4_entry(uint32_t i) {  // i = region*8192 + x*32 + c
+    uint32_t t = c_T0.t[(i >> 5) & 255u];
+    if (i & 8192u) t = __builtin_amdgcn_alignbit(t, t, 16);  // T2 = rotl16 T0
+    const uint32_t t1 = rotl8(t);                            // T1 = rotl8 T0, T3 = rotl8 T2
+    return (i & 16u) ? make_uint2(t1, t) : make_uint2(t, t1);
+}
+struct TLook4 {
+    const uint2* ttab;
+    uint32_t lb;
+    __device__ __forceinline__ uint32_t at(uint32_t s, int k, uint32_t sel) const {
+        return lds_at<uint32_t>(ttab, perm(s, lb, sel | ((4u + (uint32_t)k) << 8)));
+    }
+    __device__ __forceinline__ uint32_t t0(uint32_t s, int k) const { return at(s, k, 0x0C0C0000u); }
+    __device__ __forceinline__ uint32_t t1(uint32_t s, int k) const { return at(s, k, 0x0C0C0003u); }
+    __device__ __forceinline__ uint32_t t2(uint32_t s, int k) const { return at(s, k, 0x0C020000u); }
+    __device__ __forceinline__ uint32_t t3(uint32_t s, int k) const { return at(s, k, 0x0C020003u); }
+    __device__ __forceinline__ uint32_t t1r(uint32_t s, int k) const { return t1(s, k); }
+    __device__ __forceinline__ uint32_t t3r(uint32_t s, int k) const { return t3(s, k); }
+    static constexpr bool kFour = true;
 };
 
 // Wave priority while a round's 16 lookups are issued (s_setprio): the SIMD arbiter then prefers
@@ -159,8 +197,8 @@ struct TLook {
 #endif
 
 // AES-256 rounds FIRST..13 (full) and 14 (final) on the state s0..s3 (after round FIRST-1).
-template <int FIRST, class RK>
-__device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, const TLook& T,
+template <int FIRST, class TL, class RK>
+__device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, const TL& T,
                                                const RK& rk) {
     uint4 k;
 #pragma unroll
@@ -170,15 +208,15 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(NEB_PRIO);
 #endif
-        const uint32_t a0 = T.t0(s0, 0), a1 = T.t0(s1, 1), a2 = T.t2(s2, 2), a3 = T.t2(s3, 3);
-        const uint32_t b0 = T.t0(s1, 0), b1 = T.t0(s2, 1), b2 = T.t2(s3, 2), b3 = T.t2(s0, 3);
-        const uint32_t c0 = T.t0(s2, 0), c1 = T.t0(s3, 1), c2 = T.t2(s0, 2), c3 = T.t2(s1, 3);
-        const uint32_t d0 = T.t0(s3, 0), d1 = T.t0(s0, 1), d2 = T.t2(s1, 2), d3 = T.t2(s2, 3);
+        const uint32_t a0 = T.t0(s0, 0), a1 = T.t1r(s1, 1), a2 = T.t2(s2, 2), a3 = T.t3r(s3, 3);
+        const uint32_t b0 = T.t0(s1, 0), b1 = T.t1r(s2, 1), b2 = T.t2(s3, 2), b3 = T.t3r(s0, 3);
+        const uint32_t c0 = T.t0(s2, 0), c1 = T.t1r(s3, 1), c2 = T.t2(s0, 2), c3 = T.t3r(s1, 3);
+        const uint32_t d0 = T.t0(s3, 0), d1 = T.t1r(s0, 1), d2 = T.t2(s1, 2), d3 = T.t3r(s2, 3);
 #if NEB_PRIO
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(0);
 #endif
-        // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k, T1 = rotl8 T0, T3 = rotl8 T2
+        // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k; with two tables T1 = rotl8 T0, T3 = rotl8 T2
 #ifdef NEB_DUMMY_VALU
         {  // experiment: extra VALU work per round that feeds nothing but a final register
             uint32_t d0 = s0 ^ 0x1234u, d1 = s1 ^ 0x5678u;
@@ -190,7 +228,19 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
             asm volatile("" ::"v"(d0), "v"(d1));
         }
 #endif
-        if constexpr (RK::kUniform) {
+        if constexpr (TL::kFour) {
+            if constexpr (RK::kUniform) {
+                s0 = x3s(x3(a0, a1, a2), a3, k.x);
+                s1 = x3s(x3(b0, b1, b2), b3, k.y);
+                s2 = x3s(x3(c0, c1, c2), c3, k.z);
+                s3 = x3s(x3(d0, d1, d2), d3, k.w);
+            } else {
+                s0 = x3(x3(a0, a1, a2), a3, k.x);
+                s1 = x3(x3(b0, b1, b2), b3, k.y);
+                s2 = x3(x3(c0, c1, c2), c3, k.z);
+                s3 = x3(x3(d0, d1, d2), d3, k.w);
+            }
+        } else if constexpr (RK::kUniform) {
             s0 = x3s(a0, a2, k.x) ^ rotl8(a1 ^ a3);
             s1 = x3s(b0, b2, k.y) ^ rotl8(b1 ^ b3);
             s2 = x3s(c0, c2, k.z) ^ rotl8(c1 ^ c3);
@@ -231,8 +281,8 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
     return o;
 }
 
-template <class RK>
-__device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, const TLook& T,
+template <class TL, class RK>
+__device__ __forceinline__ uint4 aes256_block(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, const TL& T,
                                               const RK& rk) {
     const uint4 k = rk.get(0);
     return aes256_rounds<1>(s0 ^ k.x, s1 ^ k.y, s2 ^ k.z, s3 ^ k.w, T, rk);
@@ -248,8 +298,8 @@ struct CtrConst {
     uint32_t k0w;  // word 3 of round key 0
 };
 
-template <class RK>
-__device__ __forceinline__ CtrConst aes_ctr_prep(uint32_t c1, uint32_t c2, const TLook& T, const RK& rk) {
+template <class TL, class RK>
+__device__ __forceinline__ CtrConst aes_ctr_prep(uint32_t c1, uint32_t c2, const TL& T, const RK& rk) {
     const uint4 k0 = rk.get(0), k1 = rk.get(1), k2 = rk.get(2);
     const uint32_t s0 = k0.x, s1 = c1 ^ k0.y, s2 = c2 ^ k0.z, s3 = k0.w;  // counter bytes = 0
     CtrConst c;
@@ -265,23 +315,23 @@ __device__ __forceinline__ CtrConst aes_ctr_prep(uint32_t c1, uint32_t c2, const
     return c;
 }
 
-template <class RK>
-__device__ __forceinline__ uint4 aes256_ctr_block(const CtrConst& c, uint32_t ctr, const TLook& T, const RK& rk) {
+template <class TL, class RK>
+__device__ __forceinline__ uint4 aes256_ctr_block(const CtrConst& c, uint32_t ctr, const TL& T, const RK& rk) {
     const uint32_t s3 = c.k0w ^ bswap32(ctr);
-    const uint32_t t0 = c.K.x ^ rotl8(T.t2(s3, 3));
+    const uint32_t t0 = c.K.x ^ T.t3(s3, 3);
     const uint32_t t1 = c.K.y ^ T.t2(s3, 2);
-    const uint32_t u0 = x3(c.L.x, T.t0(t0, 0), rotl8(T.t0(t1, 1)));
-    const uint32_t u1 = x3(c.L.y, T.t0(t1, 0), rotl8(T.t2(t0, 3)));
-    const uint32_t u2 = x3(c.L.z, T.t2(t0, 2), rotl8(T.t2(t1, 3)));
-    const uint32_t u3 = x3(c.L.w, T.t2(t1, 2), rotl8(T.t0(t0, 1)));
+    const uint32_t u0 = x3(c.L.x, T.t0(t0, 0), T.t1(t1, 1));
+    const uint32_t u1 = x3(c.L.y, T.t0(t1, 0), T.t3(t0, 3));
+    const uint32_t u2 = x3(c.L.z, T.t2(t0, 2), T.t3(t1, 3));
+    const uint32_t u3 = x3(c.L.w, T.t2(t1, 2), T.t1(t0, 1));
     return aes256_rounds<3>(u0, u1, u2, u3, T, rk);
 }
 
 // The same with every counter below 2^8 (packets under 4 KiB): byte 14 is zero too, so round 1
 // varies only through T3[byte 15] in column 0, and round 2 through the 4 bytes of that column,
 // one per output column: 1 + 4 lookups per block instead of 2 + 8.
-template <class RK>
-__device__ __forceinline__ CtrConst aes_ctr_prep8(uint32_t c1, uint32_t c2, const TLook& T, const RK& rk) {
+template <class TL, class RK>
+__device__ __forceinline__ CtrConst aes_ctr_prep8(uint32_t c1, uint32_t c2, const TL& T, const RK& rk) {
     CtrConst c = aes_ctr_prep(c1, c2, T, rk);
     const uint4 k2 = rk.get(2);
     c.K.y ^= T.t2(c.k0w, 2);  // round 1 column 1 is constant now
@@ -292,13 +342,13 @@ __device__ __forceinline__ CtrConst aes_ctr_prep8(uint32_t c1, uint32_t c2, cons
     return c;
 }
 
-template <class RK>
-__device__ __forceinline__ uint4 aes256_ctr8_block(const CtrConst& c, uint32_t ctr, const TLook& T, const RK& rk) {
-    const uint32_t t0 = c.K.x ^ rotl8(T.t2(c.k0w ^ (ctr << 24), 3));
+template <class TL, class RK>
+__device__ __forceinline__ uint4 aes256_ctr8_block(const CtrConst& c, uint32_t ctr, const TL& T, const RK& rk) {
+    const uint32_t t0 = c.K.x ^ T.t3(c.k0w ^ (ctr << 24), 3);
     const uint32_t u0 = c.L.x ^ T.t0(t0, 0);
-    const uint32_t u1 = c.L.y ^ rotl8(T.t2(t0, 3));
+    const uint32_t u1 = c.L.y ^ T.t3(t0, 3);
     const uint32_t u2 = c.L.z ^ T.t2(t0, 2);
-    const uint32_t u3 = c.L.w ^ rotl8(T.t0(t0, 1));
+    const uint32_t u3 = c.L.w ^ T.t1(t0, 1);
     return aes256_rounds<3>(u0, u1, u2, u3, T, rk);
 }
 
@@ -330,21 +380,68 @@ __device__ __forceinline__ uint4 gf_reduce(const uint32_t z[8]) {
     return make_uint4(x3(z[0], t0, of), t1, t2, t3);
 }
 
+// (byte K of w) & 0xF0 in one VALU op (SDWA byte select); hipcc emits a shift + and for most K.
+template <int K>
+__device__ __forceinline__ uint32_t byte_hi_nibble(uint32_t w) {
+    uint32_t r;
+    if constexpr (K == 0) {
+        r = w & 0xF0u;
+    } else {
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_%c3 src1_sel:DWORD"
+            : "=v"(r) : "v"(w), "s"(0xF0u), "i"(K));
+    }
+    return r;
+}
+
 // x · F where ftab (LDS) is a full table F_p[v] at byte p*256 + v*16; acc is XORed in.
+// Table addresses: the high nibble of byte k as is, the low nibble after one shift of the word:
+// 9 VALU per word for its 8 lookups.
 __device__ __forceinline__ uint4 gf_mul_full(uint4 x, uint4 acc, const uint4* ftab) {
     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const uint32_t hi = xw[q] & 0xF0F0F0F0u;          // bytes k: nibble r = 6-2k, << 4
-        const uint32_t lo = (xw[q] << 4) & 0xF0F0F0F0u;   // bytes k: nibble r = 7-2k, << 4
+        const uint32_t hi = xw[q];        // byte k: nibble r = 6-2k in bits 4-7
+        const uint32_t lo = xw[q] << 4;   // byte k: nibble r = 7-2k in bits 4-7
+        const uint32_t ah[4] = {byte_hi_nibble<0>(hi), byte_hi_nibble<1>(hi), byte_hi_nibble<2>(hi),
+                                byte_hi_nibble<3>(hi)};
+        const uint32_t al[4] = {byte_hi_nibble<0>(lo), byte_hi_nibble<1>(lo), byte_hi_nibble<2>(lo),
+                                byte_hi_nibble<3>(lo)};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint4 e1 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 6 - 2 * k) * 256u + byte_of(hi, k));
-            const uint4 e2 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 7 - 2 * k) * 256u + byte_of(lo, k));
+            const uint4 e1 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 6 - 2 * k) * 256u + ah[k]);
+            const uint4 e2 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 7 - 2 * k) * 256u + al[k]);
             acc = x34(acc, e1, e2);
         }
     }
     return acc;
+}
+
+// x · P where ptab (LDS) holds the 8 position tables T_r[v] = v·x^(4r)·P (reduced) at byte
+// r*256 + v*16: nibble r of word q contributes T_r[v]·x^(32q), a shift by whole words, so the 32
+// lookups XOR straight into a 224-bit product that is reduced once. No shifts (the Shoup form
+// shifts every lookup by 4r bits): ~125 VALU per multiply instead of ~240, at 2 KiB per power.
+// For P = H^4 the tables are the first 8 positions of the single-key full table.
+__device__ __forceinline__ uint4 gf_mul_pos(uint4 x, const uint4* ptab) {
+    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+    uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t hi = xw[q], lo = xw[q] << 4;
+        const uint32_t ah[4] = {byte_hi_nibble<0>(hi), byte_hi_nibble<1>(hi), byte_hi_nibble<2>(hi),
+                                byte_hi_nibble<3>(hi)};
+        const uint32_t al[4] = {byte_hi_nibble<0>(lo), byte_hi_nibble<1>(lo), byte_hi_nibble<2>(lo),
+                                byte_hi_nibble<3>(lo)};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 e1 = lds_at<uint4>(ptab, (uint32_t)(6 - 2 * k) * 256u + ah[k]);
+            const uint4 e2 = lds_at<uint4>(ptab, (uint32_t)(7 - 2 * k) * 256u + al[k]);
+            z[q] = x3(z[q], e1.x, e2.x);
+            z[q + 1] = x3(z[q + 1], e1.y, e2.y);
+            z[q + 2] = x3(z[q + 2], e1.z, e2.z);
+            z[q + 3] = x3(z[q + 3], e1.w, e2.w);
+        }
+    }
+    return gf_reduce(z);
 }
 
 // x · H^k where `tab` is the LDS byte offset (multiple of 256, < 2^24, relative to `base`) of a
@@ -491,9 +588,9 @@ __device__ __forceinline__ uint4 gcm_lane_io(const neb_desc& d, const LaneBlock&
 
 // Keystream block of lane block b. CM: counter-mode caching level — 0 none, 1 every counter of
 // the wave below 2^16, 2 below 2^8.
-template <int CM, class RK>
+template <int CM, class TL, class RK>
 __device__ __forceinline__ uint4 gcm_lane_ks(const LaneBlock& b, uint32_t c1, uint32_t c2, const CtrConst& cc,
-                                             const TLook& T, const RK& rk) {
+                                             const TL& T, const RK& rk) {
 #ifdef NEB_ABLATE_AES
     return make_uint4(c1 ^ b.ctr, c2, b.ctr * 0x9E3779B9u, cc.k0w);
 #else
@@ -582,9 +679,19 @@ struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 
     }
 };
 constexpr uint32_t kChunkTables = 5;  // Shoup tables H, H^2, H^4, H^8, H^16 (table i = H^(2^i))
-struct GhShoup {  // one key per chunk: its Shoup tables staged in the wave's LDS slice
+#ifndef NEB_CHUNK_POS
+#define NEB_CHUNK_POS 1  // 4-lane chunks multiply by H^4 with position tables (gf_mul_pos)
+#endif
+struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position tables) in the wave's LDS slice
     const uint4* base;
-    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t lg) const { return gf_mul_shoup(a, lg * 256u, base); }
+    const uint4* pos;
+    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t lg) const {
+#if NEB_CHUNK_POS
+        return gf_mul_pos(a, pos);  // the position tables of H^(2^lg)
+#else
+        return gf_mul_shoup(a, lg * 256u, base);
+#endif
+    }
     // Pairwise tree over the packet's lanes: level i folds V_l·H^(2^i) ⊕ V_(l+2^i) into the lanes
     // l ≡ 0 mod 2^(i+1); after lg levels lane 0 holds Z with Σ_l A_l·H^(LPP-l) = Z·H.
     // lg + 1 multiplies instead of a Horner's LPP.
@@ -599,10 +706,10 @@ struct GhShoup {  // one key per chunk: its Shoup tables staged in the wave's LD
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
-template <bool OPEN, class GH>
+template <bool OPEN, class GH, class TL>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
-                                                 bool key_ok, const RkRegs& rk, const GH& gh, const uint2* ttab,
-                                                 uint2 lb8, uint32_t lane, uint32_t lg) {
+                                                 bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
+                                                 uint32_t lane, uint32_t lg) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
@@ -623,7 +730,6 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
     const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
     const uint32_t c2 = bswap32((uint32_t)d.counter);
-    const TLook T{ttab, lb8};
     uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
     auto rounds = [&](auto cm) {
         constexpr int CM = decltype(cm)::value;
@@ -678,8 +784,15 @@ __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rk
 
 // ---- one tunnel key for the whole batch -------------------------------------------------------
 
+#ifndef NEB_T4
+#define NEB_T4 1  // single-key kernel on the four-table AES (TLook4); 0 = the two-table TLook
+#endif
 #ifndef NEB_SINGLE_WAVES
-#define NEB_SINGLE_WAVES 8  // waves per workgroup (2 workgroups per CU)
+#if NEB_T4
+#define NEB_SINGLE_WAVES 16  // waves per workgroup (one workgroup per CU: 136 KiB of LDS)
+#else
+#define NEB_SINGLE_WAVES 8   // waves per workgroup (2 workgroups per CU)
+#endif
 #endif
 #ifndef NEB_SINGLE_WPE
 #define NEB_SINGLE_WPE 4    // launch bound: waves per SIMD
@@ -690,7 +803,11 @@ constexpr int kSingleThreads = kSingleWaves * kWave;
 struct SingleLds {
     uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
     uint4 shoup_h[16];       // 256 B  M[v] = v·H
+#if NEB_T4
+    uint2 ttab[2 * 256 * 32];  // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each
+#else
     uint2 ttab[256 * 32];    // 64 KiB T-table pairs, 32 copies
+#endif
 };
 
 template <bool OPEN>
@@ -699,10 +816,14 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    const uint2 lb8 = ttab_lane_base(lane);
-
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
+#if NEB_T4
+    const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
+    for (uint32_t i = tid; i < 2u * 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab4_entry(i);
+#else
+    const TLook T{lds.ttab, ttab_lane_base(lane)};
     for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
+#endif
     for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull + 4u * i);
     if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
     uint32_t rks[60];
@@ -716,18 +837,34 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
     for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
         const uint32_t p = grp * kPpw + lane / kLpp;
-        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, true, rk, gh, lds.ttab, lb8, lane, kLg);
+        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, true, rk, gh, T, lane, kLg);
     }
 }
 
 // ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------
 
+// The mixed-key kernel keeps the two-table AES: with four tables (one 16-wave workgroup per CU)
+// C3 sealed 1-2% faster but IMIX 4% slower (A/B, tools/ablate.sh NEB_CHUNK_T4=1).
+#ifndef NEB_CHUNK_T4
+#define NEB_CHUNK_T4 0
+#endif
+#if NEB_CHUNK_T4 || NEB_CHUNK_POS
+constexpr int kChunkWaves = 16;  // one workgroup per CU (116 KiB of LDS; 148 KiB with T4)
+#else
 constexpr int kChunkWaves = 8;
+#endif
 constexpr int kChunkThreads = kChunkWaves * kWave;
 
 struct ChunkLds {
-    uint4 shoup[kChunkWaves][kChunkTables][16];  // per wave: M[v] for H, H^2, H^4, H^8, H^16 (10 KiB)
+    uint4 shoup[kChunkWaves][kChunkTables][16];  // per wave: M[v] for H, H^2, H^4, H^8, H^16 (1.25 KiB)
+#if NEB_CHUNK_POS
+    uint4 pos[kChunkWaves][8 * 16];              // per wave: position tables of H^4 (2 KiB)
+#endif
+#if NEB_CHUNK_T4
+    uint2 ttab[2 * 256 * 32];                    // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each
+#else
     uint2 ttab[256 * 32];                        // 64 KiB T-table pairs, 32 copies
+#endif
 };
 
 struct ChunkArgs {
@@ -745,15 +882,28 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    const uint2 lb8 = ttab_lane_base(lane);
+#if NEB_CHUNK_T4
+    const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
+#else
+    const TLook T{lds.ttab, ttab_lane_base(lane)};
+#endif
     const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
     const uint32_t nback = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
     const uint32_t nch = nfront + nback;
     if (blockIdx.x * (uint32_t)kChunkWaves >= nch) return;  // uniform over the workgroup
+#if NEB_CHUNK_T4
+    for (uint32_t i = tid; i < 2u * 256u * 32u; i += kChunkThreads) lds.ttab[i] = ttab4_entry(i);
+#else
     for (uint32_t i = tid; i < 256u * 32u; i += kChunkThreads) lds.ttab[i] = ttab_entry(i);
+#endif
     __syncthreads();
     uint4* wtab = &lds.shoup[wave][0][0];
-    const GhShoup gh{wtab};
+#if NEB_CHUNK_POS
+    uint4* wpos = &lds.pos[wave][0];
+    const GhShoup gh{wtab, wpos};
+#else
+    const GhShoup gh{wtab, nullptr};
+#endif
 
     // First chunk: the wave's own index; later ones from the work cursor once a chunk is done, so
     // waves that drew short chunks draw again (longest first: front, then back). Every wave
@@ -773,13 +923,20 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
         // stage the chunk key's Shoup tables H^(2^i), i = 0..4 (record tables 0, 1, 3, 7, 15)
         wtab[lane] = ld_rec4(rec, kRecShoup + 64u * ((1u << (lane >> 4)) - 1u) + 4u * (lane & 15u));
         if (lane < 16u) wtab[64u + lane] = ld_rec4(rec, kRecShoup + 64u * 15u + 4u * lane);
+#if NEB_CHUNK_POS
+        {  // the position tables of H^(2^lg)
+            const uint32_t pt = rec_pos_table(lg);
+            wpos[lane] = ld_rec4(rec, pt + 4u * lane);
+            wpos[64u + lane] = ld_rec4(rec, pt + 4u * (64u + lane));
+        }
+#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t q = lane >> lg;
         const bool valid = q < count;
         const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, lds.ttab, lb8, lane, lg);
+        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -802,6 +959,8 @@ __device__ uint8_t xtime_d(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) 
 __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __restrict__ key, uint32_t* __restrict__ rec) {
     __shared__ uint4 hp[16];      // H^1..H^16
     __shared__ uint4 basis[128];  // x^i · H^kFullPow
+    __shared__ uint4 basis8[32];  // x^i · H^8
+    __shared__ uint4 basis16[32]; // x^i · H^16
     if (threadIdx.x == 0) {
         uint8_t rk[240];
         for (int i = 0; i < 32; i++) rk[i] = key[i];
@@ -863,6 +1022,13 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
             basis[i] = b;
             b = gf_mulx(b);
         }
+        uint4 b8 = hp[7], b16 = hp[15];
+        for (int i = 0; i < 32; i++) {
+            basis8[i] = b8;
+            basis16[i] = b16;
+            b8 = gf_mulx(b8);
+            b16 = gf_mulx(b16);
+        }
         rec[kRecAlg] = NEB_ALG_AESGCM;
     }
     __syncthreads();
@@ -881,6 +1047,16 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         for (uint32_t j = 0; j < 4; j++)
             if ((v >> (3 - j)) & 1u) e = xor4(e, basis[4 * p + j]);
         uint32_t* o = rec + kRecFull + 4u * i;
+        o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
+    }
+    // position tables of H^8 and H^16: T_r[v] = XOR of basis[4r + j] for the set bits of v
+    {
+        const uint32_t tab = t >> 7, i = t & 127u, r = i >> 4, v = i & 15u;
+        const uint4* bs = tab ? basis16 : basis8;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        for (uint32_t j = 0; j < 4; j++)
+            if ((v >> (3 - j)) & 1u) e = xor4(e, bs[4 * r + j]);
+        uint32_t* o = rec + (tab ? kRecPos16 : kRecPos8) + 4u * i;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
 }

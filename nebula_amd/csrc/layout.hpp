@@ -4,9 +4,9 @@
 
 namespace neb {
 
-// One key record per installed tunnel key (12.5 KiB): the first 512 B hold the key schedule and raw
+// One key record per installed tunnel key (16.5 KiB): the first 512 B hold the key schedule and raw
 // H powers; the rest holds GHASH lookup tables precomputed at install time (AES-GCM only).
-constexpr uint32_t kKeyRecDwords = 3200;
+constexpr uint32_t kKeyRecDwords = 4224;
 constexpr uint32_t kKeyRecBytes = kKeyRecDwords * 4;
 
 // AES-256-GCM record
@@ -21,7 +21,16 @@ constexpr uint32_t kRecShoup = 128;
 // kFullPow = lanes per packet of the single-key kernel (its Horner stride).
 constexpr uint32_t kFullPow = 4;
 constexpr uint32_t kRecFull = kRecShoup + 16 * 16 * 4;
-static_assert(kRecFull + 32 * 16 * 4 == kKeyRecDwords, "record layout");
+// position tables T_r[v] = (v·x^4r)·P (reduced), r = 0..7, of P = H^8 and H^16: the Horner
+// multiplies of the mixed-key kernel's 8- and 16-lane chunks (its 4-lane chunks use positions 0-7
+// of the full H^4 table). 8 × 16 entries × 4 BE words each.
+constexpr uint32_t kRecPos8 = kRecFull + 32 * 16 * 4;
+constexpr uint32_t kRecPos16 = kRecPos8 + 8 * 16 * 4;
+static_assert(kRecPos16 + 8 * 16 * 4 == kKeyRecDwords, "record layout");
+// position tables of H^(2^lg), lg = 2, 3, 4
+__host__ __device__ constexpr uint32_t rec_pos_table(uint32_t lg) {
+    return lg == 2u ? kRecFull : (lg == 3u ? kRecPos8 : kRecPos16);
+}
 
 // ChaCha20-Poly1305 record
 constexpr uint32_t kRecChaKey = 0;      // dwords [0,8): the 256-bit key as 8 little-endian words
