@@ -112,8 +112,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
-    ap.add_argument("--mode", choices=["device", "host", "tx", "rx"], default="device",
-                    help="device: the headline; host: host-resident batch; tx: the device TX batch "
+    ap.add_argument("--mode", choices=["device", "host", "host-staged", "tx", "rx"], default="device",
+                    help="device: the headline; host: host-resident batch (pinned arena: zero-copy); "
+                         "host-staged: the same through hipMemcpyAsync staging; tx: the device TX batch "
                          "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -155,7 +156,9 @@ def main():
     payload = float(b.payload_bytes)
     alg_bytes = float(b.algorithmic_bytes)
 
-    if args.mode == "host":
+    if args.mode == "host-staged":
+        os.environ["NEB_HOST_STAGED"] = "1"  # read by the engine at its first host batch
+    if args.mode in ("host", "host-staged"):
         from nebula_amd.batch import PinnedBuffer
 
         d = slot_desc(b, ciphers)
@@ -175,7 +178,11 @@ def main():
         dt = ctrl.max(te - ts)
         if rank == 0:
             print(json.dumps({
-                "metric": "GiB/s host-resident (pinned H2D + kernel + D2H) AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch",
+                "metric": ("GiB/s host-resident (pinned arena, zero-copy: kernels load/store it over PCIe) "
+                           if args.mode == "host" else
+                           "GiB/s host-resident (pinned hipMemcpyAsync H2D + kernel + D2H, 2 streams) ")
+                + ("AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch" if cfg == 1 else
+                   f"{'AES-256-GCM' if b.alg == L.ALG_AESGCM else 'ChaCha20-Poly1305'} seal+open ({workload_name})"),
                 "value": round(2 * payload * args.steps * world / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
                 "higher_is_better": True, "scaling": "weak", "data": "synthetic",

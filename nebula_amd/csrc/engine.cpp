@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -94,6 +95,10 @@ struct neb_engine {
 
     std::mutex pipe_mu;
     PipeSlot pipe[kPipeStreams];
+    // zero-copy host batches: device copies of pageable descriptors / statuses
+    neb_desc* zc_desc = nullptr;
+    int32_t* zc_status = nullptr;
+    uint32_t zc_cap = 0;
 
     SchedSpace sched;
     TxSpace tx;
@@ -216,6 +221,8 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
     if (e->tx.done) { hipEventSynchronize(e->tx.done); hipEventDestroy(e->tx.done); }
     if (e->tx.mem) hipFree(e->tx.mem);
     if (e->tx.d_io) hipFree(e->tx.d_io);
+    if (e->zc_desc) hipFree(e->zc_desc);
+    if (e->zc_status) hipFree(e->zc_status);
     if (e->d_keys) hipFree(e->d_keys);
     if (e->h_stage) hipHostFree(e->h_stage);
     if (e->d_stage) hipFree(e->d_stage);
@@ -482,7 +489,55 @@ NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint3
     return batch_device(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, stream);
 }
 
-// Host-resident batch: chunks of kPipeChunkPkts packets, each chunk's arena span copied H2D,
+// True if p is pinned host memory the device addresses at the same pointer (hipHostMalloc).
+static bool host_mapped(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer == p;
+}
+
+// Zero-copy host batch: the arena is pinned and mapped, so the kernels load and store it across
+// PCIe themselves (loads = the H2D direction, stores = D2H, both at once) with no staging copies.
+// Pageable descriptors / statuses go through device buffers. Every descriptor is bounds-checked
+// on the host first: a kernel access outside the mapping would fault the GPU.
+static int batch_host_zero_copy(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n,
+                                uint8_t* arena, size_t arena_len, int32_t* status, uint32_t key_hint) {
+    for (uint32_t i = 0; i < n; i++) {
+        const neb_desc& d = desc[i];
+        const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
+        if (d.src_off + pay > arena_len || d.dst_off + outl > arena_len || d.aad_off + d.aad_len > arena_len ||
+            pay > arena_len || (uint64_t)d.aad_len > arena_len)
+            return NEB_ERR_INVALID;
+    }
+    const bool desc_mapped = host_mapped(desc), status_mapped = host_mapped(status);
+    if ((!desc_mapped || !status_mapped) && n > e->zc_cap) {
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (e->zc_desc) { hipFree(e->zc_desc); e->zc_desc = nullptr; }
+        if (e->zc_status) { hipFree(e->zc_status); e->zc_status = nullptr; }
+        e->zc_cap = 0;
+        HIP_TRY(hipMalloc((void**)&e->zc_desc, (size_t)n * sizeof(neb_desc)));
+        HIP_TRY(hipMalloc((void**)&e->zc_status, (size_t)n * sizeof(int32_t)));
+        e->zc_cap = n;
+    }
+    const neb_desc* d_desc = desc;
+    int32_t* d_status = status;
+    if (!desc_mapped) {
+        HIP_TRY(hipMemcpyAsync(e->zc_desc, desc, (size_t)n * sizeof(neb_desc), hipMemcpyHostToDevice, e->stream));
+        d_desc = e->zc_desc;
+    }
+    if (!status_mapped) d_status = e->zc_status;
+    HIP_TRY(launch_batch(e, alg, open, d_desc, n, arena, d_status, key_hint, e->stream));
+    if (!status_mapped)
+        HIP_TRY(hipMemcpyAsync(status, d_status, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return NEB_OK;
+}
+
+// Host-resident batch. A pinned, mapped arena runs zero-copy (above) unless NEB_HOST_STAGED is
+// set; otherwise chunks of kPipeChunkPkts packets are staged: each chunk's arena span copied H2D,
 // processed and copied D2H on one of two streams, so chunk i+1's copies overlap chunk i's kernel.
 static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n, uint8_t* arena,
                       size_t arena_len, int32_t* status, uint32_t key_hint) {
@@ -492,6 +547,9 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
     if (!desc || !arena || !status) return NEB_ERR_INVALID;
     std::lock_guard<std::mutex> g(e->pipe_mu);
     hipSetDevice(e->device);
+    static const bool staged_only = std::getenv("NEB_HOST_STAGED") != nullptr;
+    if (!staged_only && host_mapped(arena))
+        return batch_host_zero_copy(e, alg, open, desc, n, arena, arena_len, status, key_hint);
     for (auto& s : e->pipe) {
         if (!s.stream) {
             HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));

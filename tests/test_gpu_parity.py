@@ -274,25 +274,54 @@ def test_full_c2_roundtrip_property(engine):
     assert np.array_equal(s2[idx], r2[idx])
 
 
+@pytest.mark.parametrize("arena_kind", ["pinned", "pageable"])
 @pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
-def test_host_pipeline_matches_device(engine, oracle_mod, alg):
+def test_host_pipeline_matches_device(engine, oracle_mod, alg, arena_kind):
+    """neb_*_batch_host: a pinned arena runs zero-copy (the kernels on host memory), a pageable one
+    through the staged H2D -> kernel -> D2H pipeline; both equal the oracle byte for byte."""
     from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
 
     b = W.make_batch(alg, 20000, 64, sizes=(90, 576, 1300), ratio=(7, 4, 1), name="host")
     ciphers = install_keys(engine, b)
+    buf = None
     try:
         d = slot_desc(b, ciphers)
-        buf = PinnedBuffer(b.arena.nbytes)
-        buf.array[:] = b.arena
-        st = host_batch(engine, alg, False, d, buf.array)
+        if arena_kind == "pinned":
+            buf = PinnedBuffer(b.arena.nbytes)
+            arena = buf.array
+            arena[:] = b.arena
+        else:
+            arena = b.arena.copy()
+        st = host_batch(engine, alg, False, d, arena)
         assert (st == 0).all()
         ref, _ = oracle_seal(oracle_mod, b)
-        assert np.array_equal(buf.array, ref)
-        st = host_batch(engine, alg, True, d, buf.array)
+        assert np.array_equal(arena, ref)
+        st = host_batch(engine, alg, True, d, arena)
         assert (st == 0).all()
         ref_o, _ = oracle_open(oracle_mod, b, ref)
-        assert np.array_equal(buf.array, ref_o)
-        buf.free()
+        assert np.array_equal(arena, ref_o)
     finally:
+        if buf is not None:
+            buf.free()
+        for c in ciphers:
+            c.destroy()
+
+
+def test_host_zero_copy_rejects_out_of_bounds(engine):
+    """A descriptor past the pinned arena is refused before any kernel touches host memory."""
+    from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
+
+    b = W.make_batch(L.ALG_AESGCM, 64, 1, name="oob")
+    ciphers = install_keys(engine, b)
+    buf = PinnedBuffer(b.arena.nbytes)
+    try:
+        buf.array[:] = b.arena
+        d = slot_desc(b, ciphers)
+        d["len"][-1] = b.stride * 4  # runs past the end of the arena
+        with pytest.raises(Exception):
+            host_batch(engine, b.alg, False, d, buf.array)
+        assert np.array_equal(buf.array, b.arena)  # nothing was written
+    finally:
+        buf.free()
         for c in ciphers:
             c.destroy()
