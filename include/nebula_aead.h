@@ -161,9 +161,12 @@ NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint3
 
 /* ---- batched data plane: host-resident arena (the TUN / UDP side) ---------------------------- */
 
-/* Same as above but desc/arena/status live in host memory (ideally from neb_host_alloc). The arena
- * range [arena_lo, arena_hi) touched by the descriptors is streamed through the device in chunks
- * with pinned H2D -> kernel -> D2H copies overlapped on two streams. Synchronous. */
+/* Same as above but desc/arena/status live in host memory. Synchronous.
+ * - arena from neb_host_alloc (pinned and mapped): zero-copy — every descriptor is bounds-checked
+ *   against arena_len (NEB_ERR_INVALID, nothing touched, otherwise), then the kernels load and
+ *   store the arena across PCIe directly; desc/status may be pinned too or ordinary memory.
+ * - any other arena (or NEB_HOST_STAGED set in the environment): the range the descriptors touch
+ *   is streamed through the device in chunks, pinned H2D -> kernel -> D2H on two streams. */
 NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
                                 size_t arena_len, int32_t* status, uint32_t key_hint);
 NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
