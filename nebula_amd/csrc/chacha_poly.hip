@@ -36,6 +36,23 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+// (lane-permuted v) + o and (lane-permuted v) ^ o in one DPP VALU op, quad_perm control Q. The
+// s_nop 1 covers the 2 wait states a DPP read needs after a VALU write of its source (inline asm
+// is opaque to the hazard recognizer).
+template <int Q>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t v, uint32_t o) {
+    uint32_t r;
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 quad_perm:[%c3,%c4,%c5,%c6] row_mask:0xf bank_mask:0xf"
+        : "=v"(r) : "v"(v), "v"(o), "i"(Q & 3), "i"((Q >> 2) & 3), "i"((Q >> 4) & 3), "i"((Q >> 6) & 3));
+    return r;
+}
+template <int Q>
+__device__ __forceinline__ uint32_t dpp_xor(uint32_t v, uint32_t o) {
+    uint32_t r;
+    asm("s_nop 1\n\tv_xor_b32_dpp %0, %1, %2 quad_perm:[%c3,%c4,%c5,%c6] row_mask:0xf bank_mask:0xf"
+        : "=v"(r) : "v"(v), "v"(o), "i"(Q & 3), "i"((Q >> 2) & 3), "i"((Q >> 4) & 3), "i"((Q >> 6) & 3));
+    return r;
+}
 
 #define NEB_QR(a, b, c, d)                \
     a += b; d ^= a; d = rotl(d, 16);      \
@@ -47,10 +64,34 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_a
 // Returns the keystream words 4w..4w+3 of the block (bytes 16w..16w+15) as little-endian words.
 __device__ __forceinline__ uint4 chacha_quad(uint32_t a0, uint32_t b0, uint32_t c0, uint32_t d0, uint32_t w) {
     uint32_t a = a0, b = b0, c = c0, d = d0;
+    // The diagonal round needs b, c, d from lanes w+1, w+2, w+3 and the next column round needs
+    // them back. No separate moves: each quarter-round reads the shifted operands through the DPP
+    // of its first adds/XORs (v_add_u32_dpp / v_xor_b32_dpp), so b, c, d simply stay in the frame
+    // of the round that wrote them — 24 VALU per double round instead of 30.
+#define NEB_QR_DPP(P1, P2, P3)                                                          \
+    a = dpp_add<P1>(b, a); d = rotl(dpp_xor<P3>(d, a), 16);                              \
+    c = dpp_add<P2>(c, d); b = rotl(dpp_xor<P1>(b, c), 12);                              \
+    a += b; d ^= a; d = rotl(d, 8);                                                     \
+    c += d; b ^= c; b = rotl(b, 7);
+#ifndef NEB_CHACHA_DPP
+#define NEB_CHACHA_DPP 1
+#endif
+#if NEB_CHACHA_DPP
+    constexpr int kL1 = 0x39, kL2 = 0x4E, kL3 = 0x93;  // quad_perm [1,2,3,0], [2,3,0,1], [3,0,1,2]
+    NEB_QR(a, b, c, d)
+    NEB_QR_DPP(kL1, kL2, kL3)  // diagonal round: lane w takes b from w+1, c from w+2, d from w+3
+#pragma unroll 3
+    for (int i = 1; i < 10; i++) {
+        NEB_QR_DPP(kL3, kL2, kL1)  // column round, back from the diagonal frame
+        NEB_QR_DPP(kL1, kL2, kL3)
+    }
+    b = qperm<3, 0, 1, 2>(b);
+    c = qperm<2, 3, 0, 1>(c);
+    d = qperm<1, 2, 3, 0>(d);
+#else  // separate quad_perm moves before and after each diagonal round
 #pragma unroll 2
     for (int i = 0; i < 10; i++) {
         NEB_QR(a, b, c, d)
-        // diagonal round: lane w takes b from w+1, c from w+2, d from w+3
         b = qperm<1, 2, 3, 0>(b);
         c = qperm<2, 3, 0, 1>(c);
         d = qperm<3, 0, 1, 2>(d);
@@ -59,6 +100,8 @@ __device__ __forceinline__ uint4 chacha_quad(uint32_t a0, uint32_t b0, uint32_t 
         c = qperm<2, 3, 0, 1>(c);
         d = qperm<1, 2, 3, 0>(d);
     }
+#endif
+#undef NEB_QR_DPP
     a += a0; b += b0; c += c0; d += d0;
     // 4x4 transpose inside the quad: lane w holds row elements (word 4e + w, e = 0..3) and needs
     // words 4w..4w+3, i.e. element w of every lane.
