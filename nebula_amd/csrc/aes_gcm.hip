@@ -660,9 +660,12 @@ __device__ __forceinline__ uint4 shfl_down4(uint4 v, uint32_t d) {
 
 // GHASH tables a packet group multiplies with: horner(A) = A·H^LPP, and final(A) = the packet's
 // Σ_l A_l·H^(LPP-l), valid at least on the packet's last lane (the one holding E_K(J0)).
-struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 + Shoup table for H
+#ifndef NEB_SINGLE_POSH
+#define NEB_SINGLE_POSH 1  // final quad Horner on H's position tables (0: H's Shoup table)
+#endif
+struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 + tables for H
     const uint4* full;
-    const uint4* shoup_h;
+    const uint4* shoup_h;  // NEB_SINGLE_POSH: the 8 position tables of H, else its Shoup table
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const {
         return gf_mul_full(a, make_uint4(0, 0, 0, 0), full);
     }
@@ -670,10 +673,17 @@ struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t, uint32_t) const {
         uint4 V = quad_bcast4<0>(A);
 #ifndef NEB_ABLATE_FINAL
+#if NEB_SINGLE_POSH
+        V = xor4(gf_mul_pos(V, shoup_h), quad_bcast4<1>(A));
+        V = xor4(gf_mul_pos(V, shoup_h), quad_bcast4<2>(A));
+        V = xor4(gf_mul_pos(V, shoup_h), quad_bcast4<3>(A));
+        V = gf_mul_pos(V, shoup_h);
+#else
         V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<1>(A));
         V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<2>(A));
         V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<3>(A));
         V = gf_mul_shoup(V, 0u, shoup_h);
+#endif
 #endif
         return V;
     }
@@ -802,7 +812,11 @@ constexpr int kSingleThreads = kSingleWaves * kWave;
 
 struct SingleLds {
     uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
+#if NEB_SINGLE_POSH
+    uint4 shoup_h[8 * 16];   // 2 KiB  position tables of H
+#else
     uint4 shoup_h[16];       // 256 B  M[v] = v·H
+#endif
 #if NEB_T4
     uint2 ttab[2 * 256 * 32];  // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each
 #else
@@ -825,7 +839,11 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
 #endif
     for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull + 4u * i);
+#if NEB_SINGLE_POSH
+    if (tid < 128u) lds.shoup_h[tid] = ld_rec4(srec, kRecPos1 + 4u * tid);
+#else
     if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
+#endif
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
@@ -961,6 +979,7 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
     __shared__ uint4 basis[128];  // x^i · H^kFullPow
     __shared__ uint4 basis8[32];  // x^i · H^8
     __shared__ uint4 basis16[32]; // x^i · H^16
+    __shared__ uint4 basis1[32];  // x^i · H
     if (threadIdx.x == 0) {
         uint8_t rk[240];
         for (int i = 0; i < 32; i++) rk[i] = key[i];
@@ -1022,12 +1041,14 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
             basis[i] = b;
             b = gf_mulx(b);
         }
-        uint4 b8 = hp[7], b16 = hp[15];
+        uint4 b8 = hp[7], b16 = hp[15], b1 = hp[0];
         for (int i = 0; i < 32; i++) {
             basis8[i] = b8;
             basis16[i] = b16;
+            basis1[i] = b1;
             b8 = gf_mulx(b8);
             b16 = gf_mulx(b16);
+            b1 = gf_mulx(b1);
         }
         rec[kRecAlg] = NEB_ALG_AESGCM;
     }
@@ -1057,6 +1078,14 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         for (uint32_t j = 0; j < 4; j++)
             if ((v >> (3 - j)) & 1u) e = xor4(e, bs[4 * r + j]);
         uint32_t* o = rec + (tab ? kRecPos16 : kRecPos8) + 4u * i;
+        o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
+    }
+    if (t < 128u) {  // and of H
+        const uint32_t r = t >> 4, v = t & 15u;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        for (uint32_t j = 0; j < 4; j++)
+            if ((v >> (3 - j)) & 1u) e = xor4(e, basis1[4 * r + j]);
+        uint32_t* o = rec + kRecPos1 + 4u * t;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
 }

@@ -4,9 +4,9 @@
 
 namespace neb {
 
-// One key record per installed tunnel key (16.5 KiB): the first 512 B hold the key schedule and raw
+// One key record per installed tunnel key (18.5 KiB): the first 512 B hold the key schedule and raw
 // H powers; the rest holds GHASH lookup tables precomputed at install time (AES-GCM only).
-constexpr uint32_t kKeyRecDwords = 4224;
+constexpr uint32_t kKeyRecDwords = 4736;
 constexpr uint32_t kKeyRecBytes = kKeyRecDwords * 4;
 
 // AES-256-GCM record
@@ -26,7 +26,9 @@ constexpr uint32_t kRecFull = kRecShoup + 16 * 16 * 4;
 // of the full H^4 table). 8 × 16 entries × 4 BE words each.
 constexpr uint32_t kRecPos8 = kRecFull + 32 * 16 * 4;
 constexpr uint32_t kRecPos16 = kRecPos8 + 8 * 16 * 4;
-static_assert(kRecPos16 + 8 * 16 * 4 == kKeyRecDwords, "record layout");
+// position tables of H itself: the single-key kernel's final quad Horner (4 multiplies by H)
+constexpr uint32_t kRecPos1 = kRecPos16 + 8 * 16 * 4;
+static_assert(kRecPos1 + 8 * 16 * 4 == kKeyRecDwords, "record layout");
 // position tables of H^(2^lg), lg = 2, 3, 4
 __host__ __device__ constexpr uint32_t rec_pos_table(uint32_t lg) {
     return lg == 2u ? kRecFull : (lg == 3u ? kRecPos8 : kRecPos16);
