@@ -327,7 +327,7 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     const size_t b_counters = align_up((neb::kSchedCounters + 2u * (size_t)nb) * 4u, 256);
     const size_t b_base = align_up((size_t)nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = (size_t)mc * 16u;
-    const size_t bytes = b_counters + b_base + 2 * b_idx + b_chunks;
+    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
     if (sp.mem) hipFree(sp.mem);
@@ -343,6 +343,8 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     sp.ws.base = (uint32_t*)m;
     m += b_base;
     sp.ws.binof = (uint32_t*)m;
+    m += b_idx;
+    sp.ws.binpos = (uint32_t*)m;
     m += b_idx;
     sp.ws.sorted = (uint32_t*)m;
     m += b_idx;

@@ -15,7 +15,9 @@ __device__ __forceinline__ uint32_t size_class(const neb_desc& d, uint32_t lpp) 
     return c < kSizeClasses ? c : kSizeClasses - 1u;
 }
 
-// pass 1: histogram of (size class, key) bins; keys outside the table go to key index max_keys
+// pass 1: histogram of (size class, key) bins; keys outside the table go to key index max_keys.
+// The returning add also ranks the packet inside its bin, so pass 3 needs no atomics: the adds
+// execute at the memory side (MI355X_MICROARCH.md, global atomics), ≈55 µs per 1 Mi packets each.
 __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn,
                                   uint32_t max_keys, uint32_t lpp, SchedWs ws) {
     if (dn) n = min(n, *dn);
@@ -24,7 +26,7 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
         const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
         const uint32_t b = size_class(d, lpp) * (max_keys + 1u) + key;
         ws.binof[i] = b;
-        atomicAdd(&ws.hist[b], 1u);
+        ws.binpos[i] = atomicAdd(&ws.hist[b], 1u);
     }
 }
 
@@ -76,14 +78,11 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     }
 }
 
-// pass 3: scatter packet indices into their bin's range
+// pass 3: scatter packet indices into their bin's range, at the rank pass 1 drew
 __global__ void sched_scatter_kernel(uint32_t n, const uint32_t* dn, SchedWs ws) {
     if (dn) n = min(n, *dn);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t b = ws.binof[i];
-        const uint32_t pos = atomicAdd(&ws.fill[b], 1u);
-        ws.sorted[ws.base[b] + pos] = i;
-    }
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        ws.sorted[ws.base[ws.binof[i]] + ws.binpos[i]] = i;
 }
 
 }  // namespace neb

@@ -46,6 +46,7 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
     uint32_t* fill;
     uint32_t* base;       // [nbins] output offset of each non-empty bin
     uint32_t* binof;      // [n] bin of each packet
+    uint32_t* binpos;     // [n] rank of each packet within its bin (the histogram atomic's return)
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
     uint4* chunks;        // [max_chunks] {start in sorted, count, key_id, size class | lg << 8}
     uint32_t max_chunks;
