@@ -106,6 +106,18 @@ def pmc_traffic(kernel: str):
         return None
 
 
+def pmc_busy(kernel: str):
+    """LDS-array and VALU busy fractions of `kernel` from the committed counter pass
+    (profiles/pmc_busy.json, tools/pmc_busy.py): the resources that actually bound the AEAD
+    kernels, reported beside the HBM roofline. None when none is committed."""
+    p = os.path.join(ROOT, "profiles", "pmc_busy.json")
+    try:
+        k = json.load(open(p))["kernels"][kernel]
+        return {"lds_busy": k["lds_busy"], "valu_busy": k["valu_busy"], "source": k["source"]}
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +277,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kern_tag),
+            "binding": pmc_busy(kern_tag),
             "kernel": kern_tag, "kernel_ms": round(seal_ms, 4), "open_kernel_ms": round(open_ms, 4),
             "algorithmic_bytes_per_launch": int(alg_bytes),
         },
