@@ -979,7 +979,8 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
     __shared__ uint4 basis[128];  // x^i · H^kFullPow
     __shared__ uint4 basis8[32];  // x^i · H^8
     __shared__ uint4 basis16[32]; // x^i · H^16
-    __shared__ uint4 basis1[32];  // x^i · H
+    __shared__ uint4 basis_h[128];  // x^i · H
+    __shared__ uint4 part[2];
     if (threadIdx.x == 0) {
         uint8_t rk[240];
         for (int i = 0; i < 32; i++) rk[i] = key[i];
@@ -1021,34 +1022,48 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         uint32_t h[4];
         for (int i = 0; i < 4; i++)
             h[i] = (uint32_t)s[4 * i] << 24 | (uint32_t)s[4 * i + 1] << 16 | (uint32_t)s[4 * i + 2] << 8 | s[4 * i + 3];
-        // powers by bit-serial multiply (SP 800-38D Algorithm 1)
-        uint32_t pw[4] = {h[0], h[1], h[2], h[3]};
+        // basis_h[i] = x^i·H: a product P·H is the XOR of basis_h[i] over the set bits i of P
+        uint4 bh = make_uint4(h[0], h[1], h[2], h[3]);
+        for (int i = 0; i < 128; i++) {
+            basis_h[i] = bh;
+            bh = gf_mulx(bh);
+        }
+        hp[0] = basis_h[0];
+    }
+    __syncthreads();
+    // H^2..H^16: H^k = H^(k-1)·H with lane i < 128 contributing basis_h[i] if bit i of H^(k-1) is
+    // set, XOR-reduced across the two waves (the bit-serial form on one lane took ~100 µs).
+    for (uint32_t k = 1; k < kNumHPow; k++) {
+        const uint32_t t = threadIdx.x;
+        const uint4 P = hp[k - 1];
+        uint4 c = make_uint4(0, 0, 0, 0);
+        if (t < 128u) {
+            const uint32_t w = t < 32u ? P.x : (t < 64u ? P.y : (t < 96u ? P.z : P.w));
+            if ((w >> (31u - (t & 31u))) & 1u) c = basis_h[t];
+        }
+        for (int m = 32; m >= 1; m >>= 1) c = xor4(c, shfl_xor4(c, m));
+        if (t == 0u || t == 64u) part[t >> 6] = c;
+        __syncthreads();
+        if (t == 0u) hp[k] = xor4(part[0], part[1]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
         for (int k = 0; k < (int)kNumHPow; k++) {
-            hp[k] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-            for (int i = 0; i < 4; i++) rec[kRecHPow + 4 * k + i] = pw[i];
-            uint32_t z[4] = {0, 0, 0, 0}, v[4] = {h[0], h[1], h[2], h[3]};
-            for (int b = 0; b < 128; b++) {
-                if ((pw[b >> 5] >> (31 - (b & 31))) & 1u)
-                    for (int i = 0; i < 4; i++) z[i] ^= v[i];
-                uint32_t lsb = v[3] & 1u;
-                v[3] = (v[3] >> 1) | (v[2] << 31); v[2] = (v[2] >> 1) | (v[1] << 31);
-                v[1] = (v[1] >> 1) | (v[0] << 31); v[0] = (v[0] >> 1) ^ (lsb ? 0xE1000000u : 0u);
-            }
-            for (int i = 0; i < 4; i++) pw[i] = z[i];
+            const uint4 v = hp[k];
+            rec[kRecHPow + 4 * k] = v.x; rec[kRecHPow + 4 * k + 1] = v.y;
+            rec[kRecHPow + 4 * k + 2] = v.z; rec[kRecHPow + 4 * k + 3] = v.w;
         }
         uint4 b = hp[kFullPow - 1];
         for (int i = 0; i < 128; i++) {
             basis[i] = b;
             b = gf_mulx(b);
         }
-        uint4 b8 = hp[7], b16 = hp[15], b1 = hp[0];
+        uint4 b8 = hp[7], b16 = hp[15];
         for (int i = 0; i < 32; i++) {
             basis8[i] = b8;
             basis16[i] = b16;
-            basis1[i] = b1;
             b8 = gf_mulx(b8);
             b16 = gf_mulx(b16);
-            b1 = gf_mulx(b1);
         }
         rec[kRecAlg] = NEB_ALG_AESGCM;
     }
@@ -1084,7 +1099,7 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         const uint32_t r = t >> 4, v = t & 15u;
         uint4 e = make_uint4(0, 0, 0, 0);
         for (uint32_t j = 0; j < 4; j++)
-            if ((v >> (3 - j)) & 1u) e = xor4(e, basis1[4 * r + j]);
+            if ((v >> (3 - j)) & 1u) e = xor4(e, basis_h[4 * r + j]);
         uint32_t* o = rec + kRecPos1 + 4u * t;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
