@@ -124,8 +124,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
-    ap.add_argument("--mode", choices=["device", "host", "host-staged", "tx", "rx"], default="device",
+    ap.add_argument("--mode", choices=["device", "host", "host-kcopy", "host-staged", "tx", "rx"], default="device",
                     help="device: the headline; host: host-resident batch (pinned arena: zero-copy); "
+                         "host-kcopy: the pinned arena staged by span-copy kernels; "
                          "host-staged: the same through hipMemcpyAsync staging; tx: the device TX batch "
                          "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -169,8 +170,10 @@ def main():
     alg_bytes = float(b.algorithmic_bytes)
 
     if args.mode == "host-staged":
-        os.environ["NEB_HOST_STAGED"] = "1"  # read by the engine at its first host batch
-    if args.mode in ("host", "host-staged"):
+        os.environ["NEB_HOST_MODE"] = "dma"  # read by the engine at its first host batch
+    if args.mode == "host-kcopy":
+        os.environ["NEB_HOST_MODE"] = "kcopy"
+    if args.mode in ("host", "host-kcopy", "host-staged"):
         from nebula_amd.batch import PinnedBuffer
 
         d = slot_desc(b, ciphers)
@@ -190,9 +193,10 @@ def main():
         dt = ctrl.max(te - ts)
         if rank == 0:
             print(json.dumps({
-                "metric": ("GiB/s host-resident (pinned arena, zero-copy: kernels load/store it over PCIe) "
-                           if args.mode == "host" else
-                           "GiB/s host-resident (pinned hipMemcpyAsync H2D + kernel + D2H, 2 streams) ")
+                "metric": {"host": "GiB/s host-resident (pinned arena, zero-copy: kernels load/store it over PCIe) ",
+                           "host-kcopy": "GiB/s host-resident (pinned arena, span-copy kernels in/out around seal/open) ",
+                           "host-staged": "GiB/s host-resident (pinned hipMemcpyAsync H2D + kernel + D2H, 3 streams) ",
+                           }[args.mode]
                 + ("AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch" if cfg == 1 else
                    f"{'AES-256-GCM' if b.alg == L.ALG_AESGCM else 'ChaCha20-Poly1305'} seal+open ({workload_name})"),
                 "value": round(2 * payload * args.steps * world / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world,

@@ -307,6 +307,39 @@ def test_host_pipeline_matches_device(engine, oracle_mod, alg, arena_kind):
             c.destroy()
 
 
+@pytest.mark.parametrize("mode", ["kcopy", "zc", "dma"])
+def test_host_modes_shuffled_descriptors(engine, oracle_mod, mode, monkeypatch):
+    """Every host path (span-copy kernels, zero-copy, hipMemcpyAsync staging) on a pinned arena with
+    the descriptors in random order: pipeline chunks then cover overlapping arena spans, which the
+    engine must retire in order (each chunk copies its whole span back). Also an arena that starts
+    one byte past a 16-byte boundary (the kernels touch only aligned host arenas: DMA staging)."""
+    from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
+
+    monkeypatch.setenv("NEB_HOST_MODE", mode)
+    b = W.make_batch(L.ALG_AESGCM, 20000, 64, sizes=(90, 576, 1300), ratio=(7, 4, 1), name="shuffled")
+    ciphers = install_keys(engine, b)
+    buf = PinnedBuffer(b.arena.nbytes + 16)
+    try:
+        d = slot_desc(b, ciphers)
+        perm = np.random.default_rng(7).permutation(b.n)
+        dp = d[perm]
+        ref, _ = oracle_seal(oracle_mod, b)
+        ref_o, _ = oracle_open(oracle_mod, b, ref)
+        for shift in (0, 1):
+            arena = buf.array[shift:shift + b.arena.nbytes]
+            arena[:] = b.arena
+            st = host_batch(engine, b.alg, False, dp, arena)
+            assert (st == 0).all()
+            assert np.array_equal(arena, ref), (mode, shift)
+            st = host_batch(engine, b.alg, True, dp, arena)
+            assert (st == 0).all()
+            assert np.array_equal(arena, ref_o), (mode, shift)
+    finally:
+        buf.free()
+        for c in ciphers:
+            c.destroy()
+
+
 def test_host_zero_copy_rejects_out_of_bounds(engine):
     """A descriptor past the pinned arena is refused before any kernel touches host memory."""
     from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
