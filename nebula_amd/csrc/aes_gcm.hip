@@ -760,8 +760,10 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 const uint4 ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
 #ifndef NEB_NO_FASTIO
                 // the common round: every active lane holds a full, 16-B aligned payload block
+                // (the arena base counts too: a caller may pass an arena at any byte address)
                 const uint32_t off = 16u * (b.k - 1u);
-                const bool full = b.is_ct && off + 16u <= d.len && ((d.src_off | d.dst_off) & 15u) == 0u;
+                const bool full = b.is_ct && off + 16u <= d.len &&
+                                  ((d.src_off | d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u;
                 if (__all(full)) {
                     const uint4 in = *reinterpret_cast<const uint4*>(args.arena + d.src_off + off);
                     const uint4 out = xor4(in, ks);

@@ -347,8 +347,9 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
             wires[s] = neb_tx_wire{slot, counter, seg_len + 32u, p, j, 0u};
             ws.seal_desc[s] = neb_desc{slot + 16u, slot + 16u, slot, counter, seg_len, 16u, T.key_id, 0u};
             // header.Encode(Version 1, Message 1, subtype 0, remote index, counter)
-            *reinterpret_cast<uint4*>(dst) = make_uint4(0x00000011u, bswap32(T.remote_index),
-                                                        bswap32((uint32_t)(counter >> 32)), bswap32((uint32_t)counter));
+            // store_block: `out` may start at any byte address
+            store_block(dst, make_uint4(0x00000011u, bswap32(T.remote_index), bswap32((uint32_t)(counter >> 32)),
+                                        bswap32((uint32_t)counter)), 16u);
         }
 
         // ---- the segment's L3+L4 header: dwords g and g + 16 of it (superpackets) ----

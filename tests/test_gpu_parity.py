@@ -174,6 +174,40 @@ def test_unaligned_offsets(engine, oracle_mod, alg):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("shift", [1, 4, 8])
+@pytest.mark.parametrize("alg,nkeys", [(L.ALG_AESGCM, 1), (L.ALG_AESGCM, 16), (L.ALG_CHACHAPOLY, 16)])
+def test_unaligned_arena_base(engine, oracle_mod, alg, nkeys, shift):
+    """The device arena itself may start at any byte address (a torch view, a Go slice): aligned
+    descriptor offsets then no longer mean aligned addresses, and the kernels must not take their
+    16-byte vector fast paths on them."""
+    import torch
+
+    from nebula_amd.batch import DeviceBatch, install_keys
+
+    b = W.make_batch(alg, 512, nkeys, sizes=(90, 576, 1300), ratio=(1, 1, 2), name="shifted")
+    ciphers = install_keys(engine, b)
+    try:
+        db = DeviceBatch(engine, b, ciphers)
+        big = torch.zeros(b.arena.nbytes + 16, dtype=torch.uint8, device=db.dev)
+        db.arena = big[shift:shift + b.arena.nbytes]
+        db.arena.copy_(torch.from_numpy(b.arena))
+        assert db.arena.data_ptr() % 16 == shift % 16
+        db.seal()
+        torch.cuda.synchronize()
+        ref, _ = oracle_seal(oracle_mod, b)
+        assert (db.status_host() == 0).all()
+        assert np.array_equal(db.arena_host(), ref)
+        db.open()
+        torch.cuda.synchronize()
+        ref_o, _ = oracle_open(oracle_mod, b, ref)
+        assert (db.status_host() == 0).all()
+        assert np.array_equal(db.arena_host(), ref_o)
+        assert not big[:shift].any() and not big[shift + b.arena.nbytes:].any()  # nothing outside
+    finally:
+        for c in ciphers:
+            c.destroy()
+
+
 @pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
 def test_auth_failures_zero_payload_only(engine, oracle_mod, alg):
     b = W.make_batch(alg, 64, 4, name="tamper")
