@@ -162,11 +162,14 @@ NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint3
 /* ---- batched data plane: host-resident arena (the TUN / UDP side) ---------------------------- */
 
 /* Same as above but desc/arena/status live in host memory. Synchronous.
- * - arena from neb_host_alloc (pinned and mapped): zero-copy — every descriptor is bounds-checked
- *   against arena_len (NEB_ERR_INVALID, nothing touched, otherwise), then the kernels load and
- *   store the arena across PCIe directly; desc/status may be pinned too or ordinary memory.
- * - any other arena (or NEB_HOST_STAGED set in the environment): the range the descriptors touch
- *   is streamed through the device in chunks, pinned H2D -> kernel -> D2H on two streams. */
+ * - arena from neb_host_alloc (pinned, mapped, 16-byte aligned): zero-copy — every descriptor is
+ *   bounds-checked against arena_len (NEB_ERR_INVALID, nothing touched, otherwise), then the
+ *   kernels load and store the arena across PCIe directly; desc/status may be pinned or ordinary.
+ * - any other arena: the range the descriptors touch is streamed through the device in chunks of
+ *   8192 packets, H2D -> kernel -> D2H, rotated over three streams; chunks whose arena ranges
+ *   overlap are serialised (each copies its whole range back).
+ * Environment, read per call: NEB_HOST_MODE=dma (or NEB_HOST_STAGED=1) stages every arena;
+ * NEB_HOST_MODE=kcopy stages a mapped arena with copy kernels instead of DMA (slower, for A/B). */
 NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
                                 size_t arena_len, int32_t* status, uint32_t key_hint);
 NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
