@@ -565,10 +565,23 @@ __device__ __forceinline__ uint4 gcm_lane_load(const neb_desc& d, const LaneBloc
     return in;
 }
 
+// Where the length lane keeps E_K(J0) from its round to the tag finish: a register, or (the
+// mixed-key kernel, whose open would otherwise spill at 128 VGPRs) the lane's LDS slot.
+struct Ej0Reg {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    __device__ __forceinline__ void set(uint4 k) { v = k; }
+    __device__ __forceinline__ uint4 get() const { return v; }
+};
+struct Ej0Lds {
+    uint4* p;
+    __device__ __forceinline__ void set(uint4 k) { *p = k; }
+    __device__ __forceinline__ uint4 get() const { return *p; }
+};
+
 // Payload XOR and GHASH input of one block given its input and keystream. Returns X (BE words).
-template <bool OPEN>
+template <bool OPEN, class EJ>
 __device__ __forceinline__ uint4 gcm_lane_io(const neb_desc& d, const LaneBlock& b, uint4 in, uint4 ks,
-                                             uint8_t* arena, uint4& ej0) {
+                                             uint8_t* arena, EJ& ej0) {
     uint4 X = make_uint4(0, 0, 0, 0);
     if (b.is_aad) X = bswap4(in);
     if (b.is_ct) {
@@ -581,7 +594,7 @@ __device__ __forceinline__ uint4 gcm_lane_io(const neb_desc& d, const LaneBlock&
     if (b.is_len) {
         const uint64_t abits = (uint64_t)d.aad_len * 8u, cbits = (uint64_t)d.len * 8u;
         X = make_uint4((uint32_t)(abits >> 32), (uint32_t)abits, (uint32_t)(cbits >> 32), (uint32_t)cbits);
-        ej0 = ks;
+        ej0.set(ks);
     }
     return X;
 }
@@ -716,10 +729,10 @@ struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position table
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
-template <bool OPEN, class GH, class TL>
+template <bool OPEN, class GH, class TL, class EJ = Ej0Reg>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
-                                                 uint32_t lane, uint32_t lg) {
+                                                 uint32_t lane, uint32_t lg, EJ ej0 = EJ{}) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
@@ -740,7 +753,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
     const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
     const uint32_t c2 = bswap32((uint32_t)d.counter);
-    uint4 A = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
+    uint4 A = make_uint4(0, 0, 0, 0);
     auto rounds = [&](auto cm) {
         constexpr int CM = decltype(cm)::value;
         CtrConst cc{};
@@ -785,7 +798,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
     else rounds(std::integral_constant<int, 0>{});
     const uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
-    if (run && gcm_finish<OPEN>(d, V, ej0, lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
+    if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
     if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
 }
 
@@ -874,11 +887,20 @@ constexpr int kChunkWaves = 16;  // one workgroup per CU (116 KiB of LDS; 148 Ki
 constexpr int kChunkWaves = 8;
 #endif
 constexpr int kChunkThreads = kChunkWaves * kWave;
+// E_K(J0) in LDS instead of a register removes the open kernel's in-loop spills (HBM traffic 280 ->
+// 238 MB per C3 launch) but made both chunk kernels 9% slower (171 -> 186 µs, rocprof A/B,
+// tools/ab_ej0.sh): off.
+#ifndef NEB_CHUNK_EJ0_LDS
+#define NEB_CHUNK_EJ0_LDS 0
+#endif
 
 struct ChunkLds {
     uint4 shoup[kChunkWaves][kChunkTables][16];  // per wave: M[v] for H, H^2, H^4, H^8, H^16 (1.25 KiB)
 #if NEB_CHUNK_POS
     uint4 pos[kChunkWaves][8 * 16];              // per wave: position tables of H^4 (2 KiB)
+#endif
+#if NEB_CHUNK_EJ0_LDS
+    uint4 ej0[kChunkWaves][kWave];               // per lane: E_K(J0) of its packet (16 KiB)
 #endif
 #if NEB_CHUNK_T4
     uint2 ttab[2 * 256 * 32];                    // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each
@@ -956,7 +978,11 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
         const uint32_t q = lane >> lg;
         const bool valid = q < count;
         const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+#if NEB_CHUNK_EJ0_LDS
+        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg, Ej0Lds{&lds.ej0[wave][lane]});
+#else
         gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg);
+#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
