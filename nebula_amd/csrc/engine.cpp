@@ -48,7 +48,10 @@ namespace {
 
 constexpr size_t kStageMin = 1 << 16;
 constexpr int kPipeStreams = 3;
-constexpr uint32_t kPipeChunkPkts = 8192;
+#ifndef NEB_PIPE_CHUNK
+#define NEB_PIPE_CHUNK 8192
+#endif
+constexpr uint32_t kPipeChunkPkts = NEB_PIPE_CHUNK;  // packets per staged host chunk
 
 struct PipeSlot {
     hipStream_t stream = nullptr;
