@@ -116,6 +116,9 @@ NEB_API const char* neb_last_error(void);
 /* Install a 32-byte key: AES-256 key schedule + H = E_K(0^128) + H^1..H^16 (AESGCM), or the raw
  * ChaCha20 key (ChaChaPoly), computed on the device into the engine's key table. */
 NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out);
+/* Waits for every asynchronous batch this engine has enqueued (on any stream) to finish, then
+ * clears the key record and frees its slot. A batch enqueued after the key is destroyed gets
+ * NEB_STATUS_BAD_KEY for its packets (the kernels check the slot's algorithm tag). */
 NEB_API int neb_cipher_destroy(neb_cipher* c);
 NEB_API uint32_t neb_cipher_key_id(const neb_cipher* c);
 NEB_API int neb_cipher_alg(const neb_cipher* c);
@@ -162,14 +165,16 @@ NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint3
 /* ---- batched data plane: host-resident arena (the TUN / UDP side) ---------------------------- */
 
 /* Same as above but desc/arena/status live in host memory. Synchronous.
- * - arena from neb_host_alloc (pinned, mapped, 16-byte aligned): zero-copy — every descriptor is
- *   bounds-checked against arena_len (NEB_ERR_INVALID, nothing touched, otherwise), then the
- *   kernels load and store the arena across PCIe directly; desc/status may be pinned or ordinary.
+ * Every descriptor is first bounds-checked against arena_len, in every mode: an invalid batch
+ * returns NEB_ERR_INVALID with the arena and the statuses untouched.
+ * - arena pinned and mapped (neb_host_alloc, at any byte address): zero-copy — the kernels load
+ *   and store the arena across PCIe directly; desc/status may be pinned or ordinary.
  * - any other arena: the range the descriptors touch is streamed through the device in chunks of
  *   8192 packets, H2D -> kernel -> D2H, rotated over three streams; chunks whose arena ranges
  *   overlap are serialised (each copies its whole range back).
  * Environment, read per call: NEB_HOST_MODE=dma (or NEB_HOST_STAGED=1) stages every arena;
- * NEB_HOST_MODE=kcopy stages a mapped arena with copy kernels instead of DMA (slower, for A/B). */
+ * NEB_HOST_MODE=kcopy stages a mapped, 16-byte aligned arena with copy kernels instead of DMA
+ * (slower, for A/B; an unaligned one is DMA-staged). */
 NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
                                 size_t arena_len, int32_t* status, uint32_t key_hint);
 NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,

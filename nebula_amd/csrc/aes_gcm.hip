@@ -31,6 +31,7 @@
 
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
+#include "bs_aes.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
 
@@ -673,10 +674,30 @@ __device__ __forceinline__ uint4 shfl_down4(uint4 v, uint32_t d) {
 
 // GHASH tables a packet group multiplies with: horner(A) = A·H^LPP, and final(A) = the packet's
 // Σ_l A_l·H^(LPP-l), valid at least on the packet's last lane (the one holding E_K(J0)).
+// Single-key kernel, experiment (off): part of the CTR keystream from the bitsliced VALU pass
+// (bs_aes.hpp) instead of the LDS T-tables, so the VALU would carry part of the AES while the LDS
+// serves the rest. Mode 1: kBsWaves waves of the workgroup run their packets on it; mode 2: every
+// wave runs an 8-round window of its packets on it, windows staggered by wave phase. Both are
+// bit-exact (GPU parity suite) and both measured ~20% slower on C2 (seal 0.124 -> 0.148-0.152 ms,
+// DESIGN.md §3.4): the pass costs ~1.5 VALU cycles per LDS cycle it saves, and VALU work beside the
+// T-table waves slows their LDS feed.
+#ifndef NEB_BITSLICE
+#define NEB_BITSLICE 0
+#endif
+constexpr bool kBitslice = NEB_BITSLICE != 0;
+#ifndef NEB_BS_WAVES
+#define NEB_BS_WAVES 4  // bitsliced waves per single-key workgroup (one per SIMD)
+#endif
+constexpr int kBsWaves = NEB_BS_WAVES;
+#ifndef NEB_BS_MODE
+#define NEB_BS_MODE 1  // 1: kBsWaves bitsliced waves; 2: every wave, an 8-round window by wave phase
+#endif
+constexpr int kBsMode = NEB_BS_MODE;
 #ifndef NEB_SINGLE_POSH
 #define NEB_SINGLE_POSH 1  // final quad Horner on H's position tables (0: H's Shoup table)
 #endif
 struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 + tables for H
+    static constexpr bool kBitslice = true;  // one key per batch: the bitsliced CTR pass applies
     const uint4* full;
     const uint4* shoup_h;  // NEB_SINGLE_POSH: the 8 position tables of H, else its Shoup table
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const {
@@ -706,6 +727,7 @@ constexpr uint32_t kChunkTables = 5;  // Shoup tables H, H^2, H^4, H^8, H^16 (ta
 #define NEB_CHUNK_POS 1  // 4-lane chunks multiply by H^4 with position tables (gf_mul_pos)
 #endif
 struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position tables) in the wave's LDS slice
+    static constexpr bool kBitslice = false;
     const uint4* base;
     const uint4* pos;
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t lg) const {
@@ -729,10 +751,11 @@ struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position table
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
-template <bool OPEN, class GH, class TL, class EJ = Ej0Reg>
+template <bool OPEN, bool BS, class GH, class TL, class EJ = Ej0Reg>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
-                                                 uint32_t lane, uint32_t lg, EJ ej0 = EJ{}) {
+                                                 uint32_t lane, uint32_t lg, EJ ej0 = EJ{},
+                                                 const uint32_t* bs_rec = nullptr, uint32_t bs_phase = 0) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
@@ -759,44 +782,102 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         CtrConst cc{};
         if constexpr (CM == 2) cc = aes_ctr_prep8(c1, c2, T, rk);
         else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
-        for (uint32_t r = 0; r < Rmax; r++) {
+        // round r's payload XOR and GHASH fold, given G = A·H^LPP (the rounds before) and the keystream
+        auto io = [&](const LaneBlock& b, uint4 G, uint4 ks) {
+#ifndef NEB_NO_FASTIO
+            // the common round: every active lane holds a full, 16-B aligned payload block
+            // (the arena base counts too: a caller may pass an arena at any byte address)
+            const uint32_t off = 16u * (b.k - 1u);
+            const bool full = b.is_ct && off + 16u <= d.len &&
+                              ((d.src_off | d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u;
+            if (__all(full)) {
+                const uint4 in = *reinterpret_cast<const uint4*>(args.arena + d.src_off + off);
+                const uint4 out = xor4(in, ks);
+                *reinterpret_cast<uint4*>(args.arena + d.dst_off + off) = out;
+                A = xor4(G, bswap4(OPEN ? in : out));
+                return;
+            }
+#endif
+            const uint4 in = gcm_lane_load(d, b, args.arena);
+            A = xor4(G, gcm_lane_io<OPEN>(d, b, in, ks, args.arena, ej0));
+        };
+        auto horner = [&](uint32_t r) -> uint4 {
+#ifdef NEB_ABLATE_HORNER
+            return A;
+#else
+            return r == 0 ? make_uint4(0, 0, 0, 0) : gh.horner(A, lg);
+#endif
+        };
+        // one round on the LDS: GHASH of the previous rounds first, then this round's T-table AES
+        // (one phase's registers at a time)
+        auto tround = [&](uint32_t r) {
             if (r < sh.R) {
                 const LaneBlock b = lane_block(sh, r, l, lg);
-                // GHASH of the previous rounds (A·H^LPP) first, then this round's AES: one phase's
-                // registers at a time keeps the kernel at 4 waves/SIMD without spills
-#ifdef NEB_ABLATE_HORNER
-                const uint4 G = A;
-#else
-                const uint4 G = (r == 0) ? make_uint4(0, 0, 0, 0) : gh.horner(A, lg);
-#endif
+                const uint4 G = horner(r);
                 __builtin_amdgcn_sched_barrier(0);
-                const uint4 ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
-#ifndef NEB_NO_FASTIO
-                // the common round: every active lane holds a full, 16-B aligned payload block
-                // (the arena base counts too: a caller may pass an arena at any byte address)
-                const uint32_t off = 16u * (b.k - 1u);
-                const bool full = b.is_ct && off + 16u <= d.len &&
-                                  ((d.src_off | d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u;
-                if (__all(full)) {
-                    const uint4 in = *reinterpret_cast<const uint4*>(args.arena + d.src_off + off);
-                    const uint4 out = xor4(in, ks);
-                    *reinterpret_cast<uint4*>(args.arena + d.dst_off + off) = out;
-                    A = xor4(G, bswap4(OPEN ? in : out));
-                    continue;
+                io(b, G, gcm_lane_ks<CM>(b, c1, c2, cc, T, rk));
+            }
+        };
+        if constexpr (BS && CM == 2 && kBsMode == 1) {
+            // Bitsliced waves (gcm_single_kernel): the keystream of every round from the VALU pass
+            // (bs_aes.hpp), 8 rounds per pass; the length lane's slot takes counter 1 (E_K(J0)).
+            for (uint32_t w0 = 0; w0 < Rmax; w0 += 8u) {
+                const uint32_t base = 4u * w0 + 2u - sh.pad - sh.na;  // counter of block 4j + l: round w0 + j
+                const uint32_t jl = sh.R - 1u - w0;                  // the length round in this pass
+                const uint32_t jmask = jl < 8u ? 1u << (4u * jl + 3u) : 0u;
+                uint4 ks[8];
+                bs_ctr_pass(c1, c2, base, jmask, bs_rec, lane, ks);
+                const uint32_t wend = min(w0 + 8u, Rmax);
+                // one copy of the round body; the keystream registers shift down a block per round
+#pragma unroll 1
+                for (uint32_t r = w0; r < wend; r++) {
+                    if (r < sh.R) io(lane_block(sh, r, l, lg), horner(r), ks[0]);
+#pragma unroll
+                    for (int q = 0; q < 7; q++) ks[q] = ks[q + 1];
                 }
-#endif
-                const uint4 in = gcm_lane_load(d, b, args.arena);
-                A = xor4(G, gcm_lane_io<OPEN>(d, b, in, ks, args.arena, ej0));
+            }
+            return;
+        }
+        uint32_t r0 = 0;
+        if constexpr (BS && CM == 2 && kBsMode == 2) {
+            // Windowed: rounds [s, s+8) of every packet from the VALU pass, s by wave phase so the
+            // waves of one SIMD take their pass at different times; the length block after it.
+            uint32_t Rmin = run ? sh.R : 0u;
+            for (uint32_t sft = LPP; sft < 64u; sft <<= 1) Rmin = min(Rmin, (uint32_t)__shfl_xor((int)Rmin, (int)sft));
+            Rmin = __builtin_amdgcn_readfirstlane(Rmin);
+            if (lg == 2u && Rmin >= 9u) {
+                const uint32_t s = (uint32_t)bs_phase * (Rmin - 9u) / 3u;
+                for (; r0 < s; r0++) tround(r0);
+                uint4 ks[8];
+                bs_ctr_pass(c1, c2, 4u * s + 2u - sh.pad - sh.na, 0u, bs_rec, lane, ks);
+                if (valid) d = args.desc[p];  // re-derived: no registers held across the pass
+                sh.na = (d.aad_len + 15u) >> 4;
+                sh.m = (d.len + 15u) >> 4;
+                sh.n = sh.na + sh.m + 1u;
+                sh.R = run ? (sh.n + LPP - 1u) >> lg : 0u;
+                sh.pad = (sh.R << lg) - sh.n;
+                cc = aes_ctr_prep8(c1, c2, T, rk);
+#pragma unroll 1
+                for (; r0 < s + 8u; r0++) {
+                    io(lane_block(sh, r0, l, lg), horner(r0), ks[0]);
+#pragma unroll
+                    for (int q = 0; q < 7; q++) ks[q] = ks[q + 1];
+                }
             }
         }
+        for (uint32_t r = r0; r < Rmax; r++) tround(r);
     };
-    // counter caching needs every block counter of every packet in the wave below 2^8 / 2^16
+    if constexpr (BS && kBsMode == 1) {
+        rounds(std::integral_constant<int, 2>{});  // the caller checked: every counter below 2^8
+    } else {
+        // counter caching needs every block counter of every packet in the wave below 2^8 / 2^16
 #ifndef NEB_NO_CTR8
-    if (__all(sh.m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
-    else
+        if (__all(sh.m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
+        else
 #endif
-    if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
-    else rounds(std::integral_constant<int, 0>{});
+        if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
+        else rounds(std::integral_constant<int, 0>{});
+    }
     const uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
     if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
     if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
@@ -865,12 +946,28 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     const RkRegs rk{rks};
     const GhFull gh{lds.full, lds.shoup_h};
 
+    // The slot must still hold an AES-GCM key when the batch runs (a key destroyed, or its slot
+    // reused by another algorithm, while the batch was queued): every packet gets BAD_KEY then.
+    const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
+    // the last kBsWaves waves (one per SIMD) run the bitsliced keystream (bs_aes.hpp)
+    const bool bs_wave = kBitslice && (kBsMode == 2 || wave >= (uint32_t)(kSingleWaves - kBsWaves));
     uint32_t npkt = args.npkt;
     if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
     for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
         const uint32_t p = grp * kPpw + lane / kLpp;
-        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, true, rk, gh, T, lane, kLg);
+        // a bitsliced wave takes the group if every packet's counters stay below 2^8 (its
+        // counter planes are one byte); otherwise the T-table path
+        bool use_bs = bs_wave;
+        if (use_bs && kBsMode == 1) {
+            const uint32_t len = p < npkt ? args.desc[p].len : 0u;
+            use_bs = __all(((len + 15u) >> 4) + 1u < 256u);
+        }
+        if (use_bs)
+            gcm_packet_group<OPEN, true>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, Ej0Reg{},
+                                         srec, (wave >> 2) & 3u);
+        else
+            gcm_packet_group<OPEN, false>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg);
     }
 }
 
@@ -979,9 +1076,9 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
         const bool valid = q < count;
         const uint32_t p = valid ? ca.sorted[start + q] : 0u;
 #if NEB_CHUNK_EJ0_LDS
-        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg, Ej0Lds{&lds.ej0[wave][lane]});
+        gcm_packet_group<OPEN, false>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg, Ej0Lds{&lds.ej0[wave][lane]});
 #else
-        gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg);
+        gcm_packet_group<OPEN, false>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg);
 #endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();

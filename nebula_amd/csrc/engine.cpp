@@ -70,6 +70,22 @@ struct PipeSlot {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// [off, off + len) lies inside [0, cap), written so that no sum can wrap around 2^64.
+inline bool span_in(uint64_t off, uint64_t len, uint64_t cap) { return off <= cap && len <= cap - off; }
+
+}  // namespace
+
+// Every region a descriptor touches lies inside a host arena of arena_len bytes: the AAD, the
+// source (payload, plus the tag when opening) and the destination (payload, plus the tag when
+// sealing). Shared with window.cpp, which validates a receive batch before touching anything.
+bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len) {
+    const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
+    return span_in(d.src_off, pay, arena_len) && span_in(d.dst_off, outl, arena_len) &&
+           span_in(d.aad_off, d.aad_len, arena_len);
+}
+
+namespace {
+
 // Arena span copy across PCIe for the kernel-staged host path: each wave instruction moves 1 KiB of
 // contiguous bytes (64 lanes x 16 B) and every lane has four loads in flight before its stores, so
 // the link carries full-size requests instead of the 64-byte pieces the zero-copy kernels issue.
@@ -185,7 +201,25 @@ struct neb_engine {
 
     SchedSpace sched;
     TxSpace tx;
+
+    // Asynchronous batches (neb_seal_batch / neb_open_batch / neb_tx_seal_batch) read key records
+    // after the call returns: the last launch on each caller stream is recorded here, and
+    // neb_cipher_destroy waits for all of them before it clears and frees a slot.
+    std::mutex fl_mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> inflight;
 };
+
+// Record the end of the work just enqueued on caller stream s (see neb_engine::inflight).
+static hipError_t note_inflight(neb_engine* e, hipStream_t s) {
+    std::lock_guard<std::mutex> g(e->fl_mu);
+    for (auto& f : e->inflight)
+        if (f.first == s) return hipEventRecord(f.second, s);
+    hipEvent_t ev = nullptr;
+    hipError_t err = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (err != hipSuccess) return err;
+    e->inflight.emplace_back(s, ev);
+    return hipEventRecord(ev, s);
+}
 
 struct neb_cipher {
     neb_engine* e;
@@ -305,6 +339,10 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
     if (e->tx.done) { hipEventSynchronize(e->tx.done); hipEventDestroy(e->tx.done); }
     if (e->tx.mem) hipFree(e->tx.mem);
     if (e->tx.d_io) hipFree(e->tx.d_io);
+    for (auto& f : e->inflight) {
+        hipEventSynchronize(f.second);
+        hipEventDestroy(f.second);
+    }
     if (e->zc_desc) hipFree(e->zc_desc);
     if (e->zc_status) hipFree(e->zc_status);
     if (e->d_keys) hipFree(e->d_keys);
@@ -374,9 +412,13 @@ NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb
 NEB_API int neb_cipher_destroy(neb_cipher* c) {
     if (!c) return NEB_ERR_INVALID;
     neb_engine* e = c->e;
+    hipSetDevice(e->device);
+    {  // batches still queued on caller streams may read this record: let them finish first
+        std::lock_guard<std::mutex> g(e->fl_mu);
+        for (auto& f : e->inflight) hipEventSynchronize(f.second);
+    }
     {
         std::lock_guard<std::mutex> g(e->io_mu);
-        hipSetDevice(e->device);
         hipMemsetAsync(e->d_keys + (size_t)c->key_id * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, e->stream);
         hipStreamSynchronize(e->stream);
     }
@@ -558,6 +600,7 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
     hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream, as for any HIP launch
     hipError_t err = launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s);
+    if (err == hipSuccess) err = note_inflight(e, s);
     if (err != hipSuccess) {
         set_error("batch launch", err);
         return NEB_ERR_HIP;
@@ -591,13 +634,6 @@ static bool host_mapped(const void* p) {
 // on the host first: a kernel access outside the mapping would fault the GPU.
 static int batch_host_zero_copy(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n,
                                 uint8_t* arena, size_t arena_len, int32_t* status, uint32_t key_hint) {
-    for (uint32_t i = 0; i < n; i++) {
-        const neb_desc& d = desc[i];
-        const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
-        if (d.src_off + pay > arena_len || d.dst_off + outl > arena_len || d.aad_off + d.aad_len > arena_len ||
-            pay > arena_len || (uint64_t)d.aad_len > arena_len)
-            return NEB_ERR_INVALID;
-    }
     const bool desc_mapped = host_mapped(desc), status_mapped = host_mapped(status);
     if ((!desc_mapped || !status_mapped) && n > e->zc_cap) {
         HIP_TRY(hipStreamSynchronize(e->stream));
@@ -622,28 +658,33 @@ static int batch_host_zero_copy(neb_engine* e, int alg, int open, const neb_desc
     return NEB_OK;
 }
 
-// Host-resident batch. A pinned, mapped, 16-byte aligned arena runs zero-copy (above). Any other
-// arena is staged in chunks of kPipeChunkPkts packets rotated over kPipeStreams streams: each
-// chunk's arena span is copied in (hipMemcpyAsync), sealed/opened on the device and copied back, so
-// one chunk's copy-in overlaps another's kernel and another's copy-back. NEB_HOST_MODE=kcopy stages
-// a mapped arena with span_copy_kernel instead (measured slower, kept for the A/B); =dma forces
-// hipMemcpyAsync staging.
+// Host-resident batch. A pinned, mapped arena runs zero-copy (above). Any other arena is staged in
+// chunks of kPipeChunkPkts packets rotated over kPipeStreams streams: each chunk's arena span is
+// copied in (hipMemcpyAsync), sealed/opened on the device and copied back, so one chunk's copy-in
+// overlaps another's kernel and another's copy-back. NEB_HOST_MODE=kcopy stages a mapped arena with
+// span_copy_kernel instead (measured slower, kept for the A/B); =dma forces hipMemcpyAsync staging.
+// Every descriptor is checked before anything is copied or launched, in every mode: an invalid batch
+// returns NEB_ERR_INVALID with the arena and the statuses untouched.
 static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n, uint8_t* arena,
                       size_t arena_len, int32_t* status, uint32_t key_hint) {
     int rc = check_batch(e, alg, key_hint);
     if (rc != NEB_OK) return rc;
     if (n == 0) return NEB_OK;
     if (!desc || !arena || !status) return NEB_ERR_INVALID;
+    for (uint32_t i = 0; i < n; i++)
+        if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
     std::lock_guard<std::mutex> g(e->pipe_mu);
     hipSetDevice(e->device);
     const HostMode mode = host_mode();
-    // The kernels' aligned fast paths test descriptor offsets, not addresses, so the kernels touch
-    // a host arena directly only when it is 16-byte aligned; otherwise it is staged by DMA into a
-    // device buffer with the same alignment modulo 16.
-    const bool mapped = mode != kHostDma && ((uintptr_t)arena & 15) == 0 && host_mapped(arena);
+    // The kernels' vector fast path tests the absolute address (arena base + offset), so a mapped
+    // arena at any byte address runs zero-copy. A staged arena lands in a device buffer with the
+    // same alignment modulo 16, so the kernels take the same paths either way.
+    const bool mapped = mode != kHostDma && host_mapped(arena);
     if (mapped && mode == kHostZeroCopy)
         return batch_host_zero_copy(e, alg, open, desc, n, arena, arena_len, status, key_hint);
-    const bool kcopy = mapped;  // mapped, aligned arena: copies by span_copy_kernel
+    // mapped arena: copies by span_copy_kernel, whose 16-byte vector copies need an aligned base
+    // (an unaligned one is DMA-staged)
+    const bool kcopy = mapped && ((uintptr_t)arena & 15) == 0;
     for (auto& s : e->pipe) {
         if (!s.stream) {
             HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
@@ -675,22 +716,12 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         PipeSlot& s = e->pipe[slot];
         if (s.count) HIP_TRY(retire(s));  // retire this slot's previous chunk before reusing its buffers
         const uint32_t cnt = std::min(kPipeChunkPkts, n - begin);
-        uint64_t lo = ~0ULL, hi = 0;
+        uint64_t lo = ~0ULL, hi = 0;  // every sum below stays within arena_len (checked above)
         for (uint32_t i = 0; i < cnt; i++) {
             const neb_desc& d = desc[begin + i];
             const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
             lo = std::min({lo, d.src_off, d.dst_off, d.aad_off});
             hi = std::max({hi, d.src_off + pay, d.dst_off + outl, d.aad_off + d.aad_len});
-        }
-        if (hi > arena_len || lo > hi) {
-            if (pend >= 0) {
-                PipeSlot& p = e->pipe[pend];
-                HIP_TRY(span_copy(arena + p.lo, p.d_buf, (size_t)(p.hi - p.lo), ks));
-                HIP_TRY(hipEventRecord(p.done, ks));
-            }
-            for (auto& o : e->pipe)
-                if (o.count) HIP_TRY(retire(o));
-            return NEB_ERR_INVALID;
         }
         lo &= ~(uint64_t)15;
         // A chunk copies its whole span back, so spans of chunks in flight must not overlap (the
@@ -826,8 +857,10 @@ NEB_API int neb_tx_seal_batch(neb_engine* e, int alg, neb_tx_tunnel* d_tunnels, 
         return NEB_OK;
     }
     std::lock_guard<std::mutex> g(e->tx.mu);
-    return tx_run(e, alg, d_tunnels, ntunnels, d_packets, npackets, d_in, d_out, out_cap, d_wires, d_wire_status,
-                  max_wires, d_nwires, d_packet_status, key_hint, s);
+    rc = tx_run(e, alg, d_tunnels, ntunnels, d_packets, npackets, d_in, d_out, out_cap, d_wires, d_wire_status,
+                max_wires, d_nwires, d_packet_status, key_hint, s);
+    if (rc == NEB_OK) HIP_TRY(note_inflight(e, s));
+    return rc;
 }
 
 NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnels, uint32_t ntunnels,
@@ -844,10 +877,10 @@ NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnel
     // the input span the packets touch, uploaded once
     uint64_t lo = ~0ull, hi = 0;
     for (uint32_t i = 0; i < npackets; i++) {
+        if (!span_in(packets[i].in_off, packets[i].len, in_len)) return NEB_ERR_INVALID;
         lo = std::min(lo, packets[i].in_off);
         hi = std::max(hi, packets[i].in_off + packets[i].len);
     }
-    if (hi > in_len) return NEB_ERR_INVALID;
     lo &= ~(uint64_t)15;
     const size_t span = (size_t)(hi - lo);
     const size_t o_tun = 0, o_pk = align_up((size_t)ntunnels * sizeof(neb_tx_tunnel), 256);

@@ -28,6 +28,8 @@
 
 #include "../../include/nebula_aead.h"
 
+bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len);  // engine.cpp
+
 namespace {
 
 struct WindowCore {
@@ -184,6 +186,9 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
                                    int32_t* status, uint32_t key_hint) {
     if (!e || (n && (!desc || !arena || !status || !windows))) return NEB_ERR_INVALID;
     if (n == 0) return NEB_OK;
+    // an invalid batch is refused before any window moves or any packet is opened
+    for (uint32_t i = 0; i < n; i++)
+        if (!neb_desc_in_arena(desc[i], 1, arena_len)) return NEB_ERR_INVALID;
     // Windows are independent: group the batch by window (stable, so each window sees its packets
     // in arrival order) and run each window's sequence under one lock acquisition.
     std::vector<uint32_t> start(nwindows + 2, 0), order(n);

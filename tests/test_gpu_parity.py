@@ -392,3 +392,68 @@ def test_host_zero_copy_rejects_out_of_bounds(engine):
         buf.free()
         for c in ciphers:
             c.destroy()
+
+
+WRAP = 2**64 - 16  # an offset whose sum with any length wraps around 2^64
+
+
+@pytest.mark.parametrize("mode", ["zc", "dma", "kcopy"])
+@pytest.mark.parametrize("case", ["src_wrap", "dst_wrap", "aad_wrap", "past_end"])
+def test_host_rejects_invalid_descriptor_untouched(engine, mode, case, monkeypatch):
+    """A host batch with one bad descriptor — an offset near 2^64 whose end wraps around, or a
+    length past the arena — is refused before anything is copied or launched, in every host mode.
+    The bad descriptor is the last of a 20000-packet batch, so the staged modes would otherwise
+    have sealed their first chunks in place already."""
+    from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
+
+    monkeypatch.setenv("NEB_HOST_MODE", mode)
+    b = W.make_batch(L.ALG_AESGCM, 20000, 4, sizes=(90, 576, 1300), ratio=(7, 4, 1), name="wrap")
+    ciphers = install_keys(engine, b)
+    buf = PinnedBuffer(b.arena.nbytes)
+    try:
+        buf.array[:] = b.arena
+        d = slot_desc(b, ciphers)
+        if case == "past_end":
+            d["len"][-1] = b.stride * 4
+        else:
+            d[case.split("_")[0] + "_off"][-1] = WRAP
+        for open_ in (False, True):
+            with pytest.raises(Exception):
+                host_batch(engine, b.alg, open_, d, buf.array)
+            assert np.array_equal(buf.array, b.arena), (mode, case, open_)
+    finally:
+        buf.free()
+        for c in ciphers:
+            c.destroy()
+
+
+def test_cipher_destroy_waits_for_queued_batches(engine, oracle_mod):
+    """neb_cipher_destroy right after an asynchronous seal was enqueued behind other work on the
+    caller's stream: the batch still runs with the installed key (destroy waits for it), so the
+    output equals the oracle; the slot is free afterwards."""
+    import torch
+
+    from nebula_amd.batch import DeviceBatch, install_keys
+
+    b = W.config(2, 1 / 16)
+    ref, _ = oracle_seal(oracle_mod, b)
+    ciphers = install_keys(engine, b)
+    db = DeviceBatch(engine, b, ciphers)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x = torch.randn(4096, 4096, device="cuda")
+        for _ in range(8):  # a few ms of work ahead of the seal on the same stream
+            x = x @ x
+            x = x / x.norm()
+        db.seal(stream=s.cuda_stream)
+    slot = ciphers[0].key_id
+    ciphers[0].destroy()
+    s.synchronize()
+    assert (db.status_host() == 0).all()
+    assert np.array_equal(db.arena_host(), ref)
+    from nebula_amd.noiseutil import CipherAESGCM
+    again = CipherAESGCM.Cipher(engine, bytes(range(32)))  # the freed slot is handed out again
+    try:
+        assert again.key_id == slot
+    finally:
+        again.destroy()

@@ -140,3 +140,31 @@ def test_rx_batch_random_traffic(engine, oracle_mod):
             c = cur[t] + rng.randrange(1, 30)
         arr.append((t, c, rng.random() < 0.05))
     _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=8, window_len=64, seed=3)
+
+
+def test_rx_batch_invalid_descriptor_touches_nothing(engine, oracle_mod):
+    """A receive batch with a descriptor whose offset wraps around 2^64 is refused before any
+    window moves or any packet is opened."""
+    from nebula_amd.connection_state import Bits, rx_open_batch
+    from nebula_amd.noiseutil import CipherAESGCM
+
+    keys = [bytes(range(32))]
+    arrivals = [(0, c, False) for c in range(3, 40)]
+    arena, desc, _ = _build(oracle_mod, L.ALG_AESGCM, keys, arrivals, 5)
+    c = CipherAESGCM.Cipher(engine, keys[0])
+    try:
+        w = Bits(8192)
+        w.Update(1)
+        w.Update(2)
+        windows = [None] * engine.max_keys
+        windows[c.key_id] = w
+        d = desc.copy()
+        d["key_id"] = c.key_id
+        d["aad_off"][-1] = 2**64 - 8
+        before = arena.copy()
+        with pytest.raises(Exception):
+            rx_open_batch(engine, L.ALG_AESGCM, windows, d, arena)
+        assert np.array_equal(arena, before)
+        assert (w.current, w.lost, w.dupe, w.out_of_window) == (2, 0, 0, 0)
+    finally:
+        c.destroy()
