@@ -124,10 +124,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
-    ap.add_argument("--mode", choices=["device", "host", "host-kcopy", "host-staged", "tx", "rx"], default="device",
+    ap.add_argument("--mode", choices=["device", "host", "host-kcopy", "host-staged", "host-split", "tx", "rx"],
+                    default="device",
                     help="device: the headline; host: host-resident batch (pinned arena: zero-copy); "
                          "host-kcopy: the pinned arena staged by span-copy kernels; "
-                         "host-staged: the same through hipMemcpyAsync staging; tx: the device TX batch "
+                         "host-staged: the same through hipMemcpyAsync staging; host-split: sources DMA-staged, "
+                         "outputs stored by the kernel into the pinned arena; tx: the device TX batch "
                          "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -173,7 +175,9 @@ def main():
         os.environ["NEB_HOST_MODE"] = "dma"  # read by the engine at its first host batch
     if args.mode == "host-kcopy":
         os.environ["NEB_HOST_MODE"] = "kcopy"
-    if args.mode in ("host", "host-kcopy", "host-staged"):
+    if args.mode == "host-split":
+        os.environ["NEB_HOST_MODE"] = "split"
+    if args.mode in ("host", "host-kcopy", "host-staged", "host-split"):
         from nebula_amd.batch import PinnedBuffer
 
         d = slot_desc(b, ciphers)
@@ -196,6 +200,8 @@ def main():
                 "metric": {"host": "GiB/s host-resident (pinned arena, zero-copy: kernels load/store it over PCIe) ",
                            "host-kcopy": "GiB/s host-resident (pinned arena, span-copy kernels in/out around seal/open) ",
                            "host-staged": "GiB/s host-resident (pinned hipMemcpyAsync H2D + kernel + D2H, 3 streams) ",
+                           "host-split": "GiB/s host-resident (pinned arena: hipMemcpyAsync H2D of the sources, kernel "
+                                         "stores into the arena) ",
                            }[args.mode]
                 + ("AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch" if cfg == 1 else
                    f"{'AES-256-GCM' if b.alg == L.ALG_AESGCM else 'ChaCha20-Poly1305'} seal+open ({workload_name})"),

@@ -153,7 +153,7 @@ hipError_t span_copy(uint8_t* dst, const uint8_t* src, size_t nbytes, hipStream_
 
 // Host batch path: NEB_HOST_MODE = "zc" (kernels on the mapped arena), "kcopy" (mapped arena staged
 // by span_copy_kernel), "dma" (hipMemcpyAsync staging); NEB_HOST_STAGED=1 is the older name of "dma".
-enum HostMode { kHostZeroCopy, kHostKernelCopy, kHostDma };
+enum HostMode { kHostZeroCopy, kHostKernelCopy, kHostDma, kHostSplit };
 // Zero-copy is the default: measured on one MI355X (C2 seal+open, 64 Ki x 1300 B) it runs at 28.4
 // GiB/s against 23.9 for DMA staging and 18.1 for span-copy staging.
 HostMode host_mode() {  // read per batch (a few hundred ns), so a process can switch between batches
@@ -161,6 +161,7 @@ HostMode host_mode() {  // read per batch (a few hundred ns), so a process can s
     const char* v = std::getenv("NEB_HOST_MODE");
     if (v && !std::strcmp(v, "kcopy")) return kHostKernelCopy;
     if (v && !std::strcmp(v, "dma")) return kHostDma;
+    if (v && !std::strcmp(v, "split")) return kHostSplit;
     return kHostZeroCopy;
 }
 
@@ -684,11 +685,17 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         return batch_host_zero_copy(e, alg, open, desc, n, arena, arena_len, status, key_hint);
     // mapped arena: copies by span_copy_kernel, whose 16-byte vector copies need an aligned base
     // (an unaligned one is DMA-staged)
-    const bool kcopy = mapped && ((uintptr_t)arena & 15) == 0;
+    const bool kcopy = mapped && mode == kHostKernelCopy && ((uintptr_t)arena & 15) == 0;
+    // split (mapped arena): each chunk's sources (payload, AAD) are DMA-staged into a device buffer
+    // while the kernel stores its outputs straight into the mapped arena, so the copy engine carries
+    // the H2D direction and the kernel's stores the D2H one, and nothing is copied back.
+    const bool split = mapped && mode == kHostSplit;
     for (auto& s : e->pipe) {
         if (!s.stream) {
             HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+            // system-scope release: a split chunk's kernel stores into the mapped arena, which is
+            // non-coherent (L2-cached) host memory by default; the event must make them visible
+            HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventReleaseToSystem));
             HIP_TRY(hipMalloc((void**)&s.d_desc, kPipeChunkPkts * sizeof(neb_desc)));
             HIP_TRY(hipMalloc((void**)&s.d_status, kPipeChunkPkts * sizeof(int32_t)));
             HIP_TRY(hipHostMalloc((void**)&s.h_desc, kPipeChunkPkts * sizeof(neb_desc), hipHostMallocDefault));
@@ -720,14 +727,19 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         for (uint32_t i = 0; i < cnt; i++) {
             const neb_desc& d = desc[begin + i];
             const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
-            lo = std::min({lo, d.src_off, d.dst_off, d.aad_off});
-            hi = std::max({hi, d.src_off + pay, d.dst_off + outl, d.aad_off + d.aad_len});
+            if (split) {  // only what the kernel reads is staged
+                lo = std::min({lo, d.src_off, d.aad_off});
+                hi = std::max({hi, d.src_off + pay, d.aad_off + d.aad_len});
+            } else {
+                lo = std::min({lo, d.src_off, d.dst_off, d.aad_off});
+                hi = std::max({hi, d.src_off + pay, d.dst_off + outl, d.aad_off + d.aad_len});
+            }
         }
         lo &= ~(uint64_t)15;
         // A chunk copies its whole span back, so spans of chunks in flight must not overlap (the
         // descriptors need not be in arena order): retire any other slot whose span intersects.
         // (kcopy chunks are ordered by their one stream; only the launch shared with `pend` races.)
-        if (!kcopy)
+        if (!kcopy && !split)
             for (auto& o : e->pipe)
                 if (&o != &s && o.count && o.lo < hi && lo < o.hi) HIP_TRY(retire(o));
         s.lo = lo;
@@ -742,8 +754,9 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         for (uint32_t i = 0; i < cnt; i++) {
             neb_desc d = desc[begin + i];
             d.src_off -= lo;
-            d.dst_off -= lo;
             d.aad_off -= lo;
+            // split: the kernel's d_buf + dst_off must land on the mapped arena (64-bit wrap-around)
+            d.dst_off = split ? (uint64_t)(uintptr_t)(arena + d.dst_off) - (uint64_t)(uintptr_t)s.d_buf : d.dst_off - lo;
             s.h_desc[i] = d;
         }
         s.user_status = status;
@@ -772,6 +785,11 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s.stream));
         HIP_TRY(hipMemcpyAsync(s.d_buf, arena + lo, span, hipMemcpyHostToDevice, s.stream));
         HIP_TRY(launch_batch(e, alg, open, s.d_desc, cnt, s.d_buf, s.d_status, key_hint, s.stream, nullptr, s.sched));
+        if (split) {
+            HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
+            HIP_TRY(hipEventRecord(s.done, s.stream));
+            continue;
+        }
         HIP_TRY(hipMemcpyAsync(arena + lo, s.d_buf, span, hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipEventRecord(s.done, s.stream));

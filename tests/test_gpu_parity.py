@@ -341,7 +341,7 @@ def test_host_pipeline_matches_device(engine, oracle_mod, alg, arena_kind):
             c.destroy()
 
 
-@pytest.mark.parametrize("mode", ["kcopy", "zc", "dma"])
+@pytest.mark.parametrize("mode", ["kcopy", "zc", "dma", "split"])
 def test_host_modes_shuffled_descriptors(engine, oracle_mod, mode, monkeypatch):
     """Every host path (span-copy kernels, zero-copy, hipMemcpyAsync staging) on a pinned arena with
     the descriptors in random order: pipeline chunks then cover overlapping arena spans, which the
@@ -397,7 +397,7 @@ def test_host_zero_copy_rejects_out_of_bounds(engine):
 WRAP = 2**64 - 16  # an offset whose sum with any length wraps around 2^64
 
 
-@pytest.mark.parametrize("mode", ["zc", "dma", "kcopy"])
+@pytest.mark.parametrize("mode", ["zc", "dma", "kcopy", "split"])
 @pytest.mark.parametrize("case", ["src_wrap", "dst_wrap", "aad_wrap", "past_end"])
 def test_host_rejects_invalid_descriptor_untouched(engine, mode, case, monkeypatch):
     """A host batch with one bad descriptor — an offset near 2^64 whose end wraps around, or a
