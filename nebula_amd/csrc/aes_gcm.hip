@@ -1006,6 +1006,18 @@ struct ChunkLds {
 #endif
 };
 
+// Chunk order (the chunks are sorted longest first):
+//  2 (default): workgroup w owns chunks w, w + G, w + 2G, ... and its waves draw them from an LDS
+//     cursor one chunk ahead, so the next descriptor load overlaps the current chunk. Balance stays
+//     dynamic inside the workgroup and no wave touches a global atomic: C3 step -8%, IMIX -27%
+//     against 0 (A/B, profiles/r2_micro/ab_chunk_order.log).
+//  1: a static stride over all waves, next descriptor loaded ahead (C3 +5%, IMIX -12%).
+//  0: one global work cursor drawn after each chunk (round 1): its returning atomics on one word
+//     serialise across the chip.
+#ifndef NEB_CHUNK_STATIC
+#define NEB_CHUNK_STATIC 2
+#endif
+
 struct ChunkArgs {
     const uint32_t* sorted;
     const uint4* chunks;
@@ -1029,7 +1041,11 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
     const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
     const uint32_t nback = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
     const uint32_t nch = nfront + nback;
+#if NEB_CHUNK_STATIC == 2
+    if (blockIdx.x >= nch) return;  // owns no chunk (uniform over the workgroup)
+#else
     if (blockIdx.x * (uint32_t)kChunkWaves >= nch) return;  // uniform over the workgroup
+#endif
 #if NEB_CHUNK_T4
     for (uint32_t i = tid; i < 2u * 256u * 32u; i += kChunkThreads) lds.ttab[i] = ttab4_entry(i);
 #else
@@ -1049,8 +1065,35 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
     // pulling its first chunk off one atomic word at launch would serialise ~4096 dequeues at
     // ≈88/µs (MI355X_MICROARCH.md, dequeue).
     const uint32_t nwaves = gridDim.x * kChunkWaves;
+#if NEB_CHUNK_STATIC == 2
+    // workgroup w owns chunks w, w + G, w + 2G, ... (G workgroups; longest first); its waves draw
+    // them from an LDS cursor, one chunk ahead, so the next descriptor is in flight meanwhile
+    __shared__ uint32_t wg_cursor;
+    if (tid == 0) wg_cursor = kChunkWaves;
+    __syncthreads();
+    auto chunk_of = [&](uint32_t k) { return blockIdx.x + k * gridDim.x; };
+    uint32_t c = chunk_of(wave);
+#elif NEB_CHUNK_STATIC == 1
+    uint32_t c = blockIdx.x * kChunkWaves + wave;
+#endif
+#if NEB_CHUNK_STATIC
+    // static stride over the longest-first chunk order, next descriptor loaded one chunk ahead
+    uint4 ch_next = ca.chunks[0];
+    if (c < nch) ch_next = ca.chunks[c < nfront ? c : ca.max_chunks - 1u - (c - nfront)];
+    while (c < nch) {
+        const uint4 ch = ch_next;
+#if NEB_CHUNK_STATIC == 2
+        uint32_t k = 0;
+        if (lane == 0u) k = atomicAdd(&wg_cursor, 1u);
+        const uint32_t cn = chunk_of(__builtin_amdgcn_readfirstlane(k));
+#else
+        const uint32_t cn = c + nwaves;
+#endif
+        if (cn < nch) ch_next = ca.chunks[cn < nfront ? cn : ca.max_chunks - 1u - (cn - nfront)];
+#else
     for (uint32_t c = blockIdx.x * kChunkWaves + wave; c < nch;) {
         const uint4 ch = ca.chunks[c < nfront ? c : ca.max_chunks - 1u - (c - nfront)];  // wave-uniform
+#endif
         const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
         const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
         const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
@@ -1083,12 +1126,16 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if NEB_CHUNK_STATIC
+        c = cn;
+#else
         uint32_t next = nch;
         if (nch > nwaves) {
             if (lane == 0u) next = atomicAdd(&ca.counters[kCntWork], 1u);
             next = nwaves + __builtin_amdgcn_readfirstlane(next);
         }
         c = next;
+#endif
     }
 }
 
