@@ -8,7 +8,7 @@ import os
 import re
 import sys
 
-CUS, SIMDS_PER_CU, VALU_CYCLES = 256, 4, 4
+CUS, SIMDS_PER_CU, VALU_CYCLES = 256, 4, 2
 
 
 def short(name):
