@@ -29,9 +29,9 @@ constexpr uint32_t kRecPos16 = kRecPos8 + 8 * 16 * 4;
 // position tables of H itself: the single-key kernel's final quad Horner (4 multiplies by H)
 constexpr uint32_t kRecPos1 = kRecPos16 + 8 * 16 * 4;
 static_assert(kRecPos1 + 8 * 16 * 4 == kKeyRecDwords, "record layout");
-// position tables of H^(2^lg), lg = 2, 3, 4
+// position tables of H^(2^lg), lg = 0, 2, 3, 4 (lg 0: the mixed-key kernel's one-lane chunks)
 __host__ __device__ constexpr uint32_t rec_pos_table(uint32_t lg) {
-    return lg == 2u ? kRecFull : (lg == 3u ? kRecPos8 : kRecPos16);
+    return lg == 0u ? kRecPos1 : (lg == 2u ? kRecFull : (lg == 3u ? kRecPos8 : kRecPos16));
 }
 
 // ChaCha20-Poly1305 record

@@ -42,13 +42,15 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
     const uint32_t c = b < nb ? ws.hist[b] : 0u;
     const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
-    const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
+    const uint32_t nwide = NEB_WIDE_CHUNKS ? c / kWidePkts : 0u;
+    const uint32_t rest = c - nwide * kWidePkts;
+    const uint32_t nfull = rest / kChunkPkts, tail = rest % kChunkPkts;
     const uint32_t lg = tail ? sched_tail_lg(tail, cls) : 2u;
     // chunks at 4 lanes per packet (the long ones) go to the front, the short tails to the back:
     // the crypto kernel takes them in that order. Front <= n/16 + bins, back <= bins and
     // front + back <= n/16 + min(n, bins): the ranges never meet inside max_chunks
     // (sched_max_chunks).
-    const uint32_t nfront = nfull + (tail && lg == 2u ? 1u : 0u), nback = tail && lg != 2u ? 1u : 0u;
+    const uint32_t nfront = nwide + nfull + (tail && lg == 2u ? 1u : 0u), nback = tail && lg != 2u ? 1u : 0u;
     uint32_t off_p, off_f, off_b, tot_p, tot_f, tot_b;
     Scan(tmp).ExclusiveSum(c, off_p, tot_p);
     __syncthreads();
@@ -64,11 +66,14 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     if (c == 0u) return;
     const uint32_t base = wg_base[0] + off_p;
     ws.base[b] = base;
-    const uint32_t cf = wg_base[1] + off_f;
+    const uint32_t cw = wg_base[1] + off_f;
+    for (uint32_t j = 0; j < nwide && cw + j < ws.max_chunks; j++)
+        ws.chunks[cw + j] = make_uint4(base + j * kWidePkts, kWidePkts, key, cls);  // lg 0
+    const uint32_t cf = cw + nwide, pbase = base + nwide * kWidePkts;
     for (uint32_t j = 0; j < nfull && cf + j < ws.max_chunks; j++)
-        ws.chunks[cf + j] = make_uint4(base + j * kChunkPkts, kChunkPkts, key, cls | (2u << kChunkLgShift));
+        ws.chunks[cf + j] = make_uint4(pbase + j * kChunkPkts, kChunkPkts, key, cls | (2u << kChunkLgShift));
     if (tail) {
-        const uint4 ch = make_uint4(base + nfull * kChunkPkts, tail, key, cls | (lg << kChunkLgShift));
+        const uint4 ch = make_uint4(pbase + nfull * kChunkPkts, tail, key, cls | (lg << kChunkLgShift));
         if (lg == 2u) {
             if (cf + nfull < ws.max_chunks) ws.chunks[cf + nfull] = ch;
         } else {

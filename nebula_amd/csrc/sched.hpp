@@ -24,6 +24,16 @@ constexpr uint32_t kSizeClasses = 8;  // round-count classes at 4 lanes per pack
 // exist (size class 0: <= 4 blocks, lg 2; class 1: <= 8 blocks, lg 3). A wave then runs a tail of
 // 1-4 packets in a quarter of the rounds instead of leaving 48-60 of its lanes idle.
 constexpr uint32_t kChunkLgShift = 8;  // chunk.w = size class | lg << kChunkLgShift
+// Wide chunks: a bin's first c / 64 x 64 packets run at one lane per packet (lg 0, Horner stride H,
+// position tables of H). Its GHASH final is one multiply per packet instead of the 4-lane tree's
+// 3 per lane, and a chunk carries 4x the packets for one staging of the key's tables: for a
+// 90-B packet 9 multiplies instead of 20. Off: C5 step 1.67 -> 1.71 ms with it (A/B,
+// profiles/r2_micro/ab_wide_chunks.log) — at one lane per packet every payload load instruction
+// touches 64 different cache lines.
+#ifndef NEB_WIDE_CHUNKS
+#define NEB_WIDE_CHUNKS 0
+#endif
+constexpr uint32_t kWidePkts = 64;
 __host__ __device__ inline uint32_t sched_tail_lg(uint32_t count, uint32_t cls) {
     const uint32_t fit = count <= 4u ? 4u : (count <= 8u ? 3u : 2u);
     const uint32_t size = cls == 0u ? 2u : (cls == 1u ? 3u : 4u);

@@ -12,6 +12,8 @@ if cfg == 4:
     b = W.make_batch(1, 65536, 4096, sizes=(90, 576, 1300), ratio=(7, 4, 1))
 elif cfg == 5:  # 61440 wave-groups: divides evenly over 16, 20 and 24 waves per CU
     b = W.make_batch(1, 983040, 1)
+elif cfg == 8:  # C5 on one GPU: 1 Mi IMIX packets over 4096 keys
+    b = W.config(4)
 elif cfg in (6, 7):  # exactly 4 (6) or 16 (7) packets per key, 4096 keys: all tail / all full chunks
     per = 4 if cfg == 6 else 16
     b = W.make_batch(1, 4096 * per, 4096)
