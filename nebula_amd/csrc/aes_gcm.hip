@@ -117,9 +117,11 @@ __device__ __forceinline__ T lds_at(const void* base, uint32_t byte_off) {
 // c = l mod 32 and reads single dwords: T0 at lb.x = 8c + 4(c >= 16), T2 at lb.y = 8c + 4(c < 16).
 // A ds_read_b32 banks on (addr/4) mod 32, so the 32 lanes of a half-wave hit dwords 2c + {0,1}
 // arranged to be 32 distinct banks: every lookup is conflict-free.
-__device__ __forceinline__ uint2 ttab_lane_base(uint32_t lane) {
+// high: added to both lane bases (bit 16 when the table sits at LDS byte 65536 + an offset-field
+// constant, so every lookup address is still one v_perm: its byte 2 comes from the lane base)
+__device__ __forceinline__ uint2 ttab_lane_base(uint32_t lane, uint32_t high = 0u) {
     const uint32_t c = lane & 31u, hi = c >> 4;
-    return make_uint2((c << 3) | (hi << 2), (c << 3) | ((hi ^ 1u) << 2));
+    return make_uint2((c << 3) | (hi << 2) | high, (c << 3) | ((hi ^ 1u) << 2) | high);
 }
 __device__ __forceinline__ uint2 ttab_entry(uint32_t i) {  // i = x*32 + c
     const uint32_t t = c_T0.t[i >> 5], t2 = __builtin_amdgcn_alignbit(t, t, 16);
@@ -144,10 +146,10 @@ struct TLook {
     const uint2* ttab;
     uint2 lb;
     __device__ __forceinline__ uint32_t t0(uint32_t s, int k) const {
-        return lds_at<uint32_t>(ttab, perm(s, lb.x, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
+        return lds_at<uint32_t>(ttab, perm(s, lb.x, 0x0C020000u | ((4u + (uint32_t)k) << 8)));
     }
     __device__ __forceinline__ uint32_t t2(uint32_t s, int k) const {
-        return lds_at<uint32_t>(ttab, perm(s, lb.y, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
+        return lds_at<uint32_t>(ttab, perm(s, lb.y, 0x0C020000u | ((4u + (uint32_t)k) << 8)));
     }
     __device__ __forceinline__ uint32_t t1(uint32_t s, int k) const { return rotl8(t0(s, k)); }
     __device__ __forceinline__ uint32_t t3(uint32_t s, int k) const { return rotl8(t2(s, k)); }
@@ -413,6 +415,36 @@ __device__ __forceinline__ uint4 gf_mul_full(uint4 x, uint4 acc, const uint4* ft
             const uint4 e2 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 7 - 2 * k) * 256u + al[k]);
             acc = x34(acc, e1, e2);
         }
+    }
+    return acc;
+}
+
+// x · F with a byte-window table (the single-key kernel's GHASH, NEB_GHASH8): 16 lookups of
+// F8_P[b] = b·x^(8P)·H^4 instead of 32 nibble lookups. Entry b of position P sits at byte
+// b*256 + P*16 of f8, so position P owns banks 4P..4P+3. A ds_read_b128 is served in groups of 16
+// lanes whose lane & 15 are all different (MI355X_MICROARCH.md, LDS): lane f reads its byte
+// positions in the rotated order P = (f + j) mod 16, so at every step the 16 lanes of a group read
+// 16 different positions — 16 different bank groups — and no lookup conflicts whatever the data.
+// f = lane & 15; cw[w] byte t = ((f + 4w + t) & 15) << 4 (the bank-group byte of step 4w + t).
+__device__ __forceinline__ uint4 gf_mul_byte(uint4 x, const uint4* f8, uint32_t f, uint4 cw) {
+    // byte j of the little-endian 128-bit z is byte j of the block (GCM order), then rotate right
+    // by 8f bits: byte j of y = byte (f + j) mod 16 of the block
+    const uint32_t z0 = bswap32(x.x), z1 = bswap32(x.y), z2 = bswap32(x.z), z3 = bswap32(x.w);
+    const bool r1 = (f & 4u) != 0u, r2 = (f & 8u) != 0u;
+    const uint32_t a0 = r1 ? z1 : z0, a1 = r1 ? z2 : z1, a2 = r1 ? z3 : z2, a3 = r1 ? z0 : z3;
+    const uint32_t b0 = r2 ? a2 : a0, b1 = r2 ? a3 : a1, b2 = r2 ? a0 : a2, b3 = r2 ? a1 : a3;
+    const uint32_t sh = (f & 3u) << 3;
+    const uint32_t y[4] = {__builtin_amdgcn_alignbit(b1, b0, sh), __builtin_amdgcn_alignbit(b2, b1, sh),
+                           __builtin_amdgcn_alignbit(b3, b2, sh), __builtin_amdgcn_alignbit(b0, b3, sh)};
+    const uint32_t c[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+        // address = (byte t of y) << 8 | (byte t of c): one v_perm
+        const uint32_t t0 = (uint32_t)(j & 3), t1 = (uint32_t)((j + 1) & 3);
+        const uint4 e1 = lds_at<uint4>(f8, perm(y[j >> 2], c[j >> 2], 0x0C0C0000u | ((4u + t0) << 8) | t0));
+        const uint4 e2 = lds_at<uint4>(f8, perm(y[(j + 1) >> 2], c[(j + 1) >> 2], 0x0C0C0000u | ((4u + t1) << 8) | t1));
+        acc = x34(acc, e1, e2);
     }
     return acc;
 }
@@ -722,6 +754,17 @@ struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 
         return V;
     }
 };
+struct GhByte {  // one key per batch, LPP 4: byte-window table for H^4 (gf_mul_byte) + tables for H
+    static constexpr bool kBitslice = true;
+    const uint4* f8;
+    const uint4* shoup_h;  // the 8 position tables of H
+    uint32_t f;            // lane & 15
+    uint4 cw;              // bank-group bytes per step (gf_mul_byte)
+    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_byte(a, f8, f, cw); }
+    __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
+        return GhFull{nullptr, shoup_h}.final(A, lane, lg);
+    }
+};
 constexpr uint32_t kChunkTables = 5;  // Shoup tables H, H^2, H^4, H^8, H^16 (table i = H^(2^i))
 #ifndef NEB_CHUNK_POS
 #define NEB_CHUNK_POS 1  // 4-lane chunks multiply by H^4 with position tables (gf_mul_pos)
@@ -890,22 +933,60 @@ __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rk
 
 // ---- one tunnel key for the whole batch -------------------------------------------------------
 
+// Single-key GHASH on the byte-window table (gf_mul_byte: 16 conflict-free lookups per multiply
+// instead of 32); its 64 KiB leave room for the two-table AES only. Bit-exact (GPU parity suite)
+// and it cuts the kernel's LDS-array cycles 6%, but the seal time does not move (0.124 ms both,
+// profiles/r2_micro/ab_ghash8.log): with the LDS less loaded, the waves' own dependency chains at
+// 4 waves per SIMD set the pace. Off: the nibble table is simpler and as fast.
+#ifndef NEB_GHASH8
+#define NEB_GHASH8 0
+#endif
+#ifndef NEB_G8_LAYOUT
+#define NEB_G8_LAYOUT 0
+#endif
 #ifndef NEB_T4
+#if NEB_GHASH8
+#define NEB_T4 0
+#else
 #define NEB_T4 1  // single-key kernel on the four-table AES (TLook4); 0 = the two-table TLook
 #endif
+#endif
+#if NEB_GHASH8 && NEB_T4
+#error "NEB_GHASH8 needs the two-table AES (64 KiB byte-window table + 128 KiB T-tables exceed the LDS)"
+#endif
 #ifndef NEB_SINGLE_WAVES
-#if NEB_T4
-#define NEB_SINGLE_WAVES 16  // waves per workgroup (one workgroup per CU: 136 KiB of LDS)
+#if NEB_T4 || NEB_GHASH8
+#define NEB_SINGLE_WAVES 16  // waves per workgroup (one workgroup per CU: 136-138 KiB of LDS)
 #else
-#define NEB_SINGLE_WAVES 8   // waves per workgroup (2 workgroups per CU)
+#define NEB_SINGLE_WAVES 8   // waves per workgroup (2 workgroups per CU, 74 KiB each)
 #endif
 #endif
+static_assert(NEB_SINGLE_WAVES * 64 <= 1024, "workgroup size");
 #ifndef NEB_SINGLE_WPE
 #define NEB_SINGLE_WPE 4    // launch bound: waves per SIMD
 #endif
 constexpr int kSingleWaves = NEB_SINGLE_WAVES;
 constexpr int kSingleThreads = kSingleWaves * kWave;
 
+#if NEB_GHASH8 && NEB_G8_LAYOUT
+struct SingleLds {  // experiment: T-tables first, the byte table above 64 KiB
+    uint2 ttab[256 * 32];    // 64 KiB  T-table pairs, 32 copies
+    uint4 shoup_h[8 * 16];   // 2 KiB   position tables of H (the final quad Horner)
+    uint4 f8[256 * 16];      // 64 KiB  F8_P[b] for H^4: entry b of position P at b*16 + P
+};
+#elif NEB_GHASH8
+// shoup_h and f8 first: their lookups fold their base into the ds_read offset field; the T-tables
+// sit at byte 66 KiB, reached through bit 16 of the lane bases plus an offset of 2 KiB. f4: the
+// record's nibble table, copied in with coalesced loads to build f8 from (every workgroup reading
+// its entries scattered from global memory put 8 MB of requests on one 8 KiB: +23 µs per launch).
+struct SingleLds {
+    uint4 shoup_h[8 * 16];   // 2 KiB   position tables of H (the final quad Horner)
+    uint4 f8[256 * 16];      // 64 KiB  F8_P[b] for H^4: entry b of position P at b*16 + P
+    uint2 ttab[256 * 32];    // 64 KiB  T-table pairs, 32 copies
+    uint4 f4[32 * 16];       // 8 KiB   F_p[v] for H^4 (prologue only)
+};
+static_assert(NEB_SINGLE_POSH, "NEB_GHASH8 keeps the position-table final");
+#else
 struct SingleLds {
     uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
 #if NEB_SINGLE_POSH
@@ -919,6 +1000,7 @@ struct SingleLds {
     uint2 ttab[256 * 32];    // 64 KiB T-table pairs, 32 copies
 #endif
 };
+#endif
 
 template <bool OPEN>
 __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_kernel(GcmArgs args) {
@@ -927,14 +1009,39 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
-#if NEB_T4
+#if NEB_GHASH8
+#if NEB_G8_LAYOUT
+    const TLook T{lds.ttab, ttab_lane_base(lane)};
+#else
+    static_assert(offsetof(SingleLds, ttab) == 65536u + 2048u, "T-table base: bit 16 + offset field");
+    const TLook T{reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(&lds) + 2048), ttab_lane_base(lane, 1u << 16)};
+#endif
+    for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
+    // F8_P[b] = F4_2P[b >> 4] ^ F4_2P+1[b & 15] from the record's nibble table (layout.hpp)
+#if NEB_G8_LAYOUT
+    for (uint32_t i = tid; i < 256u * 16u; i += kSingleThreads) {
+        const uint32_t b = i >> 4, P = i & 15u;
+        lds.f8[i] = xor4(ld_rec4(srec, kRecFull + 4u * ((2u * P) * 16u + (b >> 4))),
+                         ld_rec4(srec, kRecFull + 4u * ((2u * P + 1u) * 16u + (b & 15u))));
+    }
+#else
+    if (tid < 512u) lds.f4[tid] = ld_rec4(srec, kRecFull + 4u * tid);
+    __syncthreads();
+    for (uint32_t i = tid; i < 256u * 16u; i += kSingleThreads) {
+        const uint32_t b = i >> 4, P = i & 15u;
+        lds.f8[i] = xor4(lds.f4[(2u * P) * 16u + (b >> 4)], lds.f4[(2u * P + 1u) * 16u + (b & 15u)]);
+    }
+#endif
+#elif NEB_T4
     const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
     for (uint32_t i = tid; i < 2u * 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab4_entry(i);
 #else
     const TLook T{lds.ttab, ttab_lane_base(lane)};
     for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
 #endif
+#if !NEB_GHASH8
     for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull + 4u * i);
+#endif
 #if NEB_SINGLE_POSH
     if (tid < 128u) lds.shoup_h[tid] = ld_rec4(srec, kRecPos1 + 4u * tid);
 #else
@@ -944,7 +1051,23 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     load_round_keys(srec, rks);
     __syncthreads();
     const RkRegs rk{rks};
+#if NEB_GHASH8
+    const uint32_t f = lane & 15u;
+    uint4 cw;
+    {
+        uint32_t c[4];
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            c[w] = 0;
+#pragma unroll
+            for (int t = 0; t < 4; t++) c[w] |= ((f + 4u * w + t) & 15u) << (4 + 8 * t);
+        }
+        cw = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+    const GhByte gh{lds.f8, lds.shoup_h, f, cw};
+#else
     const GhFull gh{lds.full, lds.shoup_h};
+#endif
 
     // The slot must still hold an AES-GCM key when the batch runs (a key destroyed, or its slot
     // reused by another algorithm, while the batch was queued): every packet gets BAD_KEY then.
