@@ -853,7 +853,7 @@ static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, c
                         d_pk_status, d_nwires, s));
     HIP_TRY(neb_tx_segment(d_pk, npk, d_in, d_tun, d_out, &tx.ws, d_wires, d_nwires, max_wires, e->cu_count, s));
     HIP_TRY(launch_batch(e, alg, 0, tx.ws.seal_desc, max_wires, d_out, d_wire_status, key_hint, s, d_nwires));
-    HIP_TRY(neb_tx_finish(d_tun, ntun, &tx.ws, s));
+    HIP_TRY(neb_tx_finish(d_tun, npk, ntun, &tx.ws, s));
     HIP_TRY(hipEventRecord(tx.done, s));
     return NEB_OK;
 }

@@ -39,21 +39,32 @@ __device__ __forceinline__ uint32_t fold2(uint32_t s) {
     return (s & 0xFFFFu) + (s >> 16);
 }
 // checksum.Checksum(p[lo:hi], 0): big-endian words paired from lo, odd tail byte high, folded
+// (headers are at most 120 bytes: 8 loads in flight per step instead of one dependent load a byte)
 __device__ uint32_t csum_range(const uint8_t* p, uint32_t lo, uint32_t hi) {
-    uint32_t s = 0;
-    for (uint32_t k = lo; k < hi; k++) s += ((k - lo) & 1u) ? (uint32_t)p[k] : (uint32_t)p[k] << 8;
+    uint32_t s = 0, k = lo;
+    for (; k + 8u <= hi; k += 8u) {
+        uint32_t b[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) b[q] = p[k + q];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q += 2) s += (b[q] << 8) | b[q + 1];  // k - lo is even here
+    }
+    for (; k < hi; k++) s += ((k - lo) & 1u) ? (uint32_t)p[k] : (uint32_t)p[k] << 8;
     while (s >> 16) s = (s & 0xFFFFu) + (s >> 16);
     return s;
 }
 
 // ---- stage 1: per-packet checks and sizes ---------------------------------------------------
 
-__global__ void tx_parse_kernel(const neb_tx_packet* __restrict__ pk, uint32_t n, const uint8_t* __restrict__ in,
-                                const neb_tx_tunnel* __restrict__ tun, uint32_t ntun, const uint32_t* __restrict__ keys,
-                                uint32_t max_keys, int alg, TxWs ws, int32_t* __restrict__ pk_status) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const neb_tx_packet P = pk[i];
+struct TxParsed {
+    TxPlan plan;
+    int32_t st;
+    uint64_t scan;  // nseg << 40 | output bytes
+};
+
+__device__ TxParsed tx_parse_one(const neb_tx_packet& P, const uint8_t* __restrict__ in,
+                                 const neb_tx_tunnel* __restrict__ tun, uint32_t ntun,
+                                 const uint32_t* __restrict__ keys, uint32_t max_keys, int alg) {
     TxPlan plan{};
     int32_t st = NEB_STATUS_OK;
     const uint8_t* b = in + P.in_off;
@@ -157,11 +168,21 @@ __global__ void tx_parse_kernel(const neb_tx_packet* __restrict__ pk, uint32_t n
     } else {
         plan.nseg = 0;
     }
-    ws.plan[i] = plan;
-    ws.scan_in[i] = ((uint64_t)plan.nseg << 40) | bytes;
-    ws.tun_key[i] = st == NEB_STATUS_OK ? P.tunnel : ntun;
+    return TxParsed{plan, st, ((uint64_t)plan.nseg << 40) | bytes};
+}
+
+__global__ void tx_parse_kernel(const neb_tx_packet* __restrict__ pk, uint32_t n, const uint8_t* __restrict__ in,
+                                const neb_tx_tunnel* __restrict__ tun, uint32_t ntun, const uint32_t* __restrict__ keys,
+                                uint32_t max_keys, int alg, TxWs ws, int32_t* __restrict__ pk_status) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const neb_tx_packet P = pk[i];
+    const TxParsed r = tx_parse_one(P, in, tun, ntun, keys, max_keys, alg);
+    ws.plan[i] = r.plan;
+    ws.scan_in[i] = r.scan;
+    ws.tun_key[i] = r.st == NEB_STATUS_OK ? P.tunnel : ntun;
     ws.idx[i] = i;
-    pk_status[i] = st;
+    pk_status[i] = r.st;
 }
 
 // wire -> packet map of the fitting prefix, one wave per packet
@@ -180,16 +201,18 @@ __global__ void tx_gather_kernel(uint32_t n, TxWs ws) {
 }
 
 // Counter offsets back in batch order; the fitting prefix; per-tunnel totals; the batch totals.
-__global__ void tx_scatter_kernel(uint32_t n, uint32_t ntun, uint64_t out_cap, uint32_t max_wires, TxWs ws,
-                                  int32_t* __restrict__ pk_status, uint32_t* __restrict__ d_nwires) {
+__global__ void tx_scatter_kernel(uint32_t n, const neb_tx_tunnel* __restrict__ tun, uint32_t ntun, uint64_t out_cap,
+                                  uint32_t max_wires, TxWs ws, int32_t* __restrict__ pk_status,
+                                  uint32_t* __restrict__ d_nwires) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t p = ws.idx_sorted[i];
-    ws.ctr_off[p] = ws.ctr_sorted[i];
     const uint64_t pre = ws.scan_out[p], own = ws.scan_in[p];
     const uint64_t end_seg = (pre >> 40) + (own >> 40);
     const uint64_t end_bytes = (pre & kTxBytesMask) + (own & kTxBytesMask);
     const uint32_t t = ws.tun_key_sorted[i];
+    // tx_finish_kernel advances the counters only after the segment kernel has run
+    ws.ctr_base[p] = (t < ntun ? tun[t].message_counter : 0ull) + ws.ctr_sorted[i];
     const bool fits = end_seg <= max_wires && end_bytes <= out_cap;
     if (t < ntun) {
         if (fits) {
@@ -227,6 +250,165 @@ __global__ void tx_scatter_kernel(uint32_t n, uint32_t ntun, uint64_t out_cap, u
         ws.totals[0] = seg;
         ws.totals[1] = byt;
     }
+}
+
+// ---- the whole plan in one workgroup (n <= kTxPlanSmallMax) ----------------------------------
+//
+// Same results as parse + scan + sort + scan-by-key + scatter + finish above, in one launch:
+// at the batch sizes a TUN queue flush has (hundreds to a few thousand reads) those twelve launches
+// cost ~60 us of which almost all is launch and drain. Thread t owns packets 8t..8t+7 (blocked, in
+// batch order), so block-wide scans and a stable block radix sort by tunnel give batch-order
+// prefixes and per-tunnel counters; the tunnels' counters advance here, after every read of them.
+// The wire -> packet map stays a grid-wide launch (tx_segmap_kernel): 65 Ki uncoalesced 4-byte
+// stores from one CU took 31 us (a merge-path split over the workgroup's threads, measured).
+
+#ifdef NEB_TX_PLAN_PROF
+#define TXPROF(x) __syncthreads(); const unsigned long long x = wall_clock64()
+#else
+#define TXPROF(x)
+#endif
+
+struct TxSegPair {  // segmented-sum element: head = a tunnel's run starts inside
+    uint32_t head, sum;
+};
+struct TxSegOp {
+    __device__ TxSegPair operator()(const TxSegPair& a, const TxSegPair& b) const {
+        return TxSegPair{a.head | b.head, b.head ? b.sum : a.sum + b.sum};
+    }
+};
+
+template <uint32_t IT>
+__global__ __launch_bounds__(kTxPlanThreads) void tx_plan_small_kernel(
+    const neb_tx_packet* __restrict__ pk, uint32_t n, const uint8_t* __restrict__ in, neb_tx_tunnel* __restrict__ tun,
+    uint32_t ntun, const uint32_t* __restrict__ keys, uint32_t max_keys, int alg, uint64_t out_cap, uint32_t max_wires,
+    int key_bits, TxWs ws, int32_t* __restrict__ pk_status, uint32_t* __restrict__ d_nwires) {
+    static_assert(IT <= kTxPlanItems, "the LDS arrays hold kTxPlanSmallMax reads");
+    using Sort = hipcub::BlockRadixSort<uint32_t, kTxPlanThreads, IT, uint32_t>;
+    using Scan64 = hipcub::BlockScan<uint64_t, kTxPlanThreads>;
+    using ScanSeg = hipcub::BlockScan<TxSegPair, kTxPlanThreads>;
+    using Reduce = hipcub::BlockReduce<uint32_t, kTxPlanThreads>;
+    __shared__ union {
+        typename Sort::TempStorage sort;
+        typename Scan64::TempStorage scan;
+        typename ScanSeg::TempStorage seg;
+        typename Reduce::TempStorage red;
+    } tmp;
+    __shared__ uint32_t s_end[kTxPlanSmallMax];   // per packet: output bytes (parse -> blocked)
+    __shared__ uint32_t s_nseg[kTxPlanSmallMax];  // per packet: its segments
+    __shared__ uint32_t s_key[kTxPlanSmallMax];   // the sorted tunnel keys
+    __shared__ uint32_t s_fit;
+
+    const uint32_t t = threadIdx.x;
+    uint64_t sc[IT];
+    uint32_t key[IT], idx[IT];
+    TXPROF(T0);
+    // 1. parse (tx_parse_kernel), packets striped over the threads; then each thread takes its
+    // blocked 8 through the LDS (the output bytes of one read fit 32 bits: at most 65535 segments of
+    // at most 160 bytes)
+    for (uint32_t i = t; i < n; i += kTxPlanThreads) {
+        const neb_tx_packet P = pk[i];
+        const TxParsed r = tx_parse_one(P, in, tun, ntun, keys, max_keys, alg);
+        ws.plan[i] = r.plan;
+        pk_status[i] = r.st;
+        s_nseg[i] = r.plan.nseg;
+        s_end[i] = (uint32_t)(r.scan & kTxBytesMask);
+        s_key[i] = r.st == NEB_STATUS_OK ? P.tunnel : ntun;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t i = t * IT + k;
+        sc[k] = 0;
+        key[k] = ntun;
+        idx[k] = i;
+        if (i < n) {
+            sc[k] = ((uint64_t)s_nseg[i] << 40) | s_end[i];
+            key[k] = s_key[i];
+        }
+    }
+    __syncthreads();
+    TXPROF(T1);
+    // 2. batch-order exclusive prefix of (segments, bytes); the fitting prefix
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) tot += sc[k];
+    uint64_t pre;
+    Scan64(tmp.scan).ExclusiveSum(tot, pre);
+    uint32_t nfit = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t i = t * IT + k;
+        const uint64_t end = pre + sc[k];
+        const bool fits = (end >> 40) <= max_wires && (end & kTxBytesMask) <= out_cap;
+        if (i < n) {
+            ws.scan_out[i] = pre;
+            ws.scan_in[i] = sc[k];
+            if (!fits && key[k] < ntun) pk_status[i] = NEB_STATUS_NO_SPACE;  // outside the fitting prefix
+            nfit += fits;
+        }
+        if (!fits) key[k] = ntun;  // takes no counters
+        pre = end;
+    }
+    __syncthreads();
+    const uint32_t F = Reduce(tmp.red).Sum(nfit);  // prefixes are monotone: packets 0..F-1 fit
+    if (t == 0) s_fit = F;
+    __syncthreads();
+    const uint32_t fit = s_fit;
+    if (t == 0) {
+        const uint64_t e = fit ? ws.scan_out[fit - 1u] + ws.scan_in[fit - 1u] : 0ull;
+        *d_nwires = (uint32_t)(e >> 40);
+        ws.totals[0] = e >> 40;
+        ws.totals[1] = e & kTxBytesMask;
+    }
+    TXPROF(T2);
+    // 3. counters: a stable sort by tunnel keeps batch order inside each tunnel's run
+    __syncthreads();
+    Sort(tmp.sort).Sort(key, idx, 0, key_bits);
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) s_key[t * IT + k] = key[k];
+    __syncthreads();
+    uint32_t val[IT], head[IT];
+    TxSegPair agg{0u, 0u};
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t r = t * IT + k;
+        val[k] = key[k] < ntun ? s_nseg[idx[k]] : 0u;
+        head[k] = r == 0u || s_key[r - 1u] != key[k];
+        agg = TxSegOp{}(agg, TxSegPair{head[k], val[k]});
+    }
+    TXPROF(T3);
+    TxSegPair carry;
+    ScanSeg(tmp.seg).ExclusiveScan(agg, carry, TxSegPair{0u, 0u}, TxSegOp{});
+    uint32_t run = carry.sum;
+    uint64_t newctr[IT];
+    bool last[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t r = t * IT + k;
+        if (head[k]) run = 0;
+        last[k] = false;
+        if (key[k] < ntun) {
+            const uint64_t base = tun[key[k]].message_counter;
+            ws.ctr_base[idx[k]] = base + run;
+            last[k] = r + 1u == kTxPlanThreads * IT || s_key[r + 1u] != key[k];
+            newctr[k] = base + run + val[k];
+        }
+        run += val[k];
+    }
+    TXPROF(T4);
+    __syncthreads();  // every read of the old counters is done
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++)
+        if (last[k]) tun[key[k]].message_counter = newctr[k];
+    TXPROF(T5);
+    TXPROF(T6);
+#ifdef NEB_TX_PLAN_PROF
+    __syncthreads();
+    TXPROF(T7);
+    if (t == 0)
+        printf("txplan n=%u parse %llu prefix %llu sort %llu segscan %llu ctr %llu - %llu sync %llu (x10ns)\n", n,
+               T1 - T0, T2 - T1, T3 - T2, T4 - T3, T5 - T4, T6 - T5, T7 - T6);
+#endif
 }
 
 // ---- stage 3: one wave per segment ----------------------------------------------------------
@@ -325,14 +507,14 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
         TxPlan plan{};
         neb_tx_packet P{};
         neb_tx_tunnel T{};
-        uint32_t ctr_off = 0;
+        uint64_t ctr_base = 0;
         if (live) {
             plan = ws.plan[p];
             P = pk[p];
-            ctr_off = ws.ctr_off[p];
+            ctr_base = ws.ctr_base[p];
         }
         if (live) T = tun[P.tunnel];
-        const uint64_t counter = T.message_counter + ctr_off + j + 1u;
+        const uint64_t counter = ctr_base + j + 1u;
         const uint64_t slot = (pre & kTxBytesMask) + (uint64_t)j * plan.full_slot;
         const uint8_t* src = in + P.in_off;
         const uint32_t hl = plan.hdr_len, cs = P.csum_start, co = P.csum_offset;
@@ -525,10 +707,28 @@ extern "C" size_t neb_tx_ws_bytes(uint32_t n, uint32_t ntun, uint32_t max_wires,
     return neb::tx_ws_layout(n, ntun, max_wires, *cub_bytes, nullptr, nullptr);
 }
 
+#ifndef NEB_TX_SMALL_PLAN
+#define NEB_TX_SMALL_PLAN 1
+#endif
+
 extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const uint8_t* d_in,
-                                  const neb_tx_tunnel* d_tun, uint32_t ntun, const uint32_t* d_keys, uint32_t max_keys,
+                                  neb_tx_tunnel* d_tun, uint32_t ntun, const uint32_t* d_keys, uint32_t max_keys,
                                   int alg, const neb::TxWs* ws, uint64_t out_cap, uint32_t max_wires,
                                   int32_t* d_pk_status, uint32_t* d_nwires, hipStream_t s) {
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) <= ntun) bits++;
+    if (NEB_TX_SMALL_PLAN && n <= neb::kTxPlanSmallMax) {
+        // the block sort and scans cost by items per thread: 2 up to 2048 reads
+        if (n <= 2u * neb::kTxPlanThreads)
+            hipLaunchKernelGGL(neb::tx_plan_small_kernel<2>, dim3(1), dim3(neb::kTxPlanThreads), 0, s, d_pk, n, d_in,
+                               d_tun, ntun, d_keys, max_keys, alg, out_cap, max_wires, bits, *ws, d_pk_status, d_nwires);
+        else
+            hipLaunchKernelGGL(neb::tx_plan_small_kernel<neb::kTxPlanItems>, dim3(1), dim3(neb::kTxPlanThreads), 0, s,
+                               d_pk, n, d_in, d_tun, ntun, d_keys, max_keys, alg, out_cap, max_wires, bits, *ws,
+                               d_pk_status, d_nwires);
+        hipLaunchKernelGGL(neb::tx_segmap_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, max_wires, out_cap, *ws);
+        return hipGetLastError();
+    }
     const uint32_t tpb = 256, grid = (n + tpb - 1) / tpb;
     hipError_t e = hipMemsetAsync(ws->tun_total, 0, (size_t)ntun * sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
@@ -537,8 +737,6 @@ extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const u
     size_t cb = ws->cub_bytes;
     e = hipcub::DeviceScan::ExclusiveSum(ws->cub_tmp, cb, ws->scan_in, ws->scan_out, (int)n, s);
     if (e != hipSuccess) return e;
-    int bits = 1;
-    while (bits < 32 && (1ull << bits) <= ntun) bits++;
     cb = ws->cub_bytes;
     e = hipcub::DeviceRadixSort::SortPairs(ws->cub_tmp, cb, ws->tun_key, ws->tun_key_sorted, ws->idx, ws->idx_sorted,
                                            (int)n, 0, bits, s);
@@ -548,7 +746,7 @@ extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const u
     e = hipcub::DeviceScan::ExclusiveSumByKey(ws->cub_tmp, cb, ws->tun_key_sorted, ws->nseg_sorted, ws->ctr_sorted,
                                               (int)n, hipcub::Equality(), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(neb::tx_scatter_kernel, dim3(grid), dim3(tpb), 0, s, n, ntun, out_cap, max_wires, *ws,
+    hipLaunchKernelGGL(neb::tx_scatter_kernel, dim3(grid), dim3(tpb), 0, s, n, d_tun, ntun, out_cap, max_wires, *ws,
                        d_pk_status, d_nwires);
     hipLaunchKernelGGL(neb::tx_segmap_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, max_wires, out_cap, *ws);
     return hipGetLastError();
@@ -569,8 +767,9 @@ extern "C" hipError_t neb_tx_segment(const neb_tx_packet* d_pk, uint32_t n, cons
     return hipGetLastError();
 }
 
-extern "C" hipError_t neb_tx_finish(neb_tx_tunnel* d_tun, uint32_t ntun, const neb::TxWs* ws, hipStream_t s) {
-    if (ntun == 0) return hipSuccess;
+extern "C" hipError_t neb_tx_finish(neb_tx_tunnel* d_tun, uint32_t n, uint32_t ntun, const neb::TxWs* ws,
+                                    hipStream_t s) {
+    if (ntun == 0 || (NEB_TX_SMALL_PLAN && n <= neb::kTxPlanSmallMax)) return hipSuccess;  // done by the plan kernel
     hipLaunchKernelGGL(neb::tx_finish_kernel, dim3((ntun + 255) / 256), dim3(256), 0, s, d_tun, ntun, *ws);
     return hipGetLastError();
 }

@@ -9,6 +9,10 @@ namespace neb {
 
 constexpr uint32_t kTxMaxHdr = 120;  // IPv4 max IHL 60 + TCP max data offset 60 (segment_linux.go:30-32)
 constexpr uint64_t kTxBytesMask = (1ull << 40) - 1;  // scan word: segments << 40 | output bytes
+// Batches of at most this many TUN reads are planned by one workgroup in one launch
+// (tx_plan_small_kernel) instead of the 12-launch device-wide path.
+constexpr uint32_t kTxPlanThreads = 1024, kTxPlanItems = 8;
+constexpr uint32_t kTxPlanSmallMax = kTxPlanThreads * kTxPlanItems;
 
 enum : uint8_t { kTxPass = 0, kTxFinish = 1, kTxTcp = 2, kTxUdp = 3 };
 
@@ -34,7 +38,8 @@ struct TxWs {
     uint32_t* idx_sorted;
     uint32_t* nseg_sorted;
     uint32_t* ctr_sorted;
-    uint32_t* ctr_off;           // per packet: segments of its tunnel earlier in the batch
+    uint64_t* ctr_base;          // per packet: its tunnel's message counter + the segments of that tunnel
+                                 // earlier in the batch (the counter of segment j is ctr_base + j + 1)
     uint32_t* seg_pkt;           // per wire: its packet
     unsigned long long* tun_total;  // per tunnel: segments in this batch
     unsigned long long* totals;     // [0] segments, [1] bytes of the fitting prefix
@@ -63,7 +68,7 @@ inline size_t tx_ws_layout(uint32_t n, uint32_t ntun, uint32_t max_wires, size_t
     w.idx_sorted = (uint32_t*)take((size_t)n * 4);
     w.nseg_sorted = (uint32_t*)take((size_t)n * 4);
     w.ctr_sorted = (uint32_t*)take((size_t)n * 4);
-    w.ctr_off = (uint32_t*)take((size_t)n * 4);
+    w.ctr_base = (uint64_t*)take((size_t)n * 8);
     w.tun_total = (unsigned long long*)take((size_t)(ntun ? ntun : 1) * 8);
     w.totals = (unsigned long long*)take(16);
     w.seal_desc = (neb_desc*)take((size_t)(max_wires ? max_wires : 1) * sizeof(neb_desc));
@@ -77,12 +82,15 @@ inline size_t tx_ws_layout(uint32_t n, uint32_t ntun, uint32_t max_wires, size_t
 }  // namespace neb
 
 extern "C" size_t neb_tx_ws_bytes(uint32_t n, uint32_t ntun, uint32_t max_wires, size_t* cub_bytes);
+// Plans the batch; for n <= kTxPlanSmallMax it also advances the tunnels' message counters
+// (neb_tx_finish is then a no-op to skip).
 extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const uint8_t* d_in,
-                                  const neb_tx_tunnel* d_tun, uint32_t ntun, const uint32_t* d_keys, uint32_t max_keys,
+                                  neb_tx_tunnel* d_tun, uint32_t ntun, const uint32_t* d_keys, uint32_t max_keys,
                                   int alg, const neb::TxWs* ws, uint64_t out_cap, uint32_t max_wires,
                                   int32_t* d_pk_status, uint32_t* d_nwires, hipStream_t s);
 extern "C" hipError_t neb_tx_segment(const neb_tx_packet* d_pk, uint32_t n, const uint8_t* d_in,
                                      const neb_tx_tunnel* d_tun, uint8_t* d_out, const neb::TxWs* ws,
                                      neb_tx_wire* d_wires, const uint32_t* d_nwires, uint32_t max_wires, int cu_count,
                                      hipStream_t s);
-extern "C" hipError_t neb_tx_finish(neb_tx_tunnel* d_tun, uint32_t ntun, const neb::TxWs* ws, hipStream_t s);
+extern "C" hipError_t neb_tx_finish(neb_tx_tunnel* d_tun, uint32_t n, uint32_t ntun, const neb::TxWs* ws,
+                                    hipStream_t s);

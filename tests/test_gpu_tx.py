@@ -181,3 +181,24 @@ def test_tx_batch_random_superpackets(engine, oracle_mod):
             d, _, cs = build_udpv6_super(pay)
             P.append(_pk(d, rng.randrange(8), 1, S.GSO_UDP_L4, rng.choice([333, 1452]), cs, 6))
     _check(engine, oracle_mod, L.ALG_AESGCM, P, _tunnels(rng, n=8, keyless=()), out_cap=8 << 20, max_wires=8192)
+
+
+@pytest.mark.parametrize("cut", [False, True])
+def test_tx_batch_large_plan_path(engine, oracle_mod, cut):
+    """More TUN reads than one workgroup plans (kTxPlanSmallMax = 8192): the device-wide planning
+    path (hipCUB scan, radix sort, scan-by-key) and its counter update after the seal, with keyless
+    tunnels, invalid reads and, with `cut`, an output that keeps only a prefix."""
+    import segment_oracle as S
+
+    rng = random.Random(21 + cut)
+    P = []
+    for i in range(8300):
+        if i % 997 == 5:
+            d, _, cs = build_tcpv4_super(rng.choice([3000, 9000]))
+            P.append(_pk(d, rng.randrange(16), 1, S.GSO_TCPV4, 1448, cs, 16))
+        elif i % 331 == 7:
+            P.append(_pk(b"", rng.randrange(16)))  # short tun read
+        else:
+            P.append(_pk(bytes(rng.getrandbits(8) for _ in range(rng.randrange(20, 90))), rng.randrange(17)))
+    tun = _tunnels(rng, n=16, keyless=(5,))
+    _check(engine, oracle_mod, L.ALG_AESGCM, P, tun, out_cap=(600_000 if cut else 4 << 20), max_wires=16384)
