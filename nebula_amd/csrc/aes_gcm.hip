@@ -550,6 +550,9 @@ struct GcmArgs {
     uint32_t key_hint;     // SINGLE: the one key_id
     int32_t* status;
     const uint32_t* npkt_dev;  // optional: the batch's packet count in device memory (min with npkt)
+    // TX batches only (tx.hip): a descriptor's first `flags` plaintext bytes are read from its
+    // destination (the patched header image), the rest from src (the TUN read itself)
+    uint32_t hdr_from_dst;
 };
 
 struct PktShape {
@@ -585,7 +588,9 @@ __device__ __forceinline__ LaneBlock lane_block(const PktShape& sh, uint32_t r, 
 }
 
 // Input block of lane block b: the AAD block or the payload block (zero-padded), else zero.
-__device__ __forceinline__ uint4 gcm_lane_load(const neb_desc& d, const LaneBlock& b, const uint8_t* arena) {
+// hdr: plaintext bytes [0, hdr) come from the destination (GcmArgs::hdr_from_dst).
+__device__ __forceinline__ uint4 gcm_lane_load(const neb_desc& d, const LaneBlock& b, const uint8_t* arena,
+                                               uint32_t hdr) {
     uint4 in = make_uint4(0, 0, 0, 0);
     if (b.is_aad) {
         const uint32_t off = 16u * (uint32_t)(b.g - 1);
@@ -593,7 +598,9 @@ __device__ __forceinline__ uint4 gcm_lane_load(const neb_desc& d, const LaneBloc
     }
     if (b.is_ct) {
         const uint32_t off = 16u * (b.k - 1u);
-        in = load_block(arena + d.src_off + off, min(16u, d.len - off));
+        const uint32_t nb = min(16u, d.len - off);
+        in = off < hdr ? load_block_hdr(arena + d.dst_off + off, arena + d.src_off + off, nb, hdr - off)
+                       : load_block(arena + d.src_off + off, nb);
     }
     return in;
 }
@@ -807,6 +814,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
     if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
     const bool run = valid && st == NEB_STATUS_OK;
+    const uint32_t hdr = args.hdr_from_dst ? d.flags : 0u;
     PktShape sh;
     sh.na = (d.aad_len + 15u) >> 4;
     sh.m = (d.len + 15u) >> 4;
@@ -828,20 +836,23 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         // round r's payload XOR and GHASH fold, given G = A·H^LPP (the rounds before) and the keystream
         auto io = [&](const LaneBlock& b, uint4 G, uint4 ks) {
 #ifndef NEB_NO_FASTIO
-            // the common round: every active lane holds a full, 16-B aligned payload block
-            // (the arena base counts too: a caller may pass an arena at any byte address)
+            // the common round: every active lane holds a full payload block with a 16-B aligned
+            // destination (the arena base counts too: a caller may pass an arena at any byte
+            // address); a source off 16-B alignment (a TX segment inside its TUN read) is read as
+            // two aligned blocks and shifted
             const uint32_t off = 16u * (b.k - 1u);
-            const bool full = b.is_ct && off + 16u <= d.len &&
-                              ((d.src_off | d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u;
+            const bool full = b.is_ct && off + 16u <= d.len && off >= hdr &&
+                              ((d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u;
             if (__all(full)) {
-                const uint4 in = *reinterpret_cast<const uint4*>(args.arena + d.src_off + off);
+                const uint8_t* sp = args.arena + d.src_off + off;
+                const uint4 in = __all(((uint32_t)(uintptr_t)sp & 3u) == 0u) ? load_u4_a4(sp) : load_shifted16(sp);
                 const uint4 out = xor4(in, ks);
                 *reinterpret_cast<uint4*>(args.arena + d.dst_off + off) = out;
                 A = xor4(G, bswap4(OPEN ? in : out));
                 return;
             }
 #endif
-            const uint4 in = gcm_lane_load(d, b, args.arena);
+            const uint4 in = gcm_lane_load(d, b, args.arena, hdr);
             A = xor4(G, gcm_lane_io<OPEN>(d, b, in, ks, args.arena, ej0));
         };
         auto horner = [&](uint32_t r) -> uint4 {
@@ -1187,7 +1198,9 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
     // waves that drew short chunks draw again (longest first: front, then back). Every wave
     // pulling its first chunk off one atomic word at launch would serialise ~4096 dequeues at
     // ≈88/µs (MI355X_MICROARCH.md, dequeue).
+#if NEB_CHUNK_STATIC != 2
     const uint32_t nwaves = gridDim.x * kChunkWaves;
+#endif
 #if NEB_CHUNK_STATIC == 2
     // workgroup w owns chunks w, w + G, w + 2G, ... (G workgroups; longest first); its waves draw
     // them from an LDS cursor, one chunk ahead, so the next descriptor is in flight meanwhile
@@ -1432,8 +1445,9 @@ static hipError_t launch_grid(K kern, int threads, uint32_t work_waves, int cu_c
 // One tunnel key (key_hint) for every descriptor.
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                           int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n};
+                                           int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
+                                           int hdr_from_dst) {
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
     return open ? launch_grid(neb::gcm_single_kernel<true>, neb::kSingleThreads, groups, cu_count, s, a)
                 : launch_grid(neb::gcm_single_kernel<false>, neb::kSingleThreads, groups, cu_count, s, a);
@@ -1444,8 +1458,8 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, int cu_count,
-                                            hipStream_t s) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr};
+                                            hipStream_t s, int hdr_from_dst) {
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst};
     neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks};
     // one wave per chunk up to the occupancy cap (tails make chunks outnumber n / 16); the chunk
     // count is only known on the device: workgroups past it exit before filling their tables

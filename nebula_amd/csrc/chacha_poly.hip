@@ -231,6 +231,7 @@ struct ChachaArgs {
     uint32_t key_hint;
     int32_t* status;
     const uint32_t* npkt_dev;  // optional: the batch's packet count in device memory (min with npkt)
+    uint32_t hdr_from_dst;     // TX batches: the first `flags` plaintext bytes from dst (GcmArgs)
 };
 
 template <bool OPEN>
@@ -313,7 +314,9 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
             } else if (i < (int32_t)(na + m)) {
                 uint32_t off = 16u * ((uint32_t)i - na);
                 uint32_t nb = min(16u, d.len - off);
-                uint4 in = load_block(arena + d.src_off + off, nb);
+                const uint32_t hdr = args.hdr_from_dst ? d.flags : 0u;
+                uint4 in = off < hdr ? load_block_hdr(arena + d.dst_off + off, arena + d.src_off + off, nb, hdr - off)
+                                     : load_block(arena + d.src_off + off, nb);
                 uint4 out = xor4c(in, mask_block(ks, nb));
                 store_block(arena + d.dst_off + off, out, nb);
                 uint4 c = OPEN ? in : out;
@@ -388,7 +391,8 @@ static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStrea
 
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                       int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s) {
-    neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n};
+                                       int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
+                                       int hdr_from_dst) {
+    neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst};
     return open ? launch_chacha<true>(a, cu_count, s) : launch_chacha<false>(a, cu_count, s);
 }

@@ -72,6 +72,33 @@ __device__ __forceinline__ void store_block(uint8_t* p, uint4 v, uint32_t n) {
     }
 }
 
+// 16 bytes at a 4-byte aligned address: one global_load_dwordx4 (gfx950 needs dword alignment only)
+struct alignas(4) U4a4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ uint4 load_u4_a4(const uint8_t* p) {
+    const U4a4 v = *reinterpret_cast<const U4a4*>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// 16 bytes at any byte address p from the two aligned 16-byte blocks that hold them (never beyond
+// the aligned block of the last byte read, so never into another page).
+__device__ __forceinline__ uint4 load_shifted16(const uint8_t* p) {
+    const uint32_t s = (uint32_t)reinterpret_cast<uintptr_t>(p) & 15u;
+    const uint4* a = reinterpret_cast<const uint4*>(p - s);
+    const uint4 lo = a[0];
+    uint4 hi = make_uint4(0, 0, 0, 0);
+    if (s) hi = a[1];
+    const uint32_t q = s >> 2, r = 8u * (s & 3u);
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t t[5];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++)
+        t[k] = q == 0u ? w[k] : q == 1u ? w[k + 1] : q == 2u ? w[k + 2] : w[k + 3];
+    return make_uint4(__builtin_amdgcn_alignbit(t[1], t[0], r), __builtin_amdgcn_alignbit(t[2], t[1], r),
+                      __builtin_amdgcn_alignbit(t[3], t[2], r), __builtin_amdgcn_alignbit(t[4], t[3], r));
+}
+
 // Keep the first n bytes (0..16) of a little-endian block, zero the rest.
 __device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t n) {
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -82,6 +109,16 @@ __device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t n) {
         w[i] &= m;
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Block of n bytes (1..16) whose first h bytes come from hp and the rest from sp (the TX seal's
+// plaintext: the patched L3/L4 header image in the output slot, the payload in the TUN read).
+__device__ __forceinline__ uint4 load_block_hdr(const uint8_t* hp, const uint8_t* sp, uint32_t n, uint32_t h) {
+    if (h >= n) return load_block(hp, n);
+    const uint4 a = load_block(hp, h);
+    const uint4 b = load_block(sp, n);
+    const uint4 bh = mask_block(b, h);
+    return make_uint4(a.x | (b.x ^ bh.x), a.y | (b.y ^ bh.y), a.z | (b.z ^ bh.z), a.w | (b.w ^ bh.w));
 }
 
 }  // namespace neb

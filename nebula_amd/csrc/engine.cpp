@@ -21,17 +21,19 @@
 extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                           int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s);
+                                           int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
+                                           int hdr_from_dst);
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, int cu_count,
-                                            hipStream_t s);
+                                            hipStream_t s, int hdr_from_dst);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
-                                       int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s);
+                                       int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
+                                       int hdr_from_dst);
 
 // Device workspace of the mixed-key scheduler (sched.hpp). One per engine; a batch waits on the
 // previous user's event before reusing it, so batches on different streams never overlap in it.
@@ -483,14 +485,15 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
 }
 
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
-// only known on the device, e.g. the segments of a TX batch).
+// only known on the device, e.g. the segments of a TX batch). hdr_from_dst: the TX batch's
+// descriptors (tx.hip) read their first `flags` plaintext bytes from the destination.
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr,
-                               SchedSpace* sched = nullptr) {
+                               SchedSpace* sched = nullptr, int hdr_from_dst = 0) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
             return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
-                                        e->cu_count, s);
+                                        e->cu_count, s, hdr_from_dst);
         // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
@@ -499,12 +502,12 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count, s);
+                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count, s, hdr_from_dst);
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
         return err;
     }
     return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n, e->cu_count,
-                            s);
+                            s, hdr_from_dst);
 }
 
 // One packet through the device: [desc | status | aad | payload (+tag)] in one staging buffer.
@@ -852,7 +855,8 @@ static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, c
     HIP_TRY(neb_tx_plan(d_pk, npk, d_in, d_tun, ntun, e->d_keys, e->max_keys, alg, &tx.ws, out_cap, max_wires,
                         d_pk_status, d_nwires, s));
     HIP_TRY(neb_tx_segment(d_pk, npk, d_in, d_tun, d_out, &tx.ws, d_wires, d_nwires, max_wires, e->cu_count, s));
-    HIP_TRY(launch_batch(e, alg, 0, tx.ws.seal_desc, max_wires, d_out, d_wire_status, key_hint, s, d_nwires));
+    HIP_TRY(launch_batch(e, alg, 0, tx.ws.seal_desc, max_wires, d_out, d_wire_status, key_hint, s, d_nwires, nullptr,
+                         neb::kTxSealFromInput));
     HIP_TRY(neb_tx_finish(d_tun, npk, ntun, &tx.ws, s));
     HIP_TRY(hipEventRecord(tx.done, s));
     return NEB_OK;

@@ -527,7 +527,15 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
 
         if (live && g == 0) {
             wires[s] = neb_tx_wire{slot, counter, seg_len + 32u, p, j, 0u};
-            ws.seal_desc[s] = neb_desc{slot + 16u, slot + 16u, slot, counter, seg_len, 16u, T.key_id, 0u};
+            if constexpr (kTxSealFromInput) {
+                // plaintext byte x of the segment image: x < hdr from the slot (the patched header, or
+                // a plain packet up to its finished checksum), else the TUN read's byte in_off + a + x
+                const uint32_t hdr = gsok ? hl : plan.kind == kTxFinish ? cs + co + 2u : 0u;
+                const uint64_t src = (uint64_t)((uintptr_t)(in + P.in_off + a) - (uintptr_t)out);
+                ws.seal_desc[s] = neb_desc{src, slot + 16u, slot, counter, seg_len, 16u, T.key_id, hdr};
+            } else {
+                ws.seal_desc[s] = neb_desc{slot + 16u, slot + 16u, slot, counter, seg_len, 16u, T.key_id, 0u};
+            }
             // header.Encode(Version 1, Message 1, subtype 0, remote index, counter)
             // store_block: `out` may start at any byte address
             store_block(dst, make_uint4(0x00000011u, bswap32(T.remote_index), bswap32((uint32_t)(counter >> 32)),
@@ -599,10 +607,35 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
         const uint32_t zlo = plan.kind == kTxFinish ? cs + co : 0u, zhi = plan.kind == kTxFinish ? cs + co + 2u : 0u;
         const uint8_t* psrc = src + hl + a;
         const uint32_t nunits = work ? (pl + 15u) >> 4 : 0u;
-        const bool in_regs = nunits <= kTxGroup * kTxRegUnits;
+        const bool in_regs = !kTxSealFromInput && nunits <= kTxGroup * kTxRegUnits;
         const bool flip = ((hl ^ sum_lo) & 1u) != 0u;  // units start at the parity of hl
         uint4 keep[kTxRegUnits];
-        if (in_regs) {
+        if (kTxSealFromInput) {
+            // the checksum only: kTxRegUnits loads in flight per lane, then their sums
+            if (need_sum) {
+                for (uint32_t u0 = 0; u0 < nunits; u0 += kTxGroup * kTxRegUnits) {
+#pragma unroll
+                    for (uint32_t k = 0; k < kTxRegUnits; k++) {
+                        const uint32_t u = u0 + g + kTxGroup * k;
+                        keep[k] = make_uint4(0, 0, 0, 0);
+                        if (u < nunits) keep[k] = load_block(psrc + 16u * u, min(16u, pl - 16u * u));
+                    }
+#pragma unroll
+                    for (uint32_t k = 0; k < kTxRegUnits; k++) {
+                        const uint32_t u = u0 + g + kTxGroup * k;
+                        if (u < nunits) {
+                            uint4 v = keep[k];
+                            if (plan.kind == kTxFinish) {
+                                v = zero_range(v, hl + 16u * u, 0u, sum_lo);
+                                v = zero_range(v, hl + 16u * u, zlo, zhi);
+                            }
+                            const uint32_t su = unit_le_sum(v);
+                            le += flip ? bswap16(fold16(su)) : su;
+                        }
+                    }
+                }
+            }
+        } else if (in_regs) {
 #pragma unroll
             for (uint32_t k = 0; k < kTxRegUnits; k++) {
                 const uint32_t u = g + kTxGroup * k;
@@ -665,7 +698,17 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
                 }
             }
         }
-        if (in_regs) {
+        if (kTxSealFromInput) {
+            // a plain packet's prefix up to its finished checksum; the seal reads the rest from the read
+            if (work && plan.kind == kTxFinish) {
+                const uint32_t hdr = cs + co + 2u;
+                for (uint32_t u = g; 16u * u < hdr; u += kTxGroup) {
+                    const uint32_t nb = min(16u, hdr - 16u * u);
+                    const uint4 v = put_be_unit(load_block(psrc + 16u * u, nb), 16u * u, cs + co, csum);
+                    store_block(ddst + 16u * u, v, nb);
+                }
+            }
+        } else if (in_regs) {
 #pragma unroll
             for (uint32_t k = 0; k < kTxRegUnits; k++) {
                 const uint32_t u = g + kTxGroup * k;

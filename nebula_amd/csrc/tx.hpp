@@ -16,6 +16,15 @@ constexpr uint32_t kTxPlanSmallMax = kTxPlanThreads * kTxPlanItems;
 
 enum : uint8_t { kTxPass = 0, kTxFinish = 1, kTxTcp = 2, kTxUdp = 3 };
 
+// The seal reads each segment's payload straight from its TUN read and only the patched header
+// prefix from the output slot (neb_desc::flags = that prefix's length, GcmArgs::hdr_from_dst): the
+// segment kernel writes headers and computes checksums but copies no payload. 0 = round-1 path
+// (the segment kernel copies the whole segment image into the slot; the seal runs in place).
+#ifndef NEB_TX_FUSED
+#define NEB_TX_FUSED 1
+#endif
+constexpr int kTxSealFromInput = NEB_TX_FUSED;
+
 struct TxPlan {          // per packet (tx_parse_kernel)
     uint32_t nseg;       // 0 = dropped
     uint32_t hdr_len;    // superpackets: the corrected L3+L4 header length
