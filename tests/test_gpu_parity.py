@@ -174,6 +174,32 @@ def test_unaligned_offsets(engine, oracle_mod, alg):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("alg,nkeys", [(L.ALG_AESGCM, 1), (L.ALG_AESGCM, 8), (L.ALG_CHACHAPOLY, 8)])
+def test_aligned_dst_skewed_src(engine, oracle_mod, alg, nkeys):
+    """Out-of-place with 16-byte aligned destinations and sources at every byte skew: whole waves of
+    dword-aligned sources (one dwordx4 per block), whole waves of byte-skewed ones and mixed waves
+    (two aligned blocks and a shift), as a TX segment's payload inside its TUN read is read."""
+    rng = np.random.default_rng(17 + nkeys)
+    n = 16 * 24
+    keys = rng.integers(0, 256, 32 * nkeys, dtype=np.uint8)
+    stride = 3072
+    arena = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    desc = np.zeros(n, L.DESC_DTYPE)
+    for i in range(n):
+        w = i // 16
+        skew = 0 if w < 4 else (4 * (w % 4) if w < 8 else (3 + 4 * (w % 3) if w < 12 else int(rng.integers(0, 16))))
+        base = i * stride
+        ln = int(rng.choice([1300, 1448, 577, 16, 15]))
+        src = base + 32 + skew
+        dst = base + 1536
+        desc[i] = (src, dst, base, int(rng.integers(0, 2**62)), ln, 16, i % nkeys, 0)
+    b = W.Batch(alg, keys, np.zeros(nkeys, np.uint32), desc, arena, 0, "skewed-src")
+    ref, _ = oracle_seal(oracle_mod, b)
+    got, st = run_device(engine, b, seal=True)
+    assert (st == 0).all()
+    assert np.array_equal(got, ref)
+
+
 @pytest.mark.parametrize("shift", [1, 4, 8])
 @pytest.mark.parametrize("alg,nkeys", [(L.ALG_AESGCM, 1), (L.ALG_AESGCM, 16), (L.ALG_CHACHAPOLY, 16)])
 def test_unaligned_arena_base(engine, oracle_mod, alg, nkeys, shift):

@@ -57,12 +57,15 @@ def _mixed_packets(S, rng):
     return P
 
 
-def _to_arrays(packets):
+def _to_arrays(packets, skew=None):
     from nebula_amd.inside import TX_PACKET_DTYPE
 
     offs, arena = [], bytearray()
     for p in packets:
-        off = (len(arena) + 15) & ~15 if len(offs) % 2 == 0 else len(arena) + 4  # 16- and 4-aligned inputs
+        if skew is not None:  # read i starts skew[i % len(skew)] bytes past a 16-byte boundary
+            off = ((len(arena) + 15) & ~15) + skew[len(offs) % len(skew)]
+        else:
+            off = (len(arena) + 15) & ~15 if len(offs) % 2 == 0 else len(arena) + 4  # 16- and 4-aligned inputs
         arena.extend(bytes(off - len(arena)))
         offs.append(off)
         arena.extend(p["data"])
@@ -74,7 +77,8 @@ def _to_arrays(packets):
     return pk, np.frombuffer(bytes(arena), np.uint8).copy()
 
 
-def _check(engine, oracle_mod, alg, packets, tun_spec, out_cap=1 << 20, max_wires=4096, device=False, key_hint=None):
+def _check(engine, oracle_mod, alg, packets, tun_spec, out_cap=1 << 20, max_wires=4096, device=False, key_hint=None,
+           skew=None):
     import segment_oracle as S
     from nebula_amd.inside import TX_TUNNEL_DTYPE, DeviceTxBatch, tx_seal_batch_host
     from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
@@ -85,7 +89,7 @@ def _check(engine, oracle_mod, alg, packets, tun_spec, out_cap=1 << 20, max_wire
         tun = np.zeros(len(tun_spec), TX_TUNNEL_DTYPE)
         for i, (t, c) in enumerate(zip(tun_spec, ciphers)):
             tun[i] = (t["counter"], c.key_id if c is not None else L.KEYS_MIXED, t["remote_index"])
-        pk, arena = _to_arrays(packets)
+        pk, arena = _to_arrays(packets, skew)
 
         def seal(a, key, ctr, hdr, seg):
             return oracle_mod.seal(a, key, oracle_mod.nonce(a, ctr), hdr, seg)
@@ -202,3 +206,21 @@ def test_tx_batch_large_plan_path(engine, oracle_mod, cut):
             P.append(_pk(bytes(rng.getrandbits(8) for _ in range(rng.randrange(20, 90))), rng.randrange(17)))
     tun = _tunnels(rng, n=16, keyless=(5,))
     _check(engine, oracle_mod, L.ALG_AESGCM, P, tun, out_cap=(600_000 if cut else 4 << 20), max_wires=16384)
+
+
+@pytest.mark.parametrize("alg,single", [(L.ALG_AESGCM, True), (L.ALG_AESGCM, False), (L.ALG_CHACHAPOLY, False)])
+def test_tx_batch_byte_skewed_reads(engine, oracle_mod, alg, single):
+    """TUN reads at every byte skew from a 16-byte boundary: the seal reads each segment's payload
+    from inside its read (sources 1-15 bytes off alignment, a header prefix from the slot), on the
+    single-key kernel, the mixed-key chunk kernel and ChaCha20-Poly1305."""
+    import segment_oracle as S
+
+    rng = random.Random(31 + single + alg)
+    P = []
+    for i in range(32):
+        d, _, cs = build_tcpv4_super(rng.choice([1447, 5000, 14000]))
+        P.append(_pk(d, 0 if single else i % 3, 1, S.GSO_TCPV4, rng.choice([1448, 1200, 999]), cs, 16))
+    P.append(_pk(bytes(rng.getrandbits(8) for _ in range(300)), 0))                      # plain
+    tun = _tunnels(rng, n=1 if single else 3, keyless=())
+    _check(engine, oracle_mod, alg, P, tun, out_cap=4 << 20, max_wires=4096, key_hint=0 if single else None,
+           skew=list(range(16)))
