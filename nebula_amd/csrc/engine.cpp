@@ -205,6 +205,24 @@ struct neb_engine {
     SchedSpace sched;
     TxSpace tx;
 
+    // Pipelined batched receive (window.cpp): each chunk's open on a stream (and mixed-key
+    // workspace) of its own, so consecutive chunks overlap on the device; descriptors and statuses
+    // staged in pinned memory; one event per chunk.
+    struct RxSlot {
+        hipStream_t stream = nullptr;
+        hipEvent_t ev = nullptr;
+        SchedSpace* sched = nullptr;
+    };
+    struct RxSpace {
+        std::mutex mu;  // held from neb_rx_pipe_begin to neb_rx_pipe_end
+        neb_desc* h_desc = nullptr;
+        int32_t* h_status = nullptr;
+        neb_desc* d_desc = nullptr;
+        int32_t* d_status = nullptr;
+        uint32_t cap = 0;
+        std::vector<RxSlot> slot;
+    } rx;
+
     // Asynchronous batches (neb_seal_batch / neb_open_batch / neb_tx_seal_batch) read key records
     // after the call returns: the last launch on each caller stream is recorded here, and
     // neb_cipher_destroy waits for all of them before it clears and frees a slot.
@@ -346,6 +364,19 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
         hipEventSynchronize(f.second);
         hipEventDestroy(f.second);
     }
+    for (auto& r : e->rx.slot) {
+        if (r.stream) { hipStreamSynchronize(r.stream); hipStreamDestroy(r.stream); }
+        if (r.ev) hipEventDestroy(r.ev);
+        if (r.sched) {
+            if (r.sched->done) { hipEventSynchronize(r.sched->done); hipEventDestroy(r.sched->done); }
+            if (r.sched->mem) hipFree(r.sched->mem);
+            delete r.sched;
+        }
+    }
+    if (e->rx.h_desc) hipHostFree(e->rx.h_desc);
+    if (e->rx.h_status) hipHostFree(e->rx.h_status);
+    if (e->rx.d_desc) hipFree(e->rx.d_desc);
+    if (e->rx.d_status) hipFree(e->rx.d_status);
     if (e->zc_desc) hipFree(e->zc_desc);
     if (e->zc_status) hipFree(e->zc_status);
     if (e->d_keys) hipFree(e->d_keys);
@@ -815,6 +846,84 @@ NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, ui
 NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
                                 size_t arena_len, int32_t* status, uint32_t key_hint) {
     return batch_host(e, alg, 1, desc, n, arena, arena_len, status, key_hint);
+}
+
+// ---- pipelined receive (window.cpp) -----------------------------------------------------------
+// The caller has validated every descriptor. begin: true = the arena is mapped pinned memory and
+// zero-copy is the host mode; the pipeline is then reserved for the caller (e->rx.mu) until end.
+// false with *rc == NEB_OK: use the synchronous neb_open_batch_host instead.
+
+bool neb_rx_pipe_begin(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena, uint32_t n, uint32_t nchunks,
+                       neb_desc** h_desc, int32_t** h_status, int* rc) {
+    *rc = check_batch(e, alg, key_hint);
+    if (*rc != NEB_OK || n == 0 || host_mode() != kHostZeroCopy || !host_mapped(arena)) return false;
+    auto& r = e->rx;
+    r.mu.lock();
+    hipSetDevice(e->device);
+    auto fail = [&] {
+        r.mu.unlock();
+        *rc = NEB_ERR_HIP;
+        return false;
+    };
+    while (r.slot.size() < nchunks) {
+        neb_engine::RxSlot sl;
+        sl.sched = new (std::nothrow) SchedSpace;
+        // the kernels' stores into the mapped arena must be visible to the host at the event
+        if (!sl.sched || hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming | hipEventReleaseToSystem) != hipSuccess) {
+            if (sl.stream) hipStreamDestroy(sl.stream);
+            delete sl.sched;
+            return fail();
+        }
+        r.slot.push_back(sl);
+    }
+    if (n > r.cap) {
+        for (auto& sl : r.slot)
+            if (hipStreamSynchronize(sl.stream) != hipSuccess) return fail();
+        if (r.h_desc) hipHostFree(r.h_desc);
+        if (r.h_status) hipHostFree(r.h_status);
+        if (r.d_desc) hipFree(r.d_desc);
+        if (r.d_status) hipFree(r.d_status);
+        r.h_desc = nullptr;
+        r.h_status = nullptr;
+        r.d_desc = nullptr;
+        r.d_status = nullptr;
+        r.cap = 0;
+        if (hipHostMalloc((void**)&r.h_desc, (size_t)n * sizeof(neb_desc), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&r.h_status, (size_t)n * sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void**)&r.d_desc, (size_t)n * sizeof(neb_desc)) != hipSuccess ||
+            hipMalloc((void**)&r.d_status, (size_t)n * sizeof(int32_t)) != hipSuccess)
+            return fail();
+        r.cap = n;
+    }
+    *h_desc = r.h_desc;
+    *h_status = r.h_status;
+    return true;
+}
+
+// Queue chunk k: descriptors [c0, c0 + cnt) of the staging buffer, opened zero-copy in the arena.
+int neb_rx_pipe_submit(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena, uint32_t c0, uint32_t cnt,
+                       uint32_t k) {
+    auto& r = e->rx;
+    auto& sl = r.slot[k];
+    HIP_TRY(hipMemcpyAsync(r.d_desc + c0, r.h_desc + c0, (size_t)cnt * sizeof(neb_desc), hipMemcpyHostToDevice,
+                           sl.stream));
+    HIP_TRY(launch_batch(e, alg, 1, r.d_desc + c0, cnt, arena, r.d_status + c0, key_hint, sl.stream, nullptr,
+                         sl.sched));
+    HIP_TRY(hipMemcpyAsync(r.h_status + c0, r.d_status + c0, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           sl.stream));
+    HIP_TRY(hipEventRecord(sl.ev, sl.stream));
+    return NEB_OK;
+}
+
+int neb_rx_pipe_wait(neb_engine* e, uint32_t k) {
+    HIP_TRY(hipEventSynchronize(e->rx.slot[k].ev));
+    return NEB_OK;
+}
+
+void neb_rx_pipe_end(neb_engine* e) {
+    for (auto& sl : e->rx.slot) hipStreamSynchronize(sl.stream);
+    e->rx.mu.unlock();
 }
 
 // ---- transmit batch (tx.hip) ------------------------------------------------------------------

@@ -22,15 +22,34 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
 
 #include "../../include/nebula_aead.h"
 
-bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len);  // engine.cpp
+// engine.cpp
+bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len);
+extern "C" {  // internal (hidden), defined inside engine.cpp's extern "C" block
+bool neb_rx_pipe_begin(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena, uint32_t n, uint32_t nchunks,
+                       neb_desc** h_desc, int32_t** h_status, int* rc);
+int neb_rx_pipe_submit(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena, uint32_t c0, uint32_t cnt,
+                       uint32_t k);
+int neb_rx_pipe_wait(neb_engine* e, uint32_t k);
+void neb_rx_pipe_end(neb_engine* e);
+}
 
 namespace {
+
+// Zero-copy receive batches can be opened in up to kRxChunks pieces (NEB_RX_CHUNKS, at least
+// kRxMinChunk packets each) so that the host-side window work overlaps the GPU. Measured (C2 / C3,
+// 64 Ki packets, profiles/r2_host/rx_chunks.log): 1 chunk 22.8 / 15.5-17.9 GiB/s, 2 chunks 22.5 /
+// 15.8, 4 chunks 21.4 / 15.0 — the window passes run slower beside the zero-copy kernels'
+// host-memory traffic than they save. Default 1.
+constexpr uint32_t kRxChunks = 4, kRxMinChunk = 8192, kRxDefaultChunks = 1;
 
 struct WindowCore {
     uint64_t length = 0, mask = 0, current = 0;
@@ -186,92 +205,185 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
                                    int32_t* status, uint32_t key_hint) {
     if (!e || (n && (!desc || !arena || !status || !windows))) return NEB_ERR_INVALID;
     if (n == 0) return NEB_OK;
+    static const bool prof = std::getenv("NEB_RX_PROF") != nullptr;  // phase times to stderr
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
     // an invalid batch is refused before any window moves or any packet is opened
     for (uint32_t i = 0; i < n; i++)
         if (!neb_desc_in_arena(desc[i], 1, arena_len)) return NEB_ERR_INVALID;
-    // Windows are independent: group the batch by window (stable, so each window sees its packets
-    // in arrival order) and run each window's sequence under one lock acquisition.
-    std::vector<uint32_t> start(nwindows + 2, 0), order(n);
     auto group_of = [&](const neb_desc& d) -> uint32_t {
         return (d.key_id < nwindows && windows[d.key_id]) ? d.key_id : nwindows;  // nwindows: no window
     };
-    for (uint32_t i = 0; i < n; i++) start[group_of(desc[i]) + 1]++;
-    for (uint32_t g = 0; g <= nwindows; g++) start[g + 1] += start[g];
-    {
-        std::vector<uint32_t> fill(start.begin(), start.end() - 1);
-        for (uint32_t i = 0; i < n; i++) order[fill[group_of(desc[i])]++] = i;
+
+    // A zero-copy arena is opened in chunks of arrival order queued on the engine's receive stream:
+    // chunk k's GPU open overlaps the simulation of chunk k+1 and the real window pass of chunk
+    // k-1 on this thread. The simulation is the same sequential run one batch would get, only in
+    // pieces: the private window copies persist across chunks. Any other arena: one synchronous
+    // neb_open_batch_host, as before.
+    neb_desc* h_desc = nullptr;
+    int32_t* h_status = nullptr;
+    int prc = NEB_OK;
+    const bool piped = neb_rx_pipe_begin(e, alg, key_hint, arena, n, kRxChunks + 1, &h_desc, &h_status, &prc);
+    if (!piped && prc != NEB_OK) return prc;
+    static const uint32_t nch = [] {
+        const char* v = std::getenv("NEB_RX_CHUNKS");
+        const int c = v ? std::atoi(v) : (int)kRxDefaultChunks;
+        return (uint32_t)std::min(std::max(c, 1), (int)kRxChunks);
+    }();
+    uint32_t chunk = n;
+    if (piped && nch > 1) {
+        chunk = n / nch + 1;
+        chunk = std::max(chunk, std::min(n, kRxMinChunk));
     }
+    const uint32_t nchunks = (n + chunk - 1) / chunk;
     enum : uint8_t { kToGpu, kHeld };
     std::vector<uint8_t> plan(n, kHeld);
-    std::vector<neb_desc> sub;
     std::vector<uint32_t> sub_of(n, 0);
-    sub.reserve(n);
+    struct Chunk {
+        uint32_t c0 = 0, c1 = 0, k = 0;
+        std::vector<uint32_t> start, order;  // this chunk's packets grouped by window, arrival order kept
+        uint32_t ngpu = 0;                   // the packets the simulation lets through
+        std::vector<neb_desc> sub;           // (synchronous path) their descriptors and statuses
+        std::vector<int32_t> sub_status;
+        const int32_t* st = nullptr;         // their statuses once opened
+        bool queued = false;
+    };
+    std::vector<Chunk> ch(nchunks);
+    // private window copies: one per touched window when the batch is chunked (they persist from
+    // chunk to chunk), else one scratch copy reused window after window
+    std::vector<WindowCore> sim(nchunks > 1 ? nwindows : 0);
+    std::vector<uint8_t> sim_taken(nchunks > 1 ? nwindows : 0, 0);
+    WindowCore scratch;
+    double us_plan = 0, us_real = 0;
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
 
-    // 1. simulation on a private copy of each window: which packets would the sequential receive
-    //    path decrypt? (the GPU batch keeps arrival order inside each window's run)
-    WindowCore sim;
-    for (uint32_t g = 0; g < nwindows; g++) {
-        if (start[g] == start[g + 1]) continue;
+    auto simulate = [&](Chunk& c) -> int {
+        const uint32_t m = c.c1 - c.c0;
+        c.start.assign(nwindows + 2, 0);
+        c.order.resize(m);
+        for (uint32_t i = c.c0; i < c.c1; i++) c.start[group_of(desc[i]) + 1]++;
+        for (uint32_t g = 0; g <= nwindows; g++) c.start[g + 1] += c.start[g];
         {
-            std::lock_guard<std::mutex> lk(windows[g]->mu);
-            sim = windows[g]->core;
+            std::vector<uint32_t> fill(c.start.begin(), c.start.end() - 1);
+            for (uint32_t i = c.c0; i < c.c1; i++) c.order[fill[group_of(desc[i])]++] = i;
         }
-        for (uint32_t k = start[g]; k < start[g + 1]; k++) {
-            const uint32_t i = order[k];
-            if (sim.check(desc[i].counter)) {
-                sim.update(desc[i].counter);
-                plan[i] = kToGpu;
+        uint32_t ngpu = 0;
+        for (uint32_t g = 0; g < nwindows; g++) {
+            if (c.start[g] == c.start[g + 1]) continue;
+            WindowCore* wp = &scratch;
+            if (nchunks > 1) {
+                wp = &sim[g];
+                if (!sim_taken[g]) {  // a private copy, first time this batch touches the window
+                    std::lock_guard<std::mutex> lk(windows[g]->mu);
+                    sim[g] = windows[g]->core;
+                    sim_taken[g] = 1;
+                }
+            } else {
+                std::lock_guard<std::mutex> lk(windows[g]->mu);
+                scratch = windows[g]->core;  // reuses the scratch bitmap's storage
+            }
+            WindowCore& w = *wp;
+            for (uint32_t k = c.start[g]; k < c.start[g + 1]; k++) {
+                const uint32_t i = c.order[k];
+                if (w.check(desc[i].counter)) {
+                    w.update(desc[i].counter);
+                    plan[i] = kToGpu;
+                    ngpu++;
+                }
             }
         }
-    }
-    for (uint32_t i = 0; i < n; i++)
-        if (plan[i] == kToGpu) {
-            sub_of[i] = (uint32_t)sub.size();
-            sub.push_back(desc[i]);
+        c.ngpu = ngpu;
+        neb_desc* out = nullptr;
+        if (piped) {
+            out = h_desc + c.c0;  // chunk k's slice of the pinned staging buffer
+        } else {
+            c.sub.resize(ngpu);
+            c.sub_status.assign(ngpu, NEB_STATUS_BAD_KEY);
+            out = c.sub.data();
         }
-
-    // 2. one GPU open for everything the simulation lets through
-    std::vector<int32_t> sub_status(sub.size(), NEB_STATUS_BAD_KEY);
-    if (!sub.empty()) {
-        const int rc = neb_open_batch_host(e, alg, sub.data(), (uint32_t)sub.size(), arena, arena_len,
-                                           sub_status.data(), key_hint);
-        if (rc != NEB_OK) return rc;
-    }
-
-    // 3. the real windows, each in arrival order: Check → tag verdict → Update
-    for (uint32_t k = start[nwindows]; k < start[nwindows + 1]; k++) status[order[k]] = NEB_STATUS_BAD_KEY;
-    for (uint32_t g = 0; g < nwindows; g++) {
-        if (start[g] == start[g + 1]) continue;
-        neb_window* w = windows[g];
-        std::unique_lock<std::mutex> lk(w->mu);
-        for (uint32_t k = start[g]; k < start[g + 1]; k++) {
-            const uint32_t i = order[k];
-            const neb_desc& d = desc[i];
-            if (!w->core.check(d.counter)) {
-                status[i] = NEB_STATUS_REPLAY;
-                continue;
-            }
-            int32_t st;
-            if (plan[i] == kToGpu) {
-                st = sub_status[sub_of[i]];
-            } else {  // held back, yet the real window accepts it: an earlier copy failed its tag
-                lk.unlock();
-                const int rc = neb_open_batch_host(e, alg, &d, 1, arena, arena_len, &st, key_hint);
-                if (rc != NEB_OK) return rc;
-                lk.lock();
-                if (st == NEB_STATUS_OK && !w->core.check(d.counter)) {  // moved by another thread meanwhile
+        if (ngpu == m) {
+            std::memcpy(out, desc + c.c0, (size_t)m * sizeof(neb_desc));
+            for (uint32_t i = c.c0; i < c.c1; i++) sub_of[i] = i - c.c0;
+        } else {
+            uint32_t j = 0;
+            for (uint32_t i = c.c0; i < c.c1; i++)
+                if (plan[i] == kToGpu) {
+                    sub_of[i] = j;
+                    out[j++] = desc[i];
+                }
+        }
+        c.st = piped ? h_status + c.c0 : c.sub_status.data();
+        if (ngpu && piped) {
+            c.queued = true;
+            return neb_rx_pipe_submit(e, alg, key_hint, arena, c.c0, ngpu, c.k);
+        }
+        return NEB_OK;
+    };
+    // the real windows, each in arrival order: Check → tag verdict → Update
+    auto real = [&](Chunk& c) -> int {
+        for (uint32_t k = c.start[nwindows]; k < c.start[nwindows + 1]; k++) status[c.order[k]] = NEB_STATUS_BAD_KEY;
+        for (uint32_t g = 0; g < nwindows; g++) {
+            if (c.start[g] == c.start[g + 1]) continue;
+            neb_window* w = windows[g];
+            std::unique_lock<std::mutex> lk(w->mu);
+            for (uint32_t k = c.start[g]; k < c.start[g + 1]; k++) {
+                const uint32_t i = c.order[k];
+                const neb_desc& d = desc[i];
+                if (!w->core.check(d.counter)) {
                     status[i] = NEB_STATUS_REPLAY;
                     continue;
                 }
+                int32_t st;
+                if (plan[i] == kToGpu) {
+                    st = c.st[sub_of[i]];
+                } else {  // held back, yet the real window accepts it: an earlier copy failed its tag
+                    lk.unlock();
+                    const int rc = neb_open_batch_host(e, alg, &d, 1, arena, arena_len, &st, key_hint);
+                    if (rc != NEB_OK) return rc;
+                    lk.lock();
+                    if (st == NEB_STATUS_OK && !w->core.check(d.counter)) {  // moved by another thread meanwhile
+                        status[i] = NEB_STATUS_REPLAY;
+                        continue;
+                    }
+                }
+                if (st != NEB_STATUS_OK) {
+                    status[i] = st;
+                    continue;
+                }
+                status[i] = w->core.update(d.counter) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
             }
-            if (st != NEB_STATUS_OK) {
-                status[i] = st;
-                continue;
-            }
-            status[i] = w->core.update(d.counter) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
+        }
+        return NEB_OK;
+    };
+    // the chunk's statuses: the queued open's event, or (synchronous path) the open itself
+    auto gpu_done = [&](Chunk& c) -> int {
+        if (piped) return c.queued ? neb_rx_pipe_wait(e, c.k) : NEB_OK;
+        if (!c.ngpu) return NEB_OK;
+        return neb_open_batch_host(e, alg, c.sub.data(), c.ngpu, arena, arena_len, c.sub_status.data(), key_hint);
+    };
+
+    int rc = NEB_OK;
+    for (uint32_t k = 0; k <= nchunks && rc == NEB_OK; k++) {
+        if (k < nchunks) {
+            const auto ta = now();
+            ch[k].k = k;
+            ch[k].c0 = k * chunk;
+            ch[k].c1 = std::min(n, (k + 1) * chunk);
+            rc = simulate(ch[k]);
+            us_plan += us(ta, now());
+        }
+        if (k > 0 && rc == NEB_OK) {
+            rc = gpu_done(ch[k - 1]);
+            const auto ta = now();
+            if (rc == NEB_OK) rc = real(ch[k - 1]);
+            us_real += us(ta, now());
         }
     }
-    return NEB_OK;
+    if (piped) neb_rx_pipe_end(e);  // waits for anything still queued
+    if (prof)
+        std::fprintf(stderr, "rx n=%u chunks %u total %.1f us (sim %.1f, real %.1f on this thread)\n", n, nchunks,
+                     us(t0, now()), us_plan, us_real);
+    return rc;
 }
 
 }  // extern "C"

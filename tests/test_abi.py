@@ -31,6 +31,12 @@ def test_library_exports_every_declared_symbol():
     assert set(syms) == set(L.SIGNATURES), set(syms) ^ set(L.SIGNATURES)
 
 
+def test_library_has_no_unresolved_symbols():
+    """Binding every symbol at load time (RTLD_NOW) fails on a reference the build left undefined,
+    which a lazy load only reports at the first call into it."""
+    C.CDLL(L.LIB_PATH, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+
+
 def test_header_constants_match_binding():
     text = open(HDR).read()
 

@@ -14,15 +14,16 @@ pytestmark = pytest.mark.gpu
 SLOT = 16 + 1400 + 16
 
 
-def _build(oracle_mod, alg, keys, arrivals, seed):
+def _build(oracle_mod, alg, keys, arrivals, seed, lens=None):
     """arrivals: [(tunnel, counter, forged)] -> (arena, desc (tunnel index in key_id), payloads)."""
     rng = random.Random(seed)
+    lens = lens or [0, 1, 15, 16, 17, 100, 576, 1300, 1400]
     n = len(arrivals)
     arena = np.zeros(n * SLOT, np.uint8)
     desc = np.zeros(n, dtype=L.DESC_DTYPE)
     pts = []
     for i, (t, ctr, forged) in enumerate(arrivals):
-        ln = rng.choice([0, 1, 15, 16, 17, 100, 576, 1300, 1400]) if i % 5 else 1300
+        ln = rng.choice(lens) if i % 5 else lens[-2]
         pt = bytes(rng.getrandbits(8) for _ in range(ln))
         hdr = oracle_mod.header_encode(1, 1, 0, 0x1000 + t, ctr)
         ct = bytearray(oracle_mod.seal(alg, keys[t], oracle_mod.nonce(alg, ctr), hdr, pt))
@@ -54,7 +55,8 @@ def _expected(oracle_mod, R, alg, keys, arrivals, arena, pts, window_len, seeds,
     return st, exp, wins
 
 
-def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=None, installed=None, seed=1):
+def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=None, installed=None, seed=1,
+         lens=None):
     import replay_oracle as R
     from nebula_amd.connection_state import Bits, rx_open_batch
     from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
@@ -68,7 +70,7 @@ def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=N
     # tunnels whose key is not installed get a slot id from the top of the table (never allocated here)
     slot_of = {t: (ciphers[t].key_id if t in ciphers else engine.max_keys - 1 - t) for t in range(ntunnels)}
     try:
-        arena, desc, pts = _build(oracle_mod, alg, keys, arrivals, seed)
+        arena, desc, pts = _build(oracle_mod, alg, keys, arrivals, seed, lens)
         exp_status, exp_arena, owins = _expected(oracle_mod, R, alg, keys, arrivals, arena, pts, window_len, seeds,
                                                  installed)
         windows = [None] * engine.max_keys
@@ -140,6 +142,31 @@ def test_rx_batch_random_traffic(engine, oracle_mod):
             c = cur[t] + rng.randrange(1, 30)
         arr.append((t, c, rng.random() < 0.05))
     _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=8, window_len=64, seed=3)
+
+
+def test_rx_batch_pipelined_chunks(engine, oracle_mod):
+    """A receive batch long enough to be opened in several pipelined chunks (window.cpp: the next
+    chunk's simulation and the previous chunk's window pass overlap the GPU): duplicates, replays
+    and forged-then-genuine copies straddle the chunk boundaries."""
+    rng = random.Random(13)
+    cur = [2] * 6
+    arr = []
+    for k in range(20000):
+        t = rng.randrange(6)
+        r = rng.random()
+        if r < 0.7:
+            cur[t] += 1 + (rng.random() < 0.05) * rng.randrange(1, 300)
+            c = cur[t]
+        elif r < 0.9:
+            c = max(1, cur[t] - rng.randrange(0, 120))
+        else:
+            c = cur[t] + rng.randrange(1, 50)
+        arr.append((t, c, rng.random() < 0.04))
+        if k % 8192 == 8191:  # a forged copy just before a boundary, its genuine twin just after
+            cur[t] += 1
+            arr.append((t, cur[t], True))
+            arr.append((t, cur[t], False))
+    _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=6, window_len=256, seed=5, lens=[0, 1, 16, 40, 100])
 
 
 def test_rx_batch_invalid_descriptor_touches_nothing(engine, oracle_mod):
