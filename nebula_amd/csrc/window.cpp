@@ -22,7 +22,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,12 +48,92 @@ void neb_rx_pipe_end(neb_engine* e);
 
 namespace {
 
-// Zero-copy receive batches can be opened in up to kRxChunks pieces (NEB_RX_CHUNKS, at least
-// kRxMinChunk packets each) so that the host-side window work overlaps the GPU. Measured (C2 / C3,
-// 64 Ki packets, profiles/r2_host/rx_chunks.log): 1 chunk 22.8 / 15.5-17.9 GiB/s, 2 chunks 22.5 /
-// 15.8, 4 chunks 21.4 / 15.0 — the window passes run slower beside the zero-copy kernels'
-// host-memory traffic than they save. Default 1.
-constexpr uint32_t kRxChunks = 4, kRxMinChunk = 8192, kRxDefaultChunks = 1;
+// The batched receive's window simulation and real window pass run on a small persistent pool
+// when a batch touches at least kRxMinWindows windows: windows are independent, and each window's
+// packets stay on one thread, in arrival order. NEB_RX_THREADS sets the pool size (1 = this
+// thread only). Groups under kRxMinPerThread packets are not split.
+constexpr uint32_t kRxMinPerThread = 2048, kRxMinWindows = 64, kRxMaxThreads = 8;
+
+class RxPool {
+  public:
+    explicit RxPool(uint32_t nthreads) {
+        for (uint32_t t = 1; t < nthreads; t++) th_.emplace_back([this] { loop(); });
+    }
+    ~RxPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    uint32_t size() const { return (uint32_t)th_.size() + 1; }
+    // fn(j) for j in [0, n), on the pool and this thread; returns when every call has returned.
+    // Calls from several threads at once run one after another.
+    void run(uint32_t n, const std::function<void(uint32_t)>& fn) {
+        if (n <= 1 || th_.empty()) {
+            for (uint32_t j = 0; j < n; j++) fn(j);
+            return;
+        }
+        std::lock_guard<std::mutex> serial(run_mu_);
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &fn;
+            njobs_ = n;
+            next_.store(0);
+            left_ = n;
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> g(m_);
+        done_cv_.wait(g, [&] { return left_ == 0 && active_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void work() {
+        for (;;) {
+            const uint32_t j = next_.fetch_add(1);
+            if (j >= njobs_) return;
+            (*job_)(j);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_cv_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return quit_ || (gen_ != seen && job_); });
+                if (quit_) return;
+                seen = gen_;
+                active_++;
+            }
+            work();
+            std::lock_guard<std::mutex> g(m_);
+            if (--active_ == 0 && left_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_, run_mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(uint32_t)>* job_ = nullptr;
+    uint32_t njobs_ = 0, left_ = 0, active_ = 0;
+    std::atomic<uint32_t> next_{0};
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
+RxPool& rx_pool() {
+    static RxPool pool([] {
+        const char* v = std::getenv("NEB_RX_THREADS");
+        int t = v ? std::atoi(v) : (int)std::min(kRxMaxThreads, std::max(1u, std::thread::hardware_concurrency()));
+        return (uint32_t)std::max(1, std::min(t, 64));
+    }());
+    return pool;
+}
 
 struct WindowCore {
     uint64_t length = 0, mask = 0, current = 0;
@@ -207,127 +291,159 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
     if (n == 0) return NEB_OK;
     static const bool prof = std::getenv("NEB_RX_PROF") != nullptr;  // phase times to stderr
     auto now = [] { return std::chrono::steady_clock::now(); };
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     const auto t0 = now();
+    RxPool& pool = rx_pool();
+    // packet ranges for the per-packet phases: one (measured: spread over the pool they gained
+    // nothing against the wake-ups, profiles/r2_host/rx_threads.log), the code stays range-based
+    const uint32_t nr = 1;
+    auto range = [&](uint32_t r) { return std::make_pair((uint64_t)n * r / nr, (uint64_t)n * (r + 1) / nr); };
+
     // an invalid batch is refused before any window moves or any packet is opened
-    for (uint32_t i = 0; i < n; i++)
-        if (!neb_desc_in_arena(desc[i], 1, arena_len)) return NEB_ERR_INVALID;
+    std::vector<uint8_t> bad(nr, 0);
+    pool.run(nr, [&](uint32_t r) {
+        const auto [i0, i1] = range(r);
+        for (uint64_t i = i0; i < i1; i++)
+            if (!neb_desc_in_arena(desc[i], 1, arena_len)) {
+                bad[r] = 1;
+                return;
+            }
+    });
+    for (uint8_t b : bad)
+        if (b) return NEB_ERR_INVALID;
+    const auto ta = now();
     auto group_of = [&](const neb_desc& d) -> uint32_t {
         return (d.key_id < nwindows && windows[d.key_id]) ? d.key_id : nwindows;  // nwindows: no window
     };
 
-    // A zero-copy arena is opened in chunks of arrival order queued on the engine's receive stream:
-    // chunk k's GPU open overlaps the simulation of chunk k+1 and the real window pass of chunk
-    // k-1 on this thread. The simulation is the same sequential run one batch would get, only in
-    // pieces: the private window copies persist across chunks. Any other arena: one synchronous
-    // neb_open_batch_host, as before.
-    neb_desc* h_desc = nullptr;
-    int32_t* h_status = nullptr;
-    int prc = NEB_OK;
-    const bool piped = neb_rx_pipe_begin(e, alg, key_hint, arena, n, kRxChunks + 1, &h_desc, &h_status, &prc);
-    if (!piped && prc != NEB_OK) return prc;
-    static const uint32_t nch = [] {
-        const char* v = std::getenv("NEB_RX_CHUNKS");
-        const int c = v ? std::atoi(v) : (int)kRxDefaultChunks;
-        return (uint32_t)std::min(std::max(c, 1), (int)kRxChunks);
-    }();
-    uint32_t chunk = n;
-    if (piped && nch > 1) {
-        chunk = n / nch + 1;
-        chunk = std::max(chunk, std::min(n, kRxMinChunk));
+    // Group by window, arrival order kept inside each (a counting sort whose ranges are counted
+    // and scattered in parallel, ranges in arrival order).
+    const uint32_t ng = nwindows + 1;
+    std::vector<uint32_t> cnt((size_t)nr * ng, 0), start(ng + 1, 0), order(n);
+    pool.run(nr, [&](uint32_t r) {
+        const auto [i0, i1] = range(r);
+        uint32_t* c = cnt.data() + (size_t)r * ng;
+        for (uint64_t i = i0; i < i1; i++) c[group_of(desc[i])]++;
+    });
+    {
+        uint32_t acc = 0;
+        for (uint32_t g = 0; g < ng; g++) {
+            start[g] = acc;
+            for (uint32_t r = 0; r < nr; r++) {
+                const uint32_t c = cnt[(size_t)r * ng + g];
+                cnt[(size_t)r * ng + g] = acc;
+                acc += c;
+            }
+        }
+        start[ng] = acc;
     }
-    const uint32_t nchunks = (n + chunk - 1) / chunk;
+    pool.run(nr, [&](uint32_t r) {
+        const auto [i0, i1] = range(r);
+        uint32_t* c = cnt.data() + (size_t)r * ng;
+        for (uint64_t i = i0; i < i1; i++) order[c[group_of(desc[i])]++] = (uint32_t)i;
+    });
+    const auto tb = now();
+    // window groups for the per-window phases: contiguous runs of windows with about equal packets,
+    // spread over the pool when the batch touches many windows (C3, 4096 tunnels: simulation 456 ->
+    // 221 us, real pass 728 -> 472 us on 8 threads); one window's packets always stay on one thread
+    uint32_t touched = 0;
+    for (uint32_t g = 0; g < nwindows; g++) touched += start[g] != start[g + 1];
+    const uint32_t nwg = touched < kRxMinWindows ? 1u
+                                                  : std::max(1u, std::min(pool.size(), start[nwindows] / kRxMinPerThread));
+    std::vector<uint32_t> wsplit(nwg + 1, nwindows);
+    {
+        wsplit[0] = 0;
+        uint32_t g = 0;
+        for (uint32_t t = 1; t < nwg; t++) {
+            const uint64_t want = (uint64_t)start[nwindows] * t / nwg;
+            while (g < nwindows && start[g + 1] <= want) g++;
+            wsplit[t] = std::max(g, wsplit[t - 1]);
+        }
+    }
+
+    const auto tc = now();
+    // 1. simulation on a private copy of each window: which packets would the sequential receive
+    //    path decrypt? (one scratch window per thread, reused window after window)
     enum : uint8_t { kToGpu, kHeld };
     std::vector<uint8_t> plan(n, kHeld);
-    std::vector<uint32_t> sub_of(n, 0);
-    struct Chunk {
-        uint32_t c0 = 0, c1 = 0, k = 0;
-        std::vector<uint32_t> start, order;  // this chunk's packets grouped by window, arrival order kept
-        uint32_t ngpu = 0;                   // the packets the simulation lets through
-        std::vector<neb_desc> sub;           // (synchronous path) their descriptors and statuses
-        std::vector<int32_t> sub_status;
-        const int32_t* st = nullptr;         // their statuses once opened
-        bool queued = false;
-    };
-    std::vector<Chunk> ch(nchunks);
-    // private window copies: one per touched window when the batch is chunked (they persist from
-    // chunk to chunk), else one scratch copy reused window after window
-    std::vector<WindowCore> sim(nchunks > 1 ? nwindows : 0);
-    std::vector<uint8_t> sim_taken(nchunks > 1 ? nwindows : 0, 0);
-    WindowCore scratch;
-    double us_plan = 0, us_real = 0;
-    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-
-    auto simulate = [&](Chunk& c) -> int {
-        const uint32_t m = c.c1 - c.c0;
-        c.start.assign(nwindows + 2, 0);
-        c.order.resize(m);
-        for (uint32_t i = c.c0; i < c.c1; i++) c.start[group_of(desc[i]) + 1]++;
-        for (uint32_t g = 0; g <= nwindows; g++) c.start[g + 1] += c.start[g];
-        {
-            std::vector<uint32_t> fill(c.start.begin(), c.start.end() - 1);
-            for (uint32_t i = c.c0; i < c.c1; i++) c.order[fill[group_of(desc[i])]++] = i;
-        }
-        uint32_t ngpu = 0;
-        for (uint32_t g = 0; g < nwindows; g++) {
-            if (c.start[g] == c.start[g + 1]) continue;
-            WindowCore* wp = &scratch;
-            if (nchunks > 1) {
-                wp = &sim[g];
-                if (!sim_taken[g]) {  // a private copy, first time this batch touches the window
-                    std::lock_guard<std::mutex> lk(windows[g]->mu);
-                    sim[g] = windows[g]->core;
-                    sim_taken[g] = 1;
-                }
-            } else {
+    pool.run(nwg, [&](uint32_t t) {
+        WindowCore sim;
+        for (uint32_t g = wsplit[t]; g < wsplit[t + 1]; g++) {
+            if (start[g] == start[g + 1]) continue;
+            {
                 std::lock_guard<std::mutex> lk(windows[g]->mu);
-                scratch = windows[g]->core;  // reuses the scratch bitmap's storage
+                sim = windows[g]->core;
             }
-            WindowCore& w = *wp;
-            for (uint32_t k = c.start[g]; k < c.start[g + 1]; k++) {
-                const uint32_t i = c.order[k];
-                if (w.check(desc[i].counter)) {
-                    w.update(desc[i].counter);
+            for (uint32_t k = start[g]; k < start[g + 1]; k++) {
+                const uint32_t i = order[k];
+                if (sim.check(desc[i].counter)) {
+                    sim.update(desc[i].counter);
                     plan[i] = kToGpu;
-                    ngpu++;
                 }
             }
         }
-        c.ngpu = ngpu;
-        neb_desc* out = nullptr;
+    });
+    const auto t1 = now();
+
+    // 2. one GPU open for everything the simulation lets through, compacted in arrival order into
+    //    the engine's pinned staging buffer (a zero-copy arena, opened on the receive stream) or
+    //    a private vector (any other arena: neb_open_batch_host)
+    neb_desc* h_desc = nullptr;
+    int32_t* h_status = nullptr;
+    int rc = NEB_OK;
+    const bool piped = neb_rx_pipe_begin(e, alg, key_hint, arena, n, 1, &h_desc, &h_status, &rc);
+    if (!piped && rc != NEB_OK) return rc;
+    std::vector<uint32_t> sub_of(n, 0), before(nr + 1, 0);
+    pool.run(nr, [&](uint32_t r) {
+        const auto [i0, i1] = range(r);
+        uint32_t c = 0;
+        for (uint64_t i = i0; i < i1; i++) c += plan[i] == kToGpu;
+        before[r + 1] = c;
+    });
+    for (uint32_t r = 0; r < nr; r++) before[r + 1] += before[r];
+    const uint32_t ngpu = before[nr];
+    std::vector<neb_desc> sub(piped ? 0 : ngpu);
+    std::vector<int32_t> sub_status(piped ? 0 : ngpu, NEB_STATUS_BAD_KEY);
+    neb_desc* out = piped ? h_desc : sub.data();
+    pool.run(nr, [&](uint32_t r) {
+        const auto [i0, i1] = range(r);
+        uint32_t j = before[r];
+        if (before[r + 1] - j == i1 - i0) {  // every packet of the range: one copy
+            std::memcpy(out + j, desc + i0, (size_t)(i1 - i0) * sizeof(neb_desc));
+            for (uint64_t i = i0; i < i1; i++) sub_of[i] = j++;
+            return;
+        }
+        for (uint64_t i = i0; i < i1; i++)
+            if (plan[i] == kToGpu) {
+                sub_of[i] = j;
+                out[j++] = desc[i];
+            }
+    });
+    const int32_t* gst = piped ? h_status : sub_status.data();
+    const auto ts = now();
+    if (ngpu) {
         if (piped) {
-            out = h_desc + c.c0;  // chunk k's slice of the pinned staging buffer
+            rc = neb_rx_pipe_submit(e, alg, key_hint, arena, 0, ngpu, 0);
+            if (rc == NEB_OK) rc = neb_rx_pipe_wait(e, 0);
         } else {
-            c.sub.resize(ngpu);
-            c.sub_status.assign(ngpu, NEB_STATUS_BAD_KEY);
-            out = c.sub.data();
+            rc = neb_open_batch_host(e, alg, sub.data(), ngpu, arena, arena_len, sub_status.data(), key_hint);
         }
-        if (ngpu == m) {
-            std::memcpy(out, desc + c.c0, (size_t)m * sizeof(neb_desc));
-            for (uint32_t i = c.c0; i < c.c1; i++) sub_of[i] = i - c.c0;
-        } else {
-            uint32_t j = 0;
-            for (uint32_t i = c.c0; i < c.c1; i++)
-                if (plan[i] == kToGpu) {
-                    sub_of[i] = j;
-                    out[j++] = desc[i];
-                }
-        }
-        c.st = piped ? h_status + c.c0 : c.sub_status.data();
-        if (ngpu && piped) {
-            c.queued = true;
-            return neb_rx_pipe_submit(e, alg, key_hint, arena, c.c0, ngpu, c.k);
-        }
-        return NEB_OK;
-    };
-    // the real windows, each in arrival order: Check → tag verdict → Update
-    auto real = [&](Chunk& c) -> int {
-        for (uint32_t k = c.start[nwindows]; k < c.start[nwindows + 1]; k++) status[c.order[k]] = NEB_STATUS_BAD_KEY;
-        for (uint32_t g = 0; g < nwindows; g++) {
-            if (c.start[g] == c.start[g + 1]) continue;
+    }
+    const auto td = now();
+    if (piped) neb_rx_pipe_end(e);
+    if (rc != NEB_OK) return rc;
+    const auto t2 = now();
+
+    // 3. the real windows, each in arrival order: Check → tag verdict → Update
+    for (uint32_t k = start[nwindows]; k < start[nwindows + 1]; k++) status[order[k]] = NEB_STATUS_BAD_KEY;
+    std::vector<int> trc(nwg, NEB_OK);
+    pool.run(nwg, [&](uint32_t t) {
+        for (uint32_t g = wsplit[t]; g < wsplit[t + 1]; g++) {
+            if (start[g] == start[g + 1]) continue;
             neb_window* w = windows[g];
             std::unique_lock<std::mutex> lk(w->mu);
-            for (uint32_t k = c.start[g]; k < c.start[g + 1]; k++) {
-                const uint32_t i = c.order[k];
+            for (uint32_t k = start[g]; k < start[g + 1]; k++) {
+                const uint32_t i = order[k];
                 const neb_desc& d = desc[i];
                 if (!w->core.check(d.counter)) {
                     status[i] = NEB_STATUS_REPLAY;
@@ -335,11 +451,14 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
                 }
                 int32_t st;
                 if (plan[i] == kToGpu) {
-                    st = c.st[sub_of[i]];
+                    st = gst[sub_of[i]];
                 } else {  // held back, yet the real window accepts it: an earlier copy failed its tag
                     lk.unlock();
-                    const int rc = neb_open_batch_host(e, alg, &d, 1, arena, arena_len, &st, key_hint);
-                    if (rc != NEB_OK) return rc;
+                    const int r = neb_open_batch_host(e, alg, &d, 1, arena, arena_len, &st, key_hint);
+                    if (r != NEB_OK) {
+                        trc[t] = r;
+                        return;
+                    }
                     lk.lock();
                     if (st == NEB_STATUS_OK && !w->core.check(d.counter)) {  // moved by another thread meanwhile
                         status[i] = NEB_STATUS_REPLAY;
@@ -353,37 +472,16 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
                 status[i] = w->core.update(d.counter) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
             }
         }
-        return NEB_OK;
-    };
-    // the chunk's statuses: the queued open's event, or (synchronous path) the open itself
-    auto gpu_done = [&](Chunk& c) -> int {
-        if (piped) return c.queued ? neb_rx_pipe_wait(e, c.k) : NEB_OK;
-        if (!c.ngpu) return NEB_OK;
-        return neb_open_batch_host(e, alg, c.sub.data(), c.ngpu, arena, arena_len, c.sub_status.data(), key_hint);
-    };
-
-    int rc = NEB_OK;
-    for (uint32_t k = 0; k <= nchunks && rc == NEB_OK; k++) {
-        if (k < nchunks) {
-            const auto ta = now();
-            ch[k].k = k;
-            ch[k].c0 = k * chunk;
-            ch[k].c1 = std::min(n, (k + 1) * chunk);
-            rc = simulate(ch[k]);
-            us_plan += us(ta, now());
-        }
-        if (k > 0 && rc == NEB_OK) {
-            rc = gpu_done(ch[k - 1]);
-            const auto ta = now();
-            if (rc == NEB_OK) rc = real(ch[k - 1]);
-            us_real += us(ta, now());
-        }
-    }
-    if (piped) neb_rx_pipe_end(e);  // waits for anything still queued
+    });
+    for (int r : trc)
+        if (r != NEB_OK) return r;
     if (prof)
-        std::fprintf(stderr, "rx n=%u chunks %u total %.1f us (sim %.1f, real %.1f on this thread)\n", n, nchunks,
-                     us(t0, now()), us_plan, us_real);
-    return rc;
+        std::fprintf(stderr,
+                     "rx n=%u threads %u/%u plan %.1f us (validate %.1f group %.1f split %.1f sim %.1f) stage+gpu %.1f "
+                     "(submit->done %.1f) real %.1f us\n",
+                     n, nr, nwg, us(t0, t1), us(t0, ta), us(ta, tb), us(tb, tc), us(tc, t1), us(t1, t2), us(ts, td),
+                     us(t2, now()));
+    return NEB_OK;
 }
 
 }  // extern "C"
