@@ -139,6 +139,72 @@ static int run(const uint32_t* d_tab, uint32_t* d_out, int blocks, int iters, in
     return 0;
 }
 
+// Pure LDS lookup stream with NS independent AES-round states per lane (NS x 16 lookups in flight
+// per round): if the rate rises with NS, one state per lane is latency-bound, not LDS-bound.
+template <int NS>
+__global__ __launch_bounds__(kThreads, 4) void ilp_kernel(uint32_t* out, int iters) {
+    __shared__ uint2 ttab[2 * 256 * 32];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    for (uint32_t i = tid; i < 2u * 256u * 32u; i += kThreads) ttab[i] = make_uint2(i * 0x9E3779B9u, i * 0x85EBCA6Bu);
+    __syncthreads();
+    const uint32_t c = lane & 31u, hi = c >> 4;
+    const uint32_t lb = ((c << 3) | (hi << 2)) | (1u << 16) | (((c << 3) | ((hi ^ 1u) << 2)) << 24);
+    uint32_t s[NS][4];
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        s[q][0] = tid * 0x01000193u + q;
+        s[q][1] = tid ^ (0xA5A5A5A5u + q);
+        s[q][2] = blockIdx.x * 0x27D4EB2Fu + tid + 7 * q;
+        s[q][3] = ~tid + q;
+    }
+    const char* tb = reinterpret_cast<const char*>(ttab);
+    for (int it = 0; it < iters; it += NS) {
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            uint32_t a[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const int col = j & 3, row = j >> 2;
+                const uint32_t w = s[q][(col + row) & 3];
+                const uint32_t sel = (row & 1 ? 0x0C000003u : 0x0C000000u) | (row & 2 ? 0x00020000u : 0x000C0000u) |
+                                     ((4u + (uint32_t)row) << 8);
+                a[j] = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(tb + perm(w, lb, sel), 4));
+            }
+#pragma unroll
+            for (int col = 0; col < 4; col++)
+                s[q][col] = x3(x3(a[col], a[col + 4], a[col + 8]), a[col + 12], 0x1B1B1B1Bu + (uint32_t)it);
+        }
+    }
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < NS; q++) r ^= s[q][0] ^ s[q][1] ^ s[q][2] ^ s[q][3];
+    out[blockIdx.x * kThreads + tid] = r;
+}
+
+template <int NS>
+static int run_ilp(uint32_t* d_out, int blocks, int iters, int cus) {
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(ilp_kernel<NS>, dim3(blocks), dim3(kThreads), 0, 0, d_out, iters);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; rep++) {
+        CHECK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL(ilp_kernel<NS>, dim3(blocks), dim3(kThreads), 0, 0, d_out, iters);
+        CHECK(hipEventRecord(e1, 0));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best) best = ms;
+    }
+    const double wave_lookups = (double)blocks * (kThreads / 64) * iters * 16.0;  // rounds total = iters
+    printf("{\"states_per_lane\": %d, \"ms\": %.4f, \"wave_lookups_per_cu_per_ns\": %.4f}\n", NS, best,
+           wave_lookups / cus / (best * 1e6));
+    fflush(stdout);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     int iters = argc > 1 ? atoi(argv[1]) : 400;
     int dev = 0, cus = 0;
@@ -153,6 +219,12 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&d_out, (size_t)blocks * kThreads * 4));
     printf("# cus=%d blocks=%d iters=%d\n", cus, blocks, iters);
     if (run<0>(d_tab, d_out, blocks, iters, cus)) return 1;
+    if (argc > 2 && argv[2][0] == 'i') {  // LDS lookup stream, 1 / 2 / 4 independent states per lane
+        if (run_ilp<1>(d_out, blocks, iters, cus) || run_ilp<2>(d_out, blocks, iters, cus) ||
+            run_ilp<4>(d_out, blocks, iters, cus))
+            return 1;
+        return 0;
+    }
     if (argc > 2) {  // valu only
         if (run_valu<4>(d_out, blocks, iters, cus)) return 1;
         return run_valu<8>(d_out, blocks, iters, cus);
