@@ -78,6 +78,13 @@ def cpu_baseline(b, target_s: float = 6.0):
     assert (st == 0).all()
     payload = float(desc["len"].astype(np.int64).sum())
     gibs = 2 * payload * iters / (t_seal + t_open) / GIB
+    # one thread too (SURVEY.md §8d asks for 1 and n threads): about 1.5 s each way
+    t1s, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=1, iters=1)
+    it1 = max(1, int(1.5 / max(t1s, 1e-5)))
+    t1_seal, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=1, iters=it1)
+    t1_open, st = oracle.evp_batch(b.alg, 1, keys, od, big, threads=1, iters=it1)
+    assert (st == 0).all()
+    gibs1 = 2 * payload * it1 / (t1_seal + t1_open) / GIB
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -88,6 +95,7 @@ def cpu_baseline(b, target_s: float = 6.0):
         pass
     return {
         "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "value_1thread": round(gibs1, 3),
         "sample": f"{n} x {int(desc['len'][0])} B packets of the same batch, seal x{iters} + open x{iters} "
                   f"({t_seal + t_open:.1f} s), OpenSSL EVP {'AES-256-GCM' if b.alg == 1 else 'ChaCha20-Poly1305'} "
                   f"(AES-NI/PCLMUL class, as Go's crypto/cipher), {threads} pinned threads on {model}",

@@ -253,7 +253,9 @@ typedef struct neb_tx_wire {
  * and segmented exactly as decodeRead + SegmentSuperpacket do (TSO: per-segment seq, CWR/FIN/PSH,
  * IPv4 ID and lengths, IPv4 and TCP checksums; USO: lengths and UDP checksum; plain packets with
  * NEEDS_CSUM get FinishChecksum), each segment takes the next counter of its tunnel in batch order,
- * gets header.Encode(Message, remote_index, counter) and is sealed in place: wires[i] describes the
+ * gets header.Encode(Message, remote_index, counter) and is sealed into its output slot (the seal
+ * reads the payload straight from d_in, which must stay valid until the stream has run the batch;
+ * only the patched L3/L4 headers are written into the slot first): wires[i] describes the
  * i-th segment of the batch (packet order, then segment order), wire_status[i] is its seal status
  * (NEB_STATUS_EXHAUSTED = dropped, inside.go:137-145, its counter still used). The segment count is
  * written to *d_nwires. Device pointers; asynchronous on `stream`. tunnels[].message_counter is
