@@ -206,6 +206,22 @@ NEB_API int neb_window_reset_counters(neb_window* w);
 NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* windows, uint32_t nwindows,
                                    const neb_desc* desc, uint32_t n, uint8_t* arena, size_t arena_len,
                                    int32_t* status, uint32_t key_hint);
+/* Replay windows in device memory, for receive batches that stay on the device (neb_rx_open_batch).
+ * A set holds `count` windows of one power-of-two length, all absent at creation. load copies a
+ * host window's state into slot idx (NULL: the slot becomes absent); store copies slot idx back
+ * into a host window of the same length (NEB_ERR_INVALID for an absent slot). Synchronous. */
+typedef struct neb_dwindows neb_dwindows;
+NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, neb_dwindows** out);
+NEB_API int neb_dwindows_destroy(neb_dwindows* d);
+NEB_API int neb_dwindows_load(neb_dwindows* d, uint32_t idx, const neb_window* w);
+NEB_API int neb_dwindows_store(neb_dwindows* d, uint32_t idx, neb_window* w);
+/* neb_rx_open_batch_host over a device-resident batch (device descriptors, arena and statuses),
+ * with the windows of `d` (slot desc.key_id; absent or out of range → NEB_STATUS_BAD_KEY): the
+ * same statuses, arena bytes, window contents and counters as Decrypt packet by packet. Runs on
+ * `stream` and returns when the batch is done (it reads back which windows need the exact
+ * sequential finish: those where a tag failed, or counters within 2^62 of wrapping). */
+NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb_desc* d_desc, uint32_t n,
+                              uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream);
 /* ---- transmit: TUN reads (IP packets, TSO/USO superpackets) -> sealed wire packets ------------ */
 /* virtio_net_hdr values (linux/virtio_net.h), as the TUN hands them over (overlay/tio/virtio/header_linux.go) */
 #define NEB_VNET_F_NEEDS_CSUM 1

@@ -82,6 +82,11 @@ SIGNATURES = {
     "neb_window_slot": (_i, [_vp, _u64]),
     "neb_window_reset_counters": (_i, [_vp]),
     "neb_rx_open_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _u32]),
+    "neb_dwindows_create": (_i, [_vp, _u32, _u64, _vp]),
+    "neb_dwindows_destroy": (_i, [_vp]),
+    "neb_dwindows_load": (_i, [_vp, _u32, _vp]),
+    "neb_dwindows_store": (_i, [_vp, _u32, _vp]),
+    "neb_rx_open_batch": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
     "neb_tx_seal_batch": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
     "neb_tx_seal_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _vp, _u32, _vp, _vp,
                                     _u32]),

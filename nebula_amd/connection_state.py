@@ -167,4 +167,49 @@ def rx_open_batch(engine, alg: int, windows: Sequence[Optional[Bits]], desc: np.
     return status
 
 
-__all__ = ["Bits", "NewBits", "ConnectionState", "ReplayWindow", "ErrAlreadySeen", "ErrOpen", "rx_open_batch"]
+class DeviceWindows:
+    """A set of replay windows in device memory (neb_dwindows_*), slot = the tunnel's key_id, for
+    receive batches that stay on the device (rx_open_batch_device). load/store copy one window's
+    whole state between a host Bits and a slot."""
+
+    def __init__(self, engine, count: int, length: int = ReplayWindow):
+        self._lib = L.lib()
+        h = C.c_void_p()
+        L.check(self._lib.neb_dwindows_create(engine.handle, count, length, C.byref(h)), "neb_dwindows_create")
+        self._h = h
+        self.count, self.length = count, length
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def load(self, idx: int, w: Optional[Bits]) -> None:
+        L.check(self._lib.neb_dwindows_load(self._h, idx, w.handle if w is not None else None), "neb_dwindows_load")
+
+    def store(self, idx: int, w: Bits) -> None:
+        L.check(self._lib.neb_dwindows_store(self._h, idx, w.handle), "neb_dwindows_store")
+
+    def destroy(self) -> None:
+        if self._h:
+            self._lib.neb_dwindows_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def rx_open_batch_device(engine, alg: int, windows: DeviceWindows, d_desc, d_arena, d_status,
+                         key_hint: int = L.KEYS_MIXED, stream=None) -> None:
+    """Batched receive over a device-resident batch (torch tensors: descriptors as uint8 bytes,
+    arena, int32 statuses): neb_rx_open_batch. Returns when the batch is done."""
+    n = d_desc.numel() // L.DESC_DTYPE.itemsize
+    rc = L.lib().neb_rx_open_batch(engine.handle, alg, windows.handle, d_desc.data_ptr(), n, d_arena.data_ptr(),
+                                   d_status.data_ptr(), key_hint, stream)
+    L.check(rc, "neb_rx_open_batch")
+
+
+__all__ = ["Bits", "NewBits", "ConnectionState", "ReplayWindow", "ErrAlreadySeen", "ErrOpen", "rx_open_batch",
+           "DeviceWindows", "rx_open_batch_device"]

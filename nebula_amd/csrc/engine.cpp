@@ -653,6 +653,24 @@ NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint3
     return batch_device(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, stream);
 }
 
+// ---- for the device batched receive (window.cpp, rxwin.hip); internal ------------------------
+
+int neb_engine_device_of(const neb_engine* e) { return e->device; }
+int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint) { return check_batch(e, alg, key_hint); }
+
+// Open the first *d_n (a count in device memory) of at most n descriptors, on stream s.
+int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s) {
+    if (n == 0) return NEB_OK;
+    hipError_t err = launch_batch(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, s, d_n);
+    if (err == hipSuccess) err = note_inflight(e, s);
+    if (err != hipSuccess) {
+        set_error("batch launch", err);
+        return NEB_ERR_HIP;
+    }
+    return NEB_OK;
+}
+
 // True if p is pinned host memory the device addresses at the same pointer (hipHostMalloc).
 static bool host_mapped(const void* p) {
     hipPointerAttribute_t a{};

@@ -1,0 +1,120 @@
+// rxwin.hpp — device replay windows and the workspace of the device batched receive (rxwin.hip),
+// shared with window.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/nebula_aead.h"
+
+namespace neb {
+
+// A window whose counters come this close to 2^64 takes the sequential path (no uint64 wrap in
+// the parallel form). No sender reaches it: counters stop at RejectAfterMessages = 2^64 - 2^40 - 1,
+// and 2^62 messages is far beyond any tunnel's life; forged counters may, and are then exact too.
+constexpr uint64_t kRxRiskyCounter = 1ull << 62;
+enum : uint32_t { kRxTouched = 1u, kRxRisky = 2u, kRxSlow = 4u };
+
+struct RxDevWin {  // a set of windows of one length in device memory (neb_dwindows)
+    uint32_t count;
+    uint32_t words;     // bitmap words per window
+    uint64_t length;    // power of two
+    uint32_t* present;  // 0 = no window at this index
+    uint64_t* cur;
+    int64_t* lost;
+    int64_t* dupe;
+    int64_t* oow;
+    uint64_t* bits;     // count x words
+};
+
+struct RxDevWs {
+    // per packet (arrival index)
+    uint32_t* keyw;  // window, or count for none
+    uint32_t* idx;
+    uint64_t* ctr;
+    uint8_t* first;
+    uint8_t* adm;
+    int32_t* verdict;
+    // run order (sorted by window, arrival order kept)
+    uint32_t* run_w;
+    uint32_t* run_i;
+    uint64_t* run_c;
+    uint64_t* incl;  // segmented inclusive max of the counters
+    // sorted by counter, then stably by window
+    uint64_t* c_s;
+    uint32_t* i_c;
+    uint32_t* w_c;
+    uint32_t* w_cw;
+    uint32_t* i_cw;
+    // admitted packets, compacted
+    uint32_t* sub_map;
+    neb_desc* sub_desc;
+    int32_t* sub_status;
+    uint32_t* nsub;
+    // per window
+    uint32_t* wflag;
+    uint32_t* rstart;
+    uint32_t* rend;
+    uint64_t* curnew;
+    uint64_t* exit_lo;
+    uint64_t* exit_hi;
+    uint64_t* recv;
+    uint64_t* scratch;  // count x words
+    void* cub_tmp;
+    size_t cub_bytes;
+};
+
+inline size_t rx_align(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Carve an RxDevWs for n packets over `count` windows of `words` bitmap words out of base
+// (nullptr: only size it). Returns the bytes needed.
+inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, size_t cub_bytes, uint8_t* base, RxDevWs* ws) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        uint8_t* p = base ? base + off : nullptr;
+        off += rx_align(std::max<size_t>(bytes, 1));
+        return p;
+    };
+    RxDevWs w{};
+    w.keyw = (uint32_t*)take((size_t)n * 4);
+    w.idx = (uint32_t*)take((size_t)n * 4);
+    w.ctr = (uint64_t*)take((size_t)n * 8);
+    w.first = (uint8_t*)take(n);
+    w.adm = (uint8_t*)take(n);
+    w.verdict = (int32_t*)take((size_t)n * 4);
+    w.run_w = (uint32_t*)take((size_t)n * 4);
+    w.run_i = (uint32_t*)take((size_t)n * 4);
+    w.run_c = (uint64_t*)take((size_t)n * 8);
+    w.incl = (uint64_t*)take((size_t)n * 8);
+    w.c_s = (uint64_t*)take((size_t)n * 8);
+    w.i_c = (uint32_t*)take((size_t)n * 4);
+    w.w_c = (uint32_t*)take((size_t)n * 4);
+    w.w_cw = (uint32_t*)take((size_t)n * 4);
+    w.i_cw = (uint32_t*)take((size_t)n * 4);
+    w.sub_map = (uint32_t*)take((size_t)n * 4);
+    w.sub_desc = (neb_desc*)take((size_t)n * sizeof(neb_desc));
+    w.sub_status = (int32_t*)take((size_t)n * 4);
+    w.nsub = (uint32_t*)take(4);
+    w.wflag = (uint32_t*)take((size_t)count * 4);
+    w.rstart = (uint32_t*)take((size_t)count * 4);
+    w.rend = (uint32_t*)take((size_t)count * 4);
+    w.curnew = (uint64_t*)take((size_t)count * 8);
+    w.exit_lo = (uint64_t*)take((size_t)count * 8);
+    w.exit_hi = (uint64_t*)take((size_t)count * 8);
+    w.recv = (uint64_t*)take((size_t)count * 8);
+    w.scratch = (uint64_t*)take((size_t)count * words * 8);
+    w.cub_tmp = take(cub_bytes);
+    w.cub_bytes = cub_bytes;
+    if (ws) *ws = w;
+    return off;
+}
+
+}  // namespace neb
+
+extern "C" size_t neb_rxdev_cub_bytes(uint32_t n);
+extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const neb::RxDevWin* win,
+                                     const neb::RxDevWs* ws, int32_t* d_status, hipStream_t s);
+extern "C" hipError_t neb_rxdev_compact(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
+extern "C" hipError_t neb_rxdev_finish(uint32_t n, const neb::RxDevWin* win, const neb::RxDevWs* ws,
+                                       int32_t* d_status, hipStream_t s);

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../../include/nebula_aead.h"
+#include "rxwin.hpp"
 
 // engine.cpp
 bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len);
@@ -44,6 +45,10 @@ int neb_rx_pipe_submit(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena
                        uint32_t k);
 int neb_rx_pipe_wait(neb_engine* e, uint32_t k);
 void neb_rx_pipe_end(neb_engine* e);
+int neb_engine_device_of(const neb_engine* e);
+int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint);
+int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s);
 }
 
 namespace {
@@ -481,6 +486,272 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
                      "(submit->done %.1f) real %.1f us\n",
                      n, nr, nwg, us(t0, t1), us(t0, ta), us(ta, tb), us(tb, tc), us(tc, t1), us(t1, t2), us(ts, td),
                      us(t2, now()));
+    return NEB_OK;
+}
+
+// ---- replay windows in device memory (rxwin.hip) ----------------------------------------------
+
+}  // extern "C"
+
+struct neb_dwindows {
+    neb_engine* e = nullptr;
+    neb::RxDevWin win{};
+    uint8_t* mem = nullptr;
+    std::mutex mu;  // one receive batch at a time on a window set
+    uint8_t* ws_mem = nullptr;
+    size_t ws_bytes = 0;
+    neb::RxDevWs ws{};
+    uint32_t ws_n = 0;
+};
+
+namespace {
+
+#define RX_HIP(x)                               \
+    do {                                        \
+        if ((x) != hipSuccess) return NEB_ERR_HIP; \
+    } while (0)
+
+// Device slot w <-> a WindowCore (same length and word packing)
+int dw_read(const neb_dwindows* d, uint32_t w, WindowCore& c) {
+    const auto& v = d->win;
+    c.length = v.length;
+    c.mask = v.length - 1;
+    c.words.resize(v.words);
+    RX_HIP(hipMemcpy(&c.current, v.cur + w, 8, hipMemcpyDeviceToHost));
+    RX_HIP(hipMemcpy(&c.lost, v.lost + w, 8, hipMemcpyDeviceToHost));
+    RX_HIP(hipMemcpy(&c.dupe, v.dupe + w, 8, hipMemcpyDeviceToHost));
+    RX_HIP(hipMemcpy(&c.out_of_window, v.oow + w, 8, hipMemcpyDeviceToHost));
+    RX_HIP(hipMemcpy(c.words.data(), v.bits + (size_t)w * v.words, (size_t)v.words * 8, hipMemcpyDeviceToHost));
+    return NEB_OK;
+}
+int dw_write(neb_dwindows* d, uint32_t w, const WindowCore& c) {
+    const auto& v = d->win;
+    const uint32_t one = 1;
+    RX_HIP(hipMemcpy(v.cur + w, &c.current, 8, hipMemcpyHostToDevice));
+    RX_HIP(hipMemcpy(v.lost + w, &c.lost, 8, hipMemcpyHostToDevice));
+    RX_HIP(hipMemcpy(v.dupe + w, &c.dupe, 8, hipMemcpyHostToDevice));
+    RX_HIP(hipMemcpy(v.oow + w, &c.out_of_window, 8, hipMemcpyHostToDevice));
+    RX_HIP(hipMemcpy(v.bits + (size_t)w * v.words, c.words.data(), (size_t)v.words * 8, hipMemcpyHostToDevice));
+    RX_HIP(hipMemcpy(v.present + w, &one, 4, hipMemcpyHostToDevice));
+    return NEB_OK;
+}
+
+template <class T>
+int d2h(std::vector<T>& h, const T* d, size_t n, hipStream_t s) {
+    h.resize(n);
+    if (n) RX_HIP(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    return NEB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, neb_dwindows** out) {
+    if (!e || !out || count == 0 || length == 0 || (length & (length - 1)) || length > (1ull << 24))
+        return NEB_ERR_INVALID;
+    *out = nullptr;
+    hipSetDevice(neb_engine_device_of(e));
+    neb_dwindows* d = new (std::nothrow) neb_dwindows;
+    if (!d) return NEB_ERR_INVALID;
+    d->e = e;
+    auto& v = d->win;
+    v.count = count;
+    v.length = length;
+    v.words = length >= 64 ? (uint32_t)(length / 64) : 1u;
+    const size_t b_present = neb::rx_align((size_t)count * 4), b_word = neb::rx_align((size_t)count * 8);
+    const size_t bytes = b_present + 4 * b_word + (size_t)count * v.words * 8;
+    if (hipMalloc((void**)&d->mem, bytes) != hipSuccess || hipMemset(d->mem, 0, bytes) != hipSuccess) {
+        if (d->mem) hipFree(d->mem);
+        delete d;
+        return NEB_ERR_HIP;
+    }
+    uint8_t* m = d->mem;
+    v.present = (uint32_t*)m;
+    m += b_present;
+    v.cur = (uint64_t*)m;
+    m += b_word;
+    v.lost = (int64_t*)m;
+    m += b_word;
+    v.dupe = (int64_t*)m;
+    m += b_word;
+    v.oow = (int64_t*)m;
+    m += b_word;
+    v.bits = (uint64_t*)m;
+    *out = d;
+    return NEB_OK;
+}
+
+NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
+    if (!d) return NEB_ERR_INVALID;
+    hipSetDevice(neb_engine_device_of(d->e));
+    {
+        std::lock_guard<std::mutex> g(d->mu);
+        hipDeviceSynchronize();
+        if (d->ws_mem) hipFree(d->ws_mem);
+        if (d->mem) hipFree(d->mem);
+    }
+    delete d;
+    return NEB_OK;
+}
+
+NEB_API int neb_dwindows_load(neb_dwindows* d, uint32_t idx, const neb_window* w) {
+    if (!d || idx >= d->win.count) return NEB_ERR_INVALID;
+    std::lock_guard<std::mutex> g(d->mu);
+    hipSetDevice(neb_engine_device_of(d->e));
+    if (!w) {
+        const uint32_t zero = 0;
+        RX_HIP(hipMemcpy(d->win.present + idx, &zero, 4, hipMemcpyHostToDevice));
+        return NEB_OK;
+    }
+    WindowCore c;
+    {
+        std::lock_guard<std::mutex> lk(w->mu);
+        c = w->core;
+    }
+    if (c.length != d->win.length) return NEB_ERR_INVALID;
+    return dw_write(d, idx, c);
+}
+
+NEB_API int neb_dwindows_store(neb_dwindows* d, uint32_t idx, neb_window* w) {
+    if (!d || !w || idx >= d->win.count) return NEB_ERR_INVALID;
+    std::lock_guard<std::mutex> g(d->mu);
+    hipSetDevice(neb_engine_device_of(d->e));
+    uint32_t present = 0;
+    RX_HIP(hipMemcpy(&present, d->win.present + idx, 4, hipMemcpyDeviceToHost));
+    if (!present) return NEB_ERR_INVALID;
+    WindowCore c;
+    const int rc = dw_read(d, idx, c);
+    if (rc != NEB_OK) return rc;
+    std::lock_guard<std::mutex> lk(w->mu);
+    if (w->core.length != c.length) return NEB_ERR_INVALID;
+    w->core = c;
+    return NEB_OK;
+}
+
+NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb_desc* d_desc, uint32_t n,
+                              uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream) {
+    if (!e || !d || d->e != e || (n && (!d_desc || !d_arena || !d_status))) return NEB_ERR_INVALID;
+    int rc = neb_check_batch_args(e, alg, key_hint);
+    if (rc != NEB_OK) return rc;
+    if (n == 0) return NEB_OK;
+    std::lock_guard<std::mutex> g(d->mu);
+    hipSetDevice(neb_engine_device_of(e));
+    hipStream_t s = (hipStream_t)stream;
+    auto& v = d->win;
+    if (n > d->ws_n) {
+        const size_t cub = neb_rxdev_cub_bytes(n);
+        const size_t bytes = neb::rx_ws_layout(n, v.count, v.words, cub, nullptr, nullptr);
+        RX_HIP(hipStreamSynchronize(s));
+        if (d->ws_mem) hipFree(d->ws_mem);
+        d->ws_mem = nullptr;
+        d->ws_n = 0;
+        RX_HIP(hipMalloc((void**)&d->ws_mem, bytes));
+        neb::rx_ws_layout(n, v.count, v.words, cub, d->ws_mem, &d->ws);
+        d->ws_bytes = bytes;
+        d->ws_n = n;
+    }
+    const neb::RxDevWs& ws = d->ws;
+
+    // 1. group by window, prefix maxima, first occurrences; admission for the windows safe for
+    //    the parallel form
+    RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
+    std::vector<uint32_t> flag;
+    if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
+    RX_HIP(hipStreamSynchronize(s));
+    std::vector<uint32_t> risky;
+    for (uint32_t w = 0; w < v.count; w++)
+        if (flag[w] & neb::kRxRisky) risky.push_back(w);
+    std::vector<uint32_t> run_w, run_i;
+    std::vector<uint64_t> run_c;
+    std::vector<uint8_t> adm;
+    auto fetch_runs = [&]() -> int {
+        if (!run_w.empty()) return NEB_OK;
+        if (d2h(run_w, ws.run_w, n, s) || d2h(run_i, ws.run_i, n, s) || d2h(run_c, ws.run_c, n, s) ||
+            d2h(adm, ws.adm, n, s))
+            return NEB_ERR_HIP;
+        RX_HIP(hipStreamSynchronize(s));
+        return NEB_OK;
+    };
+    // windows' packet runs in run order (sorted by window: the runs are contiguous)
+    auto runs_of = [&](const std::vector<uint32_t>& ws_list, auto&& fn) -> int {
+        size_t k = 0;
+        for (uint32_t w : ws_list) {
+            while (k < n && run_w[k] < w) k++;
+            const size_t k0 = k;
+            while (k < n && run_w[k] == w) k++;
+            const int r = fn(w, k0, k);
+            if (r != NEB_OK) return r;
+        }
+        return NEB_OK;
+    };
+    if (!risky.empty() && std::getenv("NEB_RXDEV_STRICT")) return NEB_ERR_INVALID;
+    if (!risky.empty()) {  // the sequential simulation for these windows
+        if ((rc = fetch_runs()) != NEB_OK) return rc;
+        rc = runs_of(risky, [&](uint32_t w, size_t k0, size_t k1) -> int {
+            WindowCore sim;
+            const int r = dw_read(d, w, sim);
+            if (r != NEB_OK) return r;
+            for (size_t k = k0; k < k1; k++) {
+                const bool ok = sim.check(run_c[k]);
+                if (ok) sim.update(run_c[k]);
+                adm[run_i[k]] = ok;
+            }
+            return NEB_OK;
+        });
+        if (rc != NEB_OK) return rc;
+        RX_HIP(hipMemcpyAsync(ws.adm, adm.data(), n, hipMemcpyHostToDevice, s));
+    }
+
+    // 2. one open of every admitted packet
+    RX_HIP(neb_rxdev_compact(d_desc, n, &ws, s));
+    rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, ws.sub_status, key_hint, s);
+    if (rc != NEB_OK) return rc;
+
+    // 3. the parallel finish; windows with a failed tag (or risky ones) finish here, exactly
+    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, s));
+    if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
+    RX_HIP(hipStreamSynchronize(s));
+    std::vector<uint32_t> slow;
+    for (uint32_t w = 0; w < v.count; w++)
+        if ((flag[w] & neb::kRxTouched) && (flag[w] & (neb::kRxRisky | neb::kRxSlow))) slow.push_back(w);
+    if (slow.empty()) return NEB_OK;
+    // test hook: NEB_RXDEV_STRICT=1 refuses the host finish, to prove a batch ran the parallel form
+    if (std::getenv("NEB_RXDEV_STRICT")) return NEB_ERR_INVALID;
+    run_w.clear();
+    if ((rc = fetch_runs()) != NEB_OK) return rc;
+    std::vector<int32_t> verdict, status;
+    if (d2h(verdict, ws.verdict, n, s) || d2h(status, d_status, n, s)) return NEB_ERR_HIP;
+    RX_HIP(hipStreamSynchronize(s));
+    rc = runs_of(slow, [&](uint32_t w, size_t k0, size_t k1) -> int {
+        WindowCore c;
+        int r = dw_read(d, w, c);
+        if (r != NEB_OK) return r;
+        for (size_t k = k0; k < k1; k++) {  // Check → tag verdict → Update, in arrival order
+            const uint32_t i = run_i[k];
+            const uint64_t ctr = run_c[k];
+            if (!c.check(ctr)) {
+                status[i] = NEB_STATUS_REPLAY;
+                continue;
+            }
+            int32_t st = verdict[i];
+            if (!adm[i]) {  // held back, yet the real window accepts it: an earlier copy failed its tag
+                r = neb_open_batch_count(e, alg, d_desc + i, 1, nullptr, d_arena, ws.sub_status, key_hint, s);
+                if (r != NEB_OK) return r;
+                RX_HIP(hipMemcpyAsync(&st, ws.sub_status, 4, hipMemcpyDeviceToHost, s));
+                RX_HIP(hipStreamSynchronize(s));
+            }
+            if (st != NEB_STATUS_OK) {
+                status[i] = st;
+                continue;
+            }
+            status[i] = c.update(ctr) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
+        }
+        return dw_write(d, w, c);
+    });
+    if (rc != NEB_OK) return rc;
+    RX_HIP(hipMemcpyAsync(d_status, status.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+    RX_HIP(hipStreamSynchronize(s));
     return NEB_OK;
 }
 

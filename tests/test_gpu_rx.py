@@ -2,6 +2,7 @@
 recvmmsg flush, connection_state.go:99-119) against the oracle's packet-by-packet receive loop
 (oracle/replay_oracle.py rx_sequential + oracle AEAD): statuses, every arena byte (refused packets
 untouched, forged ones zeroed, accepted ones decrypted in place), window state and counters."""
+import os
 import random
 
 import numpy as np
@@ -56,7 +57,7 @@ def _expected(oracle_mod, R, alg, keys, arrivals, arena, pts, window_len, seeds,
 
 
 def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=None, installed=None, seed=1,
-         lens=None):
+         lens=None, device=False, strict=False):
     import replay_oracle as R
     from nebula_amd.connection_state import Bits, rx_open_batch
     from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
@@ -83,7 +84,33 @@ def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=N
             windows[slot_of[t]] = w
         d = desc.copy()
         d["key_id"] = [slot_of[int(t)] for t in desc["key_id"]]
-        got = rx_open_batch(engine, alg, windows, d, arena)
+        if device:  # neb_rx_open_batch: the batch and the windows in device memory
+            import torch
+
+            from nebula_amd.connection_state import DeviceWindows, rx_open_batch_device
+            dev = torch.device("cuda", engine.device)
+            dw = DeviceWindows(engine, engine.max_keys, window_len)
+            try:
+                for t, w in ewins.items():
+                    dw.load(slot_of[t], w)
+                d_desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+                d_arena = torch.from_numpy(arena).to(dev)
+                d_status = torch.full((len(d),), -1, dtype=torch.int32, device=dev)
+                if strict:  # the parallel form only: the call fails if any window needs the host
+                    os.environ["NEB_RXDEV_STRICT"] = "1"
+                try:
+                    rx_open_batch_device(engine, alg, dw, d_desc, d_arena, d_status)
+                finally:
+                    os.environ.pop("NEB_RXDEV_STRICT", None)
+                torch.cuda.synchronize()
+                got = d_status.cpu().numpy()
+                arena[:] = d_arena.cpu().numpy()
+                for t, w in ewins.items():
+                    dw.store(slot_of[t], w)
+            finally:
+                dw.destroy()
+        else:
+            got = rx_open_batch(engine, alg, windows, d, arena)
         assert got.tolist() == exp_status
         assert np.array_equal(arena, exp_arena)
         for t, w in ewins.items():
@@ -110,23 +137,47 @@ ARRIVALS = [
 ]
 
 
+@pytest.mark.parametrize("device", [False, True])
 @pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
-def test_rx_batch_matches_sequential_decrypt(engine, oracle_mod, alg):
-    st = _run(engine, oracle_mod, alg, ARRIVALS)
+def test_rx_batch_matches_sequential_decrypt(engine, oracle_mod, alg, device):
+    st = _run(engine, oracle_mod, alg, ARRIVALS, device=device)
     assert (st == L.STATUS_REPLAY).sum() >= 5 and (st == L.STATUS_AUTH_FAILED).sum() >= 3
 
 
-def test_rx_batch_missing_window_and_key(engine, oracle_mod):
+@pytest.mark.parametrize("device", [False, True])
+def test_rx_batch_missing_window_and_key(engine, oracle_mod, device):
     """Tunnel 2 has no window (no ConnectionState): BAD_KEY, untouched. Tunnel 1's key is not
     installed: its window passes the packet, the engine refuses the key, the window is not updated."""
     arr = [(0, 3, False), (2, 3, False), (1, 3, False), (1, 4, False), (0, 4, False)]
-    st = _run(engine, oracle_mod, L.ALG_AESGCM, arr, seeds={0: 2, 1: 2}, installed={0, 2})
+    st = _run(engine, oracle_mod, L.ALG_AESGCM, arr, seeds={0: 2, 1: 2}, installed={0, 2}, device=device)
     assert st.tolist() == [0, L.STATUS_BAD_KEY, L.STATUS_BAD_KEY, L.STATUS_BAD_KEY, 0]
 
 
-def test_rx_batch_random_traffic(engine, oracle_mod):
+def _random_arrivals(rng, n, ntun, forge, jump=40):
+    cur = [2] * ntun
+    arr = []
+    for _ in range(n):
+        t = rng.randrange(ntun)
+        r = rng.random()
+        if r < 0.6:
+            cur[t] += 1 + (rng.random() < 0.1) * rng.randrange(1, jump)
+            c = cur[t]
+        elif r < 0.85:
+            c = max(1, cur[t] - rng.randrange(0, 80))
+        else:
+            c = cur[t] + rng.randrange(1, 30)
+        arr.append((t, c, rng.random() < forge))
+    return arr
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_rx_batch_random_traffic(engine, oracle_mod, device):
     """A long random receive stream over 8 tunnels and a small window: loss, reordering, jumps,
     replays and forgeries, checked packet by packet against the sequential oracle."""
+    if device:
+        arr = _random_arrivals(random.Random(7), 3000, 8, 0.05)
+        _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=8, window_len=64, seed=3, device=True)
+        return
     rng = random.Random(7)
     cur = [2] * 8
     arr = []
@@ -144,10 +195,11 @@ def test_rx_batch_random_traffic(engine, oracle_mod):
     _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=8, window_len=64, seed=3)
 
 
-def test_rx_batch_pipelined_chunks(engine, oracle_mod):
-    """A receive batch long enough to be opened in several pipelined chunks (window.cpp: the next
-    chunk's simulation and the previous chunk's window pass overlap the GPU): duplicates, replays
-    and forged-then-genuine copies straddle the chunk boundaries."""
+@pytest.mark.parametrize("device", [False, True])
+def test_rx_batch_large(engine, oracle_mod, device):
+    """A 20 000-packet receive batch over 6 tunnels (the host pool's per-window split; on the
+    device, windows with forgeries take the exact sequential finish): duplicates, replays and
+    forged-then-genuine copies."""
     rng = random.Random(13)
     cur = [2] * 6
     arr = []
@@ -166,7 +218,37 @@ def test_rx_batch_pipelined_chunks(engine, oracle_mod):
             cur[t] += 1
             arr.append((t, cur[t], True))
             arr.append((t, cur[t], False))
-    _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=6, window_len=256, seed=5, lens=[0, 1, 16, 40, 100])
+    _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=6, window_len=256, seed=5, lens=[0, 1, 16, 40, 100],
+         device=device)
+
+
+@pytest.mark.parametrize("length", [1, 64, 256, 8192])
+def test_rx_device_parallel_form(engine, oracle_mod, length):
+    """Device windows, no forgeries: every window finishes on the device's parallel form (prefix
+    maxima, first occurrences, per-slot bitmap and lost counts), over warmup, steady state, jumps
+    past the window, reordering and in-batch duplicates."""
+    rng = random.Random(length)
+    arr = _random_arrivals(rng, 6000, 5, 0.0, jump=3 * length + 2)
+    _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=5, window_len=length, seed=9, lens=[0, 16, 60],
+         seeds={0: 2, 1: 2, 2: 2, 3: 2, 4: 2}, device=True, strict=True)
+
+
+def test_rx_device_one_big_window(engine, oracle_mod):
+    """One tunnel, 20 000 packets in one window run (the C2 shape): the parallel form only."""
+    rng = random.Random(77)
+    arr = _random_arrivals(rng, 20000, 1, 0.0)
+    _run(engine, oracle_mod, L.ALG_CHACHAPOLY, arr, ntunnels=1, window_len=8192, seed=4, lens=[0, 16, 90],
+         device=True, strict=True)
+
+
+def test_rx_device_counters_near_wrap(engine, oracle_mod):
+    """Counters at and beyond 2^62 (a window's current and packets near 2^64): those windows take
+    the exact sequential path on the host, the others the parallel form, in one batch."""
+    big = 1 << 62
+    arr = [(0, 3, False), (1, big + 5, False), (1, big + 3, False), (1, big + 5, False),
+           (2, 2**64 - 3, False), (2, 2**64 - 1, True), (2, 2**64 - 1, False), (2, 5, False),
+           (0, 4, False), (0, 4, False), (1, big - 1, False)]
+    _run(engine, oracle_mod, L.ALG_AESGCM, arr, device=True)
 
 
 def test_rx_batch_invalid_descriptor_touches_nothing(engine, oracle_mod):
