@@ -132,13 +132,15 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
-    ap.add_argument("--mode", choices=["device", "host", "host-kcopy", "host-staged", "host-split", "tx", "rx"],
+    ap.add_argument("--mode", choices=["device", "host", "host-kcopy", "host-staged", "host-split", "tx", "rx",
+                                       "rx-device"],
                     default="device",
                     help="device: the headline; host: host-resident batch (pinned arena: zero-copy); "
                          "host-kcopy: the pinned arena staged by span-copy kernels; "
                          "host-staged: the same through hipMemcpyAsync staging; host-split: sources DMA-staged, "
                          "outputs stored by the kernel into the pinned arena; tx: the device TX batch "
-                         "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows")
+                         "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows; "
+                         "rx-device: the same with the batch and the windows in device memory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -224,6 +226,8 @@ def main():
         return bench_tx(args, eng, ctrl, rank, world)
     if args.mode == "rx":
         return bench_rx(args, eng, b, ciphers, ctrl, rank, world)
+    if args.mode == "rx-device":
+        return bench_rx_device(args, eng, b, ciphers, ctrl, rank, world)
 
     db = DeviceBatch(eng, b, ciphers)
     stream = torch.cuda.current_stream()
@@ -416,6 +420,61 @@ def bench_rx(args, eng, b, ciphers, ctrl, rank, world):
             "warmup": args.warmup, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
             "open_only_gibs": round(payload / times["open"] / GIB, 3),
             "config": {"workload": f"{b.name}: {b.n} packets, {b.nkeys} tunnel(s), host pinned arena"},
+        }), flush=True)
+
+
+def bench_rx_device(args, eng, b, ciphers, ctrl, rank, world):
+    """Batched receive with the batch and the replay windows in device memory (neb_rx_open_batch)
+    against the plain device open of the same batch. Every step receives the next batch of the
+    same tunnels (counters advanced by n, re-sealed untimed), so every packet passes its window."""
+    import torch
+
+    from nebula_amd import _lib as L
+    from nebula_amd.batch import DeviceBatch
+    from nebula_amd.connection_state import Bits, DeviceWindows, ReplayWindow, rx_open_batch_device
+
+    db = DeviceBatch(eng, b, ciphers)
+    pt = db.arena.clone()
+    base = db.desc_host.copy()
+    dw = DeviceWindows(eng, eng.max_keys, ReplayWindow)
+    for c in ciphers:
+        w = Bits(ReplayWindow)
+        w.Update(1)
+        w.Update(2)
+        dw.load(c.key_id, w)
+    times = {"rx": 0.0, "open": 0.0}
+    for it in range(args.warmup + args.steps):
+        d = base.copy()
+        d["counter"] = d["counter"] + np.uint64(it * b.n)
+        db.desc.copy_(torch.from_numpy(d.view(np.uint8)))
+        for mode in ("open", "rx"):
+            db.arena.copy_(pt)
+            db.seal()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if mode == "rx":
+                rx_open_batch_device(eng, b.alg, dw, db.desc, db.arena, db.status, db.key_hint,
+                                     torch.cuda.current_stream().cuda_stream)
+            else:
+                db.open()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            st = db.status_host()
+            assert (st == 0).all(), (mode, np.unique(st))
+            if it >= args.warmup:
+                times[mode] += el
+    dw.destroy()
+    if rank == 0:
+        payload = float(b.payload_bytes) * args.steps
+        print(json.dumps({
+            "metric": "GiB/s device-resident batched receive (replay windows in HBM: Check -> open -> Update)",
+            "value": round(payload / times["rx"] / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+            "ms_per_step": round(times["rx"] / args.steps * 1e3, 4),
+            "open_only_gibs": round(payload / times["open"] / GIB, 3),
+            "open_only_ms": round(times["open"] / args.steps * 1e3, 4),
+            "config": {"workload": f"{b.name}: {b.n} packets, {b.nkeys} tunnel(s), device-resident, "
+                                   f"windows of {ReplayWindow}"},
         }), flush=True)
 
 

@@ -59,33 +59,46 @@ __global__ void rx_runs_kernel(uint32_t n, RxDevWin win, RxDevWs ws) {
     const uint64_t c = ws.ctr[i];
     ws.run_c[k] = c;
     if (w >= win.count) return;
-    uint32_t fl = kRxTouched;
-    if (c >= kRxRiskyCounter) fl |= kRxRisky;
+    // flag words are written by the run's head and by risky packets only (one window's whole batch
+    // on one address would serialise)
+    uint32_t fl = c >= kRxRiskyCounter ? kRxRisky : 0u;
     if (k == 0u || ws.run_w[k - 1u] != w) {
         ws.rstart[w] = k;
-        if (win.cur[w] >= kRxRiskyCounter) fl |= kRxRisky;
+        fl |= kRxTouched | (win.cur[w] >= kRxRiskyCounter ? kRxRisky : 0u);
     }
     if (k + 1u == n || ws.run_w[k + 1u] != w) ws.rend[w] = k + 1u;
-    atomicOr(&ws.wflag[w], fl);
+    if (fl) atomicOr(&ws.wflag[w], fl);
 }
 
-__global__ void rx_gather_w_kernel(uint32_t n, RxDevWs ws) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) ws.w_c[j] = ws.keyw[ws.i_c[j]];
+__device__ __forceinline__ uint32_t rx_hash(uint32_t w, uint64_t c, uint32_t lg) {
+    uint64_t h = (c ^ ((uint64_t)w << 40) ^ w) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    return (uint32_t)(h >> (64 - lg));
 }
 
-// first occurrence of (window, counter) in arrival order: the batch sorted by counter, then
-// stably by window, keeps arrival order among equal pairs
-__global__ void rx_first_kernel(uint32_t n, RxDevWs ws) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t i = ws.i_cw[j];
-    bool first = true;
-    if (j > 0u) {
-        const uint32_t q = ws.i_cw[j - 1u];
-        first = ws.w_cw[j - 1u] != ws.w_cw[j] || ws.ctr[q] != ws.ctr[i];
+// the slot of packet i's (window, counter) key: claimed by the first to arrive at it, found by
+// comparing the owner's key (exact, no hash comparison); the table has at least 2n slots
+__device__ __forceinline__ uint32_t rx_slot(const RxDevWs& ws, uint32_t i, bool insert) {
+    const uint32_t w = ws.keyw[i];
+    const uint64_t c = ws.ctr[i];
+    const uint32_t tmask = (1u << ws.tab_lg) - 1u;
+    uint32_t h = rx_hash(w, c, ws.tab_lg);
+    for (;;) {
+        const uint32_t o = insert ? atomicCAS(&ws.tab_owner[h], 0u, i + 1u) : ws.tab_owner[h];
+        if (o == 0u) return h;  // claimed (insert); a lookup always finds its own key first
+        if (o == i + 1u || (ws.keyw[o - 1u] == w && ws.ctr[o - 1u] == c)) return h;
+        h = (h + 1u) & tmask;
     }
-    ws.first[i] = first;
+}
+
+__global__ void rx_first_insert_kernel(uint32_t n, RxDevWs ws) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicMin(&ws.tab_min[rx_slot(ws, i, true)], i);
+}
+
+__global__ void rx_first_kernel(uint32_t n, RxDevWs ws) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ws.first[i] = ws.tab_min[rx_slot(ws, i, false)] == i;
 }
 
 // which packets the sequential receive would decrypt, if every tag verified (safe windows)
@@ -102,7 +115,7 @@ __global__ void rx_admit_kernel(uint32_t n, RxDevWin win, RxDevWs ws, int32_t* _
     const uint64_t cur0 = win.cur[w];
     const uint64_t prev = k == ws.rstart[w] ? cur0 : max(cur0, ws.incl[k - 1u]);
     const uint64_t c = ws.run_c[k];
-    const uint64_t* bits = win.bits + (size_t)w * win.words;
+    const uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
     bool ok = c > prev;
     if (!ok && rx_in_window(c, prev, win.length)) ok = !(c <= cur0 && rx_bit(bits, win.length - 1u, c));
     ws.adm[i] = ok && ws.first[i];
@@ -139,61 +152,101 @@ __global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
 
 __global__ void rx_zero_scratch_kernel(RxDevWin win, RxDevWs ws) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (size_t)win.count * win.words) return;
-    if (rx_fast(ws.wflag[t / win.words])) ws.scratch[t] = 0;
+    if (t >= ((size_t)win.count << win.words_lg)) return;
+    if (rx_fast(ws.wflag[t >> win.words_lg])) ws.scratch[t] = 0;
 }
 
-// per packet of a fast window: status, admitted counters into the scratch bitmap, received exits
-__global__ void rx_final_packet_kernel(uint32_t n, RxDevWin win, RxDevWs ws, int32_t* __restrict__ status) {
+// per packet of a fast window: its status; its counter into the scratch bitmap, and into the
+// received count when it leaves the window — one atomic per (wave, window, word) instead of one per packet: a
+// single tunnel's batch would otherwise serialise tens of thousands of atomics on one address.
+// Every lane runs to the end (the shuffles need the whole wave).
+__global__ void rx_final_packet_agg_kernel(uint32_t n, RxDevWin win, RxDevWs ws, int32_t* __restrict__ status) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const uint32_t w = ws.run_w[k];
-    if (w >= win.count || !rx_fast(ws.wflag[w])) return;
-    const uint32_t i = ws.run_i[k];
-    if (!ws.adm[i]) {
-        status[i] = NEB_STATUS_REPLAY;
-        return;
-    }
-    status[i] = NEB_STATUS_OK;
-    const uint64_t c = ws.run_c[k], cur = ws.curnew[w], len = win.length;
-    if (cur < len || c > cur - len) {  // still inside the final window
-        const uint64_t p = c & (len - 1u);
-        atomicOr(reinterpret_cast<unsigned long long*>(ws.scratch + (size_t)w * win.words + (p >> 6)),
-                 1ull << (p & 63));
-    }
-    if (c >= ws.exit_lo[w] && c <= ws.exit_hi[w]) atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), 1ull);
-}
-
-// per bitmap word of a fast window: the final bits, and how many leaving counters were received
-// before the batch
-__global__ void rx_final_word_kernel(RxDevWin win, RxDevWs ws) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (size_t)win.count * win.words) return;
-    const uint32_t w = (uint32_t)(t / win.words), q = (uint32_t)(t % win.words);
-    if (!rx_fast(ws.wflag[w])) return;
-    const uint64_t len = win.length, mask = len - 1u, cur0 = win.cur[w], cur = ws.curnew[w];
-    const uint64_t lo = ws.exit_lo[w], hi = min(ws.exit_hi[w], cur0);
-    const uint64_t old = win.bits[t], adm = ws.scratch[t];
-    const uint32_t nb = len < 64u ? (uint32_t)len : 64u;
-    uint64_t out = old;
-    uint64_t recv_old = 0;
-    for (uint32_t b = 0; b < nb; b++) {
-        const uint64_t s = (uint64_t)q * 64u + b;
-        const uint64_t ob = (old >> b) & 1u;
-        // the counter slot s held before the batch, and the one it holds after
-        bool has_old = true, has_new = true;
-        const uint64_t e_old = cur0 >= len ? cur0 - ((cur0 - s) & mask) : s;
-        if (cur0 < len && s > cur0) has_old = false;
-        const uint64_t c_new = cur >= len ? cur - ((cur - s) & mask) : s;
-        if (cur < len && s > cur) has_new = false;  // warmup: untouched above current
-        if (has_old && ob && e_old >= lo && e_old <= hi) recv_old++;
-        if (has_new) {
-            const uint64_t nbit = (c_new <= cur0 ? ob : 0u) | ((adm >> b) & 1u);
-            out = (out & ~(1ull << b)) | (nbit << b);
+    uint32_t w = win.count;
+    uint64_t c = 0;
+    bool adm = false;
+    if (k < n) {
+        w = ws.run_w[k];
+        if (w < win.count && rx_fast(ws.wflag[w])) {
+            const uint32_t i = ws.run_i[k];
+            adm = ws.adm[i];
+            status[i] = adm ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
+            c = ws.run_c[k];
+        } else {
+            w = win.count;
         }
     }
-    win.bits[t] = out;
-    if (recv_old) atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)recv_old);
+    uint64_t cur = 0, lo = 1, hi = 0;
+    if (adm) {
+        cur = ws.curnew[w];
+        lo = ws.exit_lo[w];
+        hi = ws.exit_hi[w];
+    }
+    const uint64_t len = win.length;
+    const bool in_final = adm && (cur < len || c > cur - len);
+    const bool leaves = adm && c >= lo && c <= hi;
+    const uint64_t p = c & (len - 1u);
+    // word key of this lane's bit; lanes of one (window, word) OR their bits into one atomic
+    const uint64_t wkey = in_final ? (((uint64_t)w << 32) | (p >> 6)) : ~0ull;
+    uint64_t pending = __ballot(in_final);
+    while (pending) {
+        const uint32_t leader = __builtin_ctzll(pending);
+        const uint64_t lk = __shfl(wkey, (int)leader);
+        const bool mine = in_final && wkey == lk;
+        uint64_t bits = mine ? 1ull << (p & 63) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
+        if (__lane_id() == leader)
+            atomicOr(reinterpret_cast<unsigned long long*>(ws.scratch + ((size_t)w << win.words_lg) + (p >> 6)), bits);
+        pending &= ~__ballot(mine);
+    }
+    uint64_t pend2 = __ballot(leaves);
+    while (pend2) {
+        const uint32_t leader = __builtin_ctzll(pend2);
+        const uint32_t lw = __shfl(w, (int)leader);
+        const uint64_t same = __ballot(leaves && w == lw);
+        if (__lane_id() == leader)
+            atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)__popcll(same));
+        pend2 &= ~same;
+    }
+}
+
+// bits of the slots [a, b) within the word whose first slot is q0 (nb slots)
+__device__ __forceinline__ uint64_t rx_seg_mask(uint64_t q0, uint32_t nb, uint64_t a, uint64_t b) {
+    const uint64_t lo = max(a, q0), hi = min(b, q0 + nb);
+    if (lo >= hi) return 0;
+    const uint32_t m = (uint32_t)(hi - lo);
+    return (m == 64u ? ~0ull : ((1ull << m) - 1u)) << (lo - q0);
+}
+// ... within the circular slot range [start, start + count) mod len (start < len)
+__device__ __forceinline__ uint64_t rx_ring_mask(uint64_t q0, uint32_t nb, uint64_t start, uint64_t count,
+                                                 uint64_t len) {
+    if (count == 0) return 0;
+    if (count >= len) return nb == 64u ? ~0ull : ((1ull << nb) - 1u);
+    uint64_t m = rx_seg_mask(q0, nb, start, min(start + count, len));
+    if (start + count > len) m |= rx_seg_mask(q0, nb, 0, start + count - len);
+    return m;
+}
+
+// per bitmap word of a fast window: the slots of the counters new in (cur0, cur] are cleared and
+// the admitted counters ORed in; the old window's counters that leave it are counted as received
+// where their old bit is set (tools/rxwin_model.py finish_ranges, checked against the oracle)
+__global__ void rx_final_word_kernel(RxDevWin win, RxDevWs ws) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ((size_t)win.count << win.words_lg)) return;
+    const uint32_t w = (uint32_t)(t >> win.words_lg), q = (uint32_t)(t & (win.words - 1u));
+    if (!rx_fast(ws.wflag[w])) return;
+    const uint64_t len = win.length, mask = len - 1u, cur0 = win.cur[w], cur = ws.curnew[w];
+    const uint32_t nb = len < 64u ? (uint32_t)len : 64u;
+    const uint64_t q0 = (uint64_t)q * 64u;
+    const uint64_t base = (cur >= len && cur - len > cur0) ? cur - len : cur0;
+    const uint64_t clear = rx_ring_mask(q0, nb, (base + 1u) & mask, cur - base, len);
+    const uint64_t lo = ws.exit_lo[w], ehi = min(ws.exit_hi[w], cur0);
+    const uint64_t leaving = ehi >= lo ? rx_ring_mask(q0, nb, lo & mask, ehi - lo + 1u, len) : 0ull;
+    const uint64_t old = win.bits[t];
+    win.bits[t] = (old & ~clear) | ws.scratch[t];
+    const uint32_t r = (uint32_t)__popcll(old & leaving);
+    if (r) atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)r);
 }
 
 __global__ void rx_commit_window_kernel(RxDevWin win, RxDevWs ws) {
@@ -216,8 +269,6 @@ static inline dim3 rx_grid(size_t n) { return dim3((unsigned)((n + 255) / 256));
 extern "C" size_t neb_rxdev_cub_bytes(uint32_t n) {
     size_t a = 0, b = 0, c = 0, d = 0;
     hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-    hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                                        (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
     hipcub::DeviceScan::InclusiveScanByKey(nullptr, c, (const uint32_t*)nullptr, (const uint64_t*)nullptr,
                                            (uint64_t*)nullptr, hipcub::Max(), (int)n, hipcub::Equality());
@@ -248,13 +299,10 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
     e = hipcub::DeviceScan::InclusiveScanByKey(ws->cub_tmp, cb, ws->run_w, ws->run_c, ws->incl, hipcub::Max(), (int)n,
                                                hipcub::Equality(), s);
     if (e != hipSuccess) return e;
-    cb = ws->cub_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(ws->cub_tmp, cb, ws->ctr, ws->c_s, ws->idx, ws->i_c, (int)n, 0, 64, s);
+    e = hipMemsetAsync(ws->tab_owner, 0, (size_t)4 << ws->tab_lg, s);
+    if (e == hipSuccess) e = hipMemsetAsync(ws->tab_min, 0xFF, (size_t)4 << ws->tab_lg, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(neb::rx_gather_w_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
-    cb = ws->cub_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(ws->cub_tmp, cb, ws->w_c, ws->w_cw, ws->i_c, ws->i_cw, (int)n, 0, wbits, s);
-    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(neb::rx_first_insert_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
     hipLaunchKernelGGL(neb::rx_first_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
     hipLaunchKernelGGL(neb::rx_admit_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
     return hipGetLastError();
@@ -274,9 +322,9 @@ extern "C" hipError_t neb_rxdev_finish(uint32_t n, const RxDevWin* win, const Rx
                                        hipStream_t s) {
     hipLaunchKernelGGL(neb::rx_verdict_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
     hipLaunchKernelGGL(neb::rx_final_window_kernel, rx_grid(win->count), dim3(256), 0, s, *win, *ws);
-    const size_t nw = (size_t)win->count * win->words;
+    const size_t nw = (size_t)win->count << win->words_lg;
     hipLaunchKernelGGL(neb::rx_zero_scratch_kernel, rx_grid(nw), dim3(256), 0, s, *win, *ws);
-    hipLaunchKernelGGL(neb::rx_final_packet_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
+    hipLaunchKernelGGL(neb::rx_final_packet_agg_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
     hipLaunchKernelGGL(neb::rx_final_word_kernel, rx_grid(nw), dim3(256), 0, s, *win, *ws);
     hipLaunchKernelGGL(neb::rx_commit_window_kernel, rx_grid(win->count), dim3(256), 0, s, *win, *ws);
     return hipGetLastError();

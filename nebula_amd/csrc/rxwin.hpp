@@ -18,7 +18,8 @@ enum : uint32_t { kRxTouched = 1u, kRxRisky = 2u, kRxSlow = 4u };
 
 struct RxDevWin {  // a set of windows of one length in device memory (neb_dwindows)
     uint32_t count;
-    uint32_t words;     // bitmap words per window
+    uint32_t words;     // bitmap words per window (a power of two)
+    uint32_t words_lg;
     uint64_t length;    // power of two
     uint32_t* present;  // 0 = no window at this index
     uint64_t* cur;
@@ -41,12 +42,11 @@ struct RxDevWs {
     uint32_t* run_i;
     uint64_t* run_c;
     uint64_t* incl;  // segmented inclusive max of the counters
-    // sorted by counter, then stably by window
-    uint64_t* c_s;
-    uint32_t* i_c;
-    uint32_t* w_c;
-    uint32_t* w_cw;
-    uint32_t* i_cw;
+    // first occurrences: an open-addressing table keyed by (window, counter), 2^tab_lg slots;
+    // a slot's owner (arrival index + 1) names its key through keyw / ctr
+    uint32_t* tab_owner;
+    uint32_t* tab_min;  // the earliest arrival with that key
+    uint32_t tab_lg;
     // admitted packets, compacted
     uint32_t* sub_map;
     neb_desc* sub_desc;
@@ -87,11 +87,10 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, size_t cu
     w.run_i = (uint32_t*)take((size_t)n * 4);
     w.run_c = (uint64_t*)take((size_t)n * 8);
     w.incl = (uint64_t*)take((size_t)n * 8);
-    w.c_s = (uint64_t*)take((size_t)n * 8);
-    w.i_c = (uint32_t*)take((size_t)n * 4);
-    w.w_c = (uint32_t*)take((size_t)n * 4);
-    w.w_cw = (uint32_t*)take((size_t)n * 4);
-    w.i_cw = (uint32_t*)take((size_t)n * 4);
+    w.tab_lg = 1;
+    while ((1ull << w.tab_lg) < 2ull * n) w.tab_lg++;
+    w.tab_owner = (uint32_t*)take((size_t)4 << w.tab_lg);
+    w.tab_min = (uint32_t*)take((size_t)4 << w.tab_lg);
     w.sub_map = (uint32_t*)take((size_t)n * 4);
     w.sub_desc = (neb_desc*)take((size_t)n * sizeof(neb_desc));
     w.sub_status = (int32_t*)take((size_t)n * 4);

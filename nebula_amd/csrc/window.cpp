@@ -559,6 +559,8 @@ NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, 
     v.count = count;
     v.length = length;
     v.words = length >= 64 ? (uint32_t)(length / 64) : 1u;
+    v.words_lg = 0;
+    while ((1u << v.words_lg) < v.words) v.words_lg++;
     const size_t b_present = neb::rx_align((size_t)count * 4), b_word = neb::rx_align((size_t)count * 8);
     const size_t bytes = b_present + 4 * b_word + (size_t)count * v.words * 8;
     if (hipMalloc((void**)&d->mem, bytes) != hipSuccess || hipMemset(d->mem, 0, bytes) != hipSuccess) {

@@ -53,7 +53,8 @@ def test_parallel_form_matches_sequential(oracle_mod, length):
             if ok:
                 assert w.update(c)
         assert adm == exp_adm, (trial, run)
-        cur, bits, lost = M.finish(run, adm, cur0, bits0, lost0, length)
-        assert cur == w.current, trial
-        assert bits == w.bits, trial
-        assert lost == w.lost, (trial, lost, w.lost)
+        for fin in (M.finish, M.finish_ranges):
+            cur, bits, lost = fin(run, adm, cur0, bits0, lost0, length)
+            assert cur == w.current, trial
+            assert bits == w.bits, (trial, fin.__name__)
+            assert lost == w.lost, (trial, fin.__name__, lost, w.lost)

@@ -37,6 +37,38 @@ def admit(run, cur0: int, bits: list, length: int):
     return out
 
 
+def ring(start: int, count: int, length: int) -> set:
+    """slots of the circular range [start, start + count) mod length (count <= length)."""
+    return {(start + k) % length for k in range(min(count, length))}
+
+
+def finish_ranges(run, adm, cur0: int, bits: list, lost0: int, length: int):
+    """The same as finish(), in the range form the device computes per bitmap word
+    (rx_final_word_kernel): the slots of the counters new in (cur0, cur] are cleared, the admitted
+    ones ORed in; the counters leaving the old window are one circular slot range too."""
+    mask = length - 1
+    cur = max([cur0] + list(run))
+    lo = cur0 - length + 1 if cur0 >= length else 1
+    hi = cur - length if cur >= length else 0
+    scratch = [False] * length
+    recv = 0
+    for c, a in zip(run, adm):
+        if not a:
+            continue
+        if cur < length or c > cur - length:
+            scratch[c & mask] = True
+        if lo <= c <= hi:
+            recv += 1
+    base = cur - length if (cur >= length and cur - length > cur0) else cur0
+    clear = ring((base + 1) & mask, cur - base, length)
+    ehi = min(hi, cur0)
+    leaving = ring(lo & mask, ehi - lo + 1, length) if ehi >= lo else set()
+    out = [(bits[s] and s not in clear) or scratch[s] for s in range(length)]
+    recv += sum(1 for s in leaving if bits[s])
+    exits = hi - lo + 1 if hi >= lo else 0
+    return cur, out, lost0 + exits - recv
+
+
 def finish(run, adm, cur0: int, bits: list, lost0: int, length: int):
     """(current, bits, lost) after the batch (rx_final_* kernels)."""
     mask = length - 1
