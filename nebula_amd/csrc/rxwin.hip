@@ -96,15 +96,10 @@ __global__ void rx_first_insert_kernel(uint32_t n, RxDevWs ws) {
     if (i < n) atomicMin(&ws.tab_min[rx_slot(ws, i, true)], i);
 }
 
-__global__ void rx_first_kernel(uint32_t n, RxDevWs ws) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) ws.first[i] = ws.tab_min[rx_slot(ws, i, false)] == i;
-}
-
 // which packets the sequential receive would decrypt, if every tag verified (safe windows)
 __global__ void rx_admit_kernel(uint32_t n, RxDevWin win, RxDevWs ws, int32_t* __restrict__ status) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
+    if (k >= n) return;  // (whole waves: the ballot below sees only live lanes)
     const uint32_t w = ws.run_w[k];
     const uint32_t i = ws.run_i[k];
     if (w >= win.count) {
@@ -118,7 +113,11 @@ __global__ void rx_admit_kernel(uint32_t n, RxDevWin win, RxDevWs ws, int32_t* _
     const uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
     bool ok = c > prev;
     if (!ok && rx_in_window(c, prev, win.length)) ok = !(c <= cur0 && rx_bit(bits, win.length - 1u, c));
-    ws.adm[i] = ok && ws.first[i];
+    ok = ok && ws.tab_min[rx_slot(ws, i, false)] == i;  // the first occurrence of (window, counter)
+    ws.adm[i] = ok;
+    // admitted count (wflag[count]): every packet admitted lets the open skip the compaction
+    const uint64_t ball = __ballot(ok);
+    if (ok && __lane_id() == (uint32_t)__builtin_ctzll(ball)) atomicAdd(&ws.wflag[win.count], (uint32_t)__popcll(ball));
 }
 
 __global__ void rx_gather_desc_kernel(const neb_desc* __restrict__ desc, RxDevWs ws) {
@@ -127,10 +126,10 @@ __global__ void rx_gather_desc_kernel(const neb_desc* __restrict__ desc, RxDevWs
 }
 
 // tag verdicts back per packet; a failed one sends its window to the sequential host pass
-__global__ void rx_verdict_kernel(uint32_t n, RxDevWs ws) {
+__global__ void rx_verdict_kernel(uint32_t n, RxDevWs ws, int all) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= *ws.nsub) return;
-    const uint32_t i = ws.sub_map[j];
+    if (j >= (all ? n : *ws.nsub)) return;
+    const uint32_t i = all ? j : ws.sub_map[j];  // all: every packet was opened in arrival order
     const int32_t st = ws.sub_status[j];
     ws.verdict[i] = st;
     if (st != NEB_STATUS_OK) atomicOr(&ws.wflag[ws.keyw[i]], kRxSlow);
@@ -148,12 +147,6 @@ __global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
     ws.exit_lo[w] = cur0 >= len ? cur0 - len + 1u : 1u;  // counter 0 is never lost
     ws.exit_hi[w] = cur >= len ? cur - len : 0u;          // lo > hi: none left
     ws.recv[w] = 0;
-}
-
-__global__ void rx_zero_scratch_kernel(RxDevWin win, RxDevWs ws) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ((size_t)win.count << win.words_lg)) return;
-    if (rx_fast(ws.wflag[t >> win.words_lg])) ws.scratch[t] = 0;
 }
 
 // per packet of a fast window: its status; its counter into the scratch bitmap, and into the
@@ -245,6 +238,7 @@ __global__ void rx_final_word_kernel(RxDevWin win, RxDevWs ws) {
     const uint64_t leaving = ehi >= lo ? rx_ring_mask(q0, nb, lo & mask, ehi - lo + 1u, len) : 0ull;
     const uint64_t old = win.bits[t];
     win.bits[t] = (old & ~clear) | ws.scratch[t];
+    ws.scratch[t] = 0;  // zero again for the next batch (zeroed once at allocation)
     const uint32_t r = (uint32_t)__popcll(old & leaving);
     if (r) atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)r);
 }
@@ -286,7 +280,7 @@ static int rx_bits_for(uint32_t v) {
 // Phase 1: group by window, prefix maxima, first occurrences, admission for the safe windows.
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const RxDevWin* win, const RxDevWs* ws,
                                      int32_t* d_status, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ws->wflag, 0, (size_t)win->count * sizeof(uint32_t), s);
+    hipError_t e = hipMemsetAsync(ws->wflag, 0, ((size_t)win->count + 1u) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(neb::rx_keys_kernel, rx_grid(n), dim3(256), 0, s, d_desc, n, *win, *ws);
     const int wbits = rx_bits_for(win->count);
@@ -303,7 +297,6 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
     if (e == hipSuccess) e = hipMemsetAsync(ws->tab_min, 0xFF, (size_t)4 << ws->tab_lg, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(neb::rx_first_insert_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
-    hipLaunchKernelGGL(neb::rx_first_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
     hipLaunchKernelGGL(neb::rx_admit_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
     return hipGetLastError();
 }
@@ -317,13 +310,18 @@ extern "C" hipError_t neb_rxdev_compact(const neb_desc* d_desc, uint32_t n, cons
     return hipGetLastError();
 }
 
+// The descriptors of the packets listed in ws->sub_map[0, *ws->nsub) (at most n), compacted.
+extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const RxDevWs* ws, hipStream_t s) {
+    hipLaunchKernelGGL(neb::rx_gather_desc_kernel, rx_grid(n), dim3(256), 0, s, d_desc, *ws);
+    return hipGetLastError();
+}
+
 // Phase 3: verdicts, then the parallel finish of every window whose admitted packets all verified.
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const RxDevWin* win, const RxDevWs* ws, int32_t* d_status,
-                                       hipStream_t s) {
-    hipLaunchKernelGGL(neb::rx_verdict_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
+                                       int all, hipStream_t s) {
+    hipLaunchKernelGGL(neb::rx_verdict_kernel, rx_grid(n), dim3(256), 0, s, n, *ws, all);
     hipLaunchKernelGGL(neb::rx_final_window_kernel, rx_grid(win->count), dim3(256), 0, s, *win, *ws);
     const size_t nw = (size_t)win->count << win->words_lg;
-    hipLaunchKernelGGL(neb::rx_zero_scratch_kernel, rx_grid(nw), dim3(256), 0, s, *win, *ws);
     hipLaunchKernelGGL(neb::rx_final_packet_agg_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
     hipLaunchKernelGGL(neb::rx_final_word_kernel, rx_grid(nw), dim3(256), 0, s, *win, *ws);
     hipLaunchKernelGGL(neb::rx_commit_window_kernel, rx_grid(win->count), dim3(256), 0, s, *win, *ws);

@@ -34,7 +34,6 @@ struct RxDevWs {
     uint32_t* keyw;  // window, or count for none
     uint32_t* idx;
     uint64_t* ctr;
-    uint8_t* first;
     uint8_t* adm;
     int32_t* verdict;
     // run order (sorted by window, arrival order kept)
@@ -53,7 +52,7 @@ struct RxDevWs {
     int32_t* sub_status;
     uint32_t* nsub;
     // per window
-    uint32_t* wflag;
+    uint32_t* wflag;  // count + 1: [count] = packets admitted
     uint32_t* rstart;
     uint32_t* rend;
     uint64_t* curnew;
@@ -80,7 +79,6 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, size_t cu
     w.keyw = (uint32_t*)take((size_t)n * 4);
     w.idx = (uint32_t*)take((size_t)n * 4);
     w.ctr = (uint64_t*)take((size_t)n * 8);
-    w.first = (uint8_t*)take(n);
     w.adm = (uint8_t*)take(n);
     w.verdict = (int32_t*)take((size_t)n * 4);
     w.run_w = (uint32_t*)take((size_t)n * 4);
@@ -95,7 +93,7 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, size_t cu
     w.sub_desc = (neb_desc*)take((size_t)n * sizeof(neb_desc));
     w.sub_status = (int32_t*)take((size_t)n * 4);
     w.nsub = (uint32_t*)take(4);
-    w.wflag = (uint32_t*)take((size_t)count * 4);
+    w.wflag = (uint32_t*)take(((size_t)count + 1) * 4);
     w.rstart = (uint32_t*)take((size_t)count * 4);
     w.rend = (uint32_t*)take((size_t)count * 4);
     w.curnew = (uint64_t*)take((size_t)count * 8);
@@ -114,6 +112,7 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, size_t cu
 extern "C" size_t neb_rxdev_cub_bytes(uint32_t n);
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const neb::RxDevWin* win,
                                      const neb::RxDevWs* ws, int32_t* d_status, hipStream_t s);
+extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
 extern "C" hipError_t neb_rxdev_compact(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const neb::RxDevWin* win, const neb::RxDevWs* ws,
-                                       int32_t* d_status, hipStream_t s);
+                                       int32_t* d_status, int all, hipStream_t s);

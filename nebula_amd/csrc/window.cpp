@@ -224,6 +224,84 @@ struct WindowCore {
     }
 };
 
+// The exact receive order for some windows' packet runs: Check → tag verdict → Update, packet
+// after packet in arrival order (connection_state.go:99-119). A packet not opened yet that its
+// window now accepts — an earlier copy of it failed its tag, or a forged counter further ahead held
+// it back in the simulation — stops its window there: the rest of that window's run is simulated
+// again from the real state (every tag assumed to verify), and all stopped windows' admitted
+// packets are opened in one batch (open_fn). A forged packet then costs one more round, never one
+// open per packet behind it. Rounds release the windows' locks; a packet the simulation admits is
+// never refused by the real pass (the simulation applies a superset of the real updates), barring
+// another thread moving the window meanwhile.
+struct ExactRun {
+    uint32_t w, k0, k1;  // window, run positions [k0, k1)
+};
+template <class Ctr, class Pkt, class WithWin, class OpenFn, class Par>
+int exact_rounds(const std::vector<ExactRun>& runs, uint32_t max_groups, Ctr&& ctr, Pkt&& pkt, uint8_t* opened,
+                 const int32_t* verd, int32_t* status, WithWin&& with_window, OpenFn&& open_fn, Par&& par) {
+    const bool stats = std::getenv("NEB_RX_STATS") != nullptr;  // rounds and opens to stderr (per call)
+    uint32_t rounds = 0, extra_opens = 0, extra_pkts = 0;
+    std::vector<uint32_t> pos(runs.size());
+    std::vector<uint32_t> active(runs.size());
+    for (size_t r = 0; r < runs.size(); r++) {
+        pos[r] = runs[r].k0;
+        active[r] = (uint32_t)r;
+    }
+    while (!active.empty()) {
+        const uint32_t ng = std::max(1u, std::min(max_groups, (uint32_t)active.size()));
+        std::vector<std::vector<uint32_t>> want(ng);
+        par(ng, [&](uint32_t gi) {
+            const size_t a0 = active.size() * gi / ng, a1 = active.size() * (gi + 1) / ng;
+            for (size_t a = a0; a < a1; a++) {
+                const uint32_t r = active[a];
+                const ExactRun& R = runs[r];
+                with_window(R.w, [&](WindowCore& core) {
+                    uint32_t k = pos[r];
+                    for (; k < R.k1; k++) {
+                        const uint32_t i = pkt(k);
+                        const uint64_t c = ctr(k);
+                        if (!core.check(c)) {
+                            status[i] = NEB_STATUS_REPLAY;
+                            continue;
+                        }
+                        if (!opened[i]) {
+                            WindowCore sim = core;
+                            for (uint32_t k2 = k; k2 < R.k1; k2++)
+                                if (sim.check(ctr(k2))) {
+                                    sim.update(ctr(k2));
+                                    if (!opened[pkt(k2)]) want[gi].push_back(pkt(k2));
+                                }
+                            break;
+                        }
+                        if (verd[i] != NEB_STATUS_OK) {
+                            status[i] = verd[i];
+                            continue;
+                        }
+                        status[i] = core.update(c) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
+                    }
+                    pos[r] = k;
+                });
+            }
+        });
+        std::vector<uint32_t> all, next;
+        for (auto& v : want) all.insert(all.end(), v.begin(), v.end());
+        for (uint32_t r : active)
+            if (pos[r] < runs[r].k1) next.push_back(r);
+        if (!all.empty()) {
+            const int rc = open_fn(all);  // sets opened[] and the verdicts of these packets
+            if (rc != NEB_OK) return rc;
+            extra_opens++;
+            extra_pkts += (uint32_t)all.size();
+        }
+        active.swap(next);
+        rounds++;
+    }
+    if (stats)
+        std::fprintf(stderr, "rx exact: %zu windows, %u rounds, %u extra opens of %u packets\n", runs.size(), rounds,
+                     extra_opens, extra_pkts);
+    return NEB_OK;
+}
+
 }  // namespace
 
 struct neb_window {
@@ -439,47 +517,41 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
     if (rc != NEB_OK) return rc;
     const auto t2 = now();
 
-    // 3. the real windows, each in arrival order: Check → tag verdict → Update
+    // 3. the real windows, each in arrival order: Check → tag verdict → Update (exact_rounds: a
+    //    packet held back that its window accepts is opened with the rest of its window's run)
     for (uint32_t k = start[nwindows]; k < start[nwindows + 1]; k++) status[order[k]] = NEB_STATUS_BAD_KEY;
-    std::vector<int> trc(nwg, NEB_OK);
-    pool.run(nwg, [&](uint32_t t) {
-        for (uint32_t g = wsplit[t]; g < wsplit[t + 1]; g++) {
-            if (start[g] == start[g + 1]) continue;
-            neb_window* w = windows[g];
-            std::unique_lock<std::mutex> lk(w->mu);
-            for (uint32_t k = start[g]; k < start[g + 1]; k++) {
-                const uint32_t i = order[k];
-                const neb_desc& d = desc[i];
-                if (!w->core.check(d.counter)) {
-                    status[i] = NEB_STATUS_REPLAY;
-                    continue;
-                }
-                int32_t st;
-                if (plan[i] == kToGpu) {
-                    st = gst[sub_of[i]];
-                } else {  // held back, yet the real window accepts it: an earlier copy failed its tag
-                    lk.unlock();
-                    const int r = neb_open_batch_host(e, alg, &d, 1, arena, arena_len, &st, key_hint);
-                    if (r != NEB_OK) {
-                        trc[t] = r;
-                        return;
-                    }
-                    lk.lock();
-                    if (st == NEB_STATUS_OK && !w->core.check(d.counter)) {  // moved by another thread meanwhile
-                        status[i] = NEB_STATUS_REPLAY;
-                        continue;
-                    }
-                }
-                if (st != NEB_STATUS_OK) {
-                    status[i] = st;
-                    continue;
-                }
-                status[i] = w->core.update(d.counter) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
-            }
+    std::vector<uint8_t> opened(n, 0);
+    std::vector<int32_t> verd(n, NEB_STATUS_BAD_KEY);
+    for (uint32_t i = 0; i < n; i++)
+        if (plan[i] == kToGpu) {
+            opened[i] = 1;
+            verd[i] = gst[sub_of[i]];
         }
-    });
-    for (int r : trc)
-        if (r != NEB_OK) return r;
+    std::vector<ExactRun> runs;
+    for (uint32_t g = 0; g < nwindows; g++)
+        if (start[g] != start[g + 1]) runs.push_back({g, start[g], start[g + 1]});
+    rc = exact_rounds(
+        runs, nwg, [&](uint32_t k) { return desc[order[k]].counter; }, [&](uint32_t k) { return order[k]; },
+        opened.data(), verd.data(), status,
+        [&](uint32_t g, auto&& fn) {
+            std::lock_guard<std::mutex> lk(windows[g]->mu);
+            fn(windows[g]->core);
+        },
+        [&](const std::vector<uint32_t>& pk) -> int {
+            std::vector<neb_desc> ds(pk.size());
+            std::vector<int32_t> st(pk.size(), NEB_STATUS_BAD_KEY);
+            for (size_t j = 0; j < pk.size(); j++) ds[j] = desc[pk[j]];
+            const int r = neb_open_batch_host(e, alg, ds.data(), (uint32_t)ds.size(), arena, arena_len, st.data(),
+                                              key_hint);
+            if (r != NEB_OK) return r;
+            for (size_t j = 0; j < pk.size(); j++) {
+                opened[pk[j]] = 1;
+                verd[pk[j]] = st[j];
+            }
+            return NEB_OK;
+        },
+        [&](uint32_t cnt, auto&& fn) { pool.run(cnt, fn); });
+    if (rc != NEB_OK) return rc;
     if (prof)
         std::fprintf(stderr,
                      "rx n=%u threads %u/%u plan %.1f us (validate %.1f group %.1f split %.1f sim %.1f) stage+gpu %.1f "
@@ -650,17 +722,26 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
         d->ws_n = 0;
         RX_HIP(hipMalloc((void**)&d->ws_mem, bytes));
         neb::rx_ws_layout(n, v.count, v.words, cub, d->ws_mem, &d->ws);
+        // the scratch bitmap is zeroed once here and again by each batch as it is consumed
+        RX_HIP(hipMemsetAsync(d->ws.scratch, 0, ((size_t)v.count << v.words_lg) * 8, s));
         d->ws_bytes = bytes;
         d->ws_n = n;
     }
     const neb::RxDevWs& ws = d->ws;
 
+    static const bool prof = std::getenv("NEB_RX_PROF") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    const auto t0 = now();
     // 1. group by window, prefix maxima, first occurrences; admission for the windows safe for
     //    the parallel form
     RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
+    const auto t1 = now();
     std::vector<uint32_t> flag;
-    if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
+    if (d2h(flag, ws.wflag, (size_t)v.count + 1, s) != NEB_OK) return NEB_ERR_HIP;
     RX_HIP(hipStreamSynchronize(s));
+    const uint32_t nadm = flag[v.count];
+    const auto t2 = now();
     std::vector<uint32_t> risky;
     for (uint32_t w = 0; w < v.count; w++)
         if (flag[w] & neb::kRxRisky) risky.push_back(w);
@@ -705,15 +786,25 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
         RX_HIP(hipMemcpyAsync(ws.adm, adm.data(), n, hipMemcpyHostToDevice, s));
     }
 
-    // 2. one open of every admitted packet
-    RX_HIP(neb_rxdev_compact(d_desc, n, &ws, s));
-    rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, ws.sub_status, key_hint, s);
+    // 2. one open of every admitted packet (all of them, the common case: no compaction)
+    const int all = risky.empty() && nadm == n;
+    if (all) {
+        rc = neb_open_batch_count(e, alg, d_desc, n, nullptr, d_arena, ws.sub_status, key_hint, s);
+    } else {
+        RX_HIP(neb_rxdev_compact(d_desc, n, &ws, s));
+        rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, ws.sub_status, key_hint, s);
+    }
     if (rc != NEB_OK) return rc;
 
     // 3. the parallel finish; windows with a failed tag (or risky ones) finish here, exactly
-    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, s));
+    const auto t3 = now();
+    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, all, s));
+    const auto t4 = now();
     if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
     RX_HIP(hipStreamSynchronize(s));
+    if (prof)
+        std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, wait %.1f, enqueue open %.1f, finish %.1f, wait %.1f us\n",
+                     n, us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4), us(t4, now()));
     std::vector<uint32_t> slow;
     for (uint32_t w = 0; w < v.count; w++)
         if ((flag[w] & neb::kRxTouched) && (flag[w] & (neb::kRxRisky | neb::kRxSlow))) slow.push_back(w);
@@ -725,32 +816,40 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
     std::vector<int32_t> verdict, status;
     if (d2h(verdict, ws.verdict, n, s) || d2h(status, d_status, n, s)) return NEB_ERR_HIP;
     RX_HIP(hipStreamSynchronize(s));
+    std::vector<ExactRun> runs;
+    std::vector<WindowCore> cores(slow.size());
+    std::vector<uint32_t> core_of(v.count, 0);
     rc = runs_of(slow, [&](uint32_t w, size_t k0, size_t k1) -> int {
-        WindowCore c;
-        int r = dw_read(d, w, c);
-        if (r != NEB_OK) return r;
-        for (size_t k = k0; k < k1; k++) {  // Check → tag verdict → Update, in arrival order
-            const uint32_t i = run_i[k];
-            const uint64_t ctr = run_c[k];
-            if (!c.check(ctr)) {
-                status[i] = NEB_STATUS_REPLAY;
-                continue;
-            }
-            int32_t st = verdict[i];
-            if (!adm[i]) {  // held back, yet the real window accepts it: an earlier copy failed its tag
-                r = neb_open_batch_count(e, alg, d_desc + i, 1, nullptr, d_arena, ws.sub_status, key_hint, s);
-                if (r != NEB_OK) return r;
-                RX_HIP(hipMemcpyAsync(&st, ws.sub_status, 4, hipMemcpyDeviceToHost, s));
-                RX_HIP(hipStreamSynchronize(s));
-            }
-            if (st != NEB_STATUS_OK) {
-                status[i] = st;
-                continue;
-            }
-            status[i] = c.update(ctr) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
-        }
-        return dw_write(d, w, c);
+        core_of[w] = (uint32_t)runs.size();
+        runs.push_back({w, (uint32_t)k0, (uint32_t)k1});
+        return dw_read(d, w, cores[core_of[w]]);
     });
+    if (rc != NEB_OK) return rc;
+    rc = exact_rounds(
+        runs, 1, [&](uint32_t k) { return run_c[k]; }, [&](uint32_t k) { return run_i[k]; }, adm.data(),
+        verdict.data(), status.data(), [&](uint32_t w, auto&& fn) { fn(cores[core_of[w]]); },
+        [&](const std::vector<uint32_t>& pk) -> int {  // one device open of these packets
+            const uint32_t cnt = (uint32_t)pk.size();
+            RX_HIP(hipMemcpyAsync(ws.sub_map, pk.data(), (size_t)cnt * 4, hipMemcpyHostToDevice, s));
+            RX_HIP(hipMemcpyAsync(ws.nsub, &cnt, 4, hipMemcpyHostToDevice, s));
+            RX_HIP(neb_rxdev_gather(d_desc, cnt, &ws, s));
+            const int r = neb_open_batch_count(e, alg, ws.sub_desc, cnt, nullptr, d_arena, ws.sub_status, key_hint, s);
+            if (r != NEB_OK) return r;
+            std::vector<int32_t> st(cnt);
+            RX_HIP(hipMemcpyAsync(st.data(), ws.sub_status, (size_t)cnt * 4, hipMemcpyDeviceToHost, s));
+            RX_HIP(hipStreamSynchronize(s));
+            for (uint32_t j = 0; j < cnt; j++) {
+                adm[pk[j]] = 1;
+                verdict[pk[j]] = st[j];
+            }
+            return NEB_OK;
+        },
+        [](uint32_t cnt, auto&& fn) {
+            for (uint32_t j = 0; j < cnt; j++) fn(j);
+        });
+    if (rc != NEB_OK) return rc;
+    for (size_t r = 0; r < runs.size(); r++)
+        if ((rc = dw_write(d, runs[r].w, cores[r])) != NEB_OK) return rc;
     if (rc != NEB_OK) return rc;
     RX_HIP(hipMemcpyAsync(d_status, status.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
     RX_HIP(hipStreamSynchronize(s));

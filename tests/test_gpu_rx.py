@@ -251,6 +251,27 @@ def test_rx_device_counters_near_wrap(engine, oracle_mod):
     _run(engine, oracle_mod, L.ALG_AESGCM, arr, device=True)
 
 
+@pytest.mark.parametrize("device", [False, True])
+def test_rx_forged_far_counter_costs_one_round(engine, oracle_mod, capfd, device):
+    """A forged packet with a counter far ahead of its window, then hundreds of genuine ones: the
+    simulation (every tag assumed to verify) holds the genuine ones back, the forgery fails, and
+    the real pass must open them all in one more batch, not one open per packet."""
+    arr = [(0, 5 + 100000, True)] + [(0, 3 + k, False) for k in range(400)] + [(1, 3, False)]
+    arr += [(0, 3 + 200000, True)] + [(0, 403 + k, False) for k in range(100)]
+    os.environ["NEB_RX_STATS"] = "1"
+    try:
+        _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=2, window_len=8192, seed=6, lens=[0, 16, 100],
+             device=device)
+    finally:
+        os.environ.pop("NEB_RX_STATS", None)
+    err = capfd.readouterr().err
+    lines = [ln for ln in err.splitlines() if ln.startswith("rx exact:")]
+    assert lines, err
+    import re
+    rounds, opens = map(int, re.search(r"(\d+) rounds, (\d+) extra opens", lines[-1]).groups())
+    assert rounds <= 3 and opens <= 2, lines[-1]
+
+
 def test_rx_batch_invalid_descriptor_touches_nothing(engine, oracle_mod):
     """A receive batch with a descriptor whose offset wraps around 2^64 is refused before any
     window moves or any packet is opened."""
