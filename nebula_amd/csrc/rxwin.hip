@@ -18,8 +18,8 @@
 //           and were received neither before nor during the batch (the sum of the fast path's
 //           and the jump path's lost accounting, bits.go:173-240);
 //   dupe and out-of-window counters do not move (Update only runs after Check passed).
-// Windows where a tag fails, or whose counters come within 2^62 of wrapping, are finished on the
-// host with the sequential code (window.cpp), exactly.
+// Windows where a tag fails, or whose counters come within 2^62 of wrapping (those admit nothing
+// here), are finished on the host with the sequential code in rounds (window.cpp exact_rounds).
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>

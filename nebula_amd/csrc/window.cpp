@@ -733,29 +733,29 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     const auto t0 = now();
-    // 1. group by window, prefix maxima, first occurrences; admission for the windows safe for
-    //    the parallel form
+    // Everything is queued at once, one host read at the end: windows whose counters come within
+    // 2^62 of wrapping hold all their packets back (admitted by none), and exact_rounds opens what
+    // their real pass accepts in batches, like the windows where a tag failed.
+    // 1. group by window, prefix maxima, first occurrences; admission for the safe windows
     RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
     const auto t1 = now();
-    std::vector<uint32_t> flag;
-    if (d2h(flag, ws.wflag, (size_t)v.count + 1, s) != NEB_OK) return NEB_ERR_HIP;
-    RX_HIP(hipStreamSynchronize(s));
-    const uint32_t nadm = flag[v.count];
+    // 2. one open of every admitted packet, compacted in arrival order
+    RX_HIP(neb_rxdev_compact(d_desc, n, &ws, s));
+    rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, ws.sub_status, key_hint, s);
+    if (rc != NEB_OK) return rc;
     const auto t2 = now();
-    std::vector<uint32_t> risky;
-    for (uint32_t w = 0; w < v.count; w++)
-        if (flag[w] & neb::kRxRisky) risky.push_back(w);
+    // 3. the parallel finish of every window whose admitted packets all verified
+    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, 0, s));
+    const auto t3 = now();
+    std::vector<uint32_t> flag;
+    if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
+    RX_HIP(hipStreamSynchronize(s));
+    if (prof)
+        std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, open %.1f, finish %.1f us, wait %.1f us\n", n, us(t0, t1),
+                     us(t1, t2), us(t2, t3), us(t3, now()));
     std::vector<uint32_t> run_w, run_i;
     std::vector<uint64_t> run_c;
     std::vector<uint8_t> adm;
-    auto fetch_runs = [&]() -> int {
-        if (!run_w.empty()) return NEB_OK;
-        if (d2h(run_w, ws.run_w, n, s) || d2h(run_i, ws.run_i, n, s) || d2h(run_c, ws.run_c, n, s) ||
-            d2h(adm, ws.adm, n, s))
-            return NEB_ERR_HIP;
-        RX_HIP(hipStreamSynchronize(s));
-        return NEB_OK;
-    };
     // windows' packet runs in run order (sorted by window: the runs are contiguous)
     auto runs_of = [&](const std::vector<uint32_t>& ws_list, auto&& fn) -> int {
         size_t k = 0;
@@ -768,53 +768,16 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
         }
         return NEB_OK;
     };
-    if (!risky.empty() && std::getenv("NEB_RXDEV_STRICT")) return NEB_ERR_INVALID;
-    if (!risky.empty()) {  // the sequential simulation for these windows
-        if ((rc = fetch_runs()) != NEB_OK) return rc;
-        rc = runs_of(risky, [&](uint32_t w, size_t k0, size_t k1) -> int {
-            WindowCore sim;
-            const int r = dw_read(d, w, sim);
-            if (r != NEB_OK) return r;
-            for (size_t k = k0; k < k1; k++) {
-                const bool ok = sim.check(run_c[k]);
-                if (ok) sim.update(run_c[k]);
-                adm[run_i[k]] = ok;
-            }
-            return NEB_OK;
-        });
-        if (rc != NEB_OK) return rc;
-        RX_HIP(hipMemcpyAsync(ws.adm, adm.data(), n, hipMemcpyHostToDevice, s));
-    }
-
-    // 2. one open of every admitted packet (all of them, the common case: no compaction)
-    const int all = risky.empty() && nadm == n;
-    if (all) {
-        rc = neb_open_batch_count(e, alg, d_desc, n, nullptr, d_arena, ws.sub_status, key_hint, s);
-    } else {
-        RX_HIP(neb_rxdev_compact(d_desc, n, &ws, s));
-        rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, ws.sub_status, key_hint, s);
-    }
-    if (rc != NEB_OK) return rc;
-
-    // 3. the parallel finish; windows with a failed tag (or risky ones) finish here, exactly
-    const auto t3 = now();
-    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, all, s));
-    const auto t4 = now();
-    if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
-    RX_HIP(hipStreamSynchronize(s));
-    if (prof)
-        std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, wait %.1f, enqueue open %.1f, finish %.1f, wait %.1f us\n",
-                     n, us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4), us(t4, now()));
     std::vector<uint32_t> slow;
     for (uint32_t w = 0; w < v.count; w++)
         if ((flag[w] & neb::kRxTouched) && (flag[w] & (neb::kRxRisky | neb::kRxSlow))) slow.push_back(w);
     if (slow.empty()) return NEB_OK;
     // test hook: NEB_RXDEV_STRICT=1 refuses the host finish, to prove a batch ran the parallel form
     if (std::getenv("NEB_RXDEV_STRICT")) return NEB_ERR_INVALID;
-    run_w.clear();
-    if ((rc = fetch_runs()) != NEB_OK) return rc;
     std::vector<int32_t> verdict, status;
-    if (d2h(verdict, ws.verdict, n, s) || d2h(status, d_status, n, s)) return NEB_ERR_HIP;
+    if (d2h(run_w, ws.run_w, n, s) || d2h(run_i, ws.run_i, n, s) || d2h(run_c, ws.run_c, n, s) ||
+        d2h(adm, ws.adm, n, s) || d2h(verdict, ws.verdict, n, s) || d2h(status, d_status, n, s))
+        return NEB_ERR_HIP;
     RX_HIP(hipStreamSynchronize(s));
     std::vector<ExactRun> runs;
     std::vector<WindowCore> cores(slow.size());
