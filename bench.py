@@ -142,6 +142,9 @@ def main():
                          "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows; "
                          "rx-device: the same with the batch and the windows in device memory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tx-superpackets", type=int, default=1457,
+                    help="tx mode: 64 KiB TSO superpackets per batch (45 segments each; 1457 -> 65 565 wires, "
+                         "1456 -> 65 520: within one pass of the 4096 waves of 16 packets)")
     args = ap.parse_args()
 
     from nebula_amd.shard import Control, dist_env
@@ -345,7 +348,7 @@ def bench_tx(args, eng, ctrl, rank, world):
     from nebula_amd.noiseutil import CipherAESGCM
 
     mss = 1448
-    arena, nsp, size, stride, per = tso_superpackets(65536, mss)
+    arena, nsp, size, stride, per = tso_superpackets(45 * args.tx_superpackets, mss)
     key = CipherAESGCM.Cipher(eng, bytes(range(32)))
     tun = np.zeros(1, TX_TUNNEL_DTYPE)
     tun[0] = (2, key.key_id, 0xBEEF)

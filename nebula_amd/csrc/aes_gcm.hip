@@ -553,6 +553,9 @@ struct GcmArgs {
     // TX batches only (tx.hip): a descriptor's first `flags` plaintext bytes are read from its
     // destination (the patched header image), the rest from src (the TUN read itself)
     uint32_t hdr_from_dst;
+    // single-key kernel: the waves of its grid (NEB_SINGLE_TAIL: packets past its full passes are
+    // left to gcm_single_tail_kernel), 0 = it takes every packet itself
+    uint32_t tail_slots;
 };
 
 struct PktShape {
@@ -952,6 +955,14 @@ __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rk
 #ifndef NEB_GHASH8
 #define NEB_GHASH8 0
 #endif
+// The last, partial pass of a batch larger than one pass of the grid's waves (e.g. 65 565 packets
+// = 4098 groups of 16 on 4096 waves) runs with 16 lanes per packet, 4 packets per wave: the groups
+// that would otherwise run alone after everything else take a quarter of the rounds
+// (bench.py --mode tx: 1457 vs 1456 superpackets, 0.243 vs 0.207 ms).
+#ifndef NEB_SINGLE_TAIL
+#define NEB_SINGLE_TAIL 1
+#endif
+
 #ifndef NEB_G8_LAYOUT
 #define NEB_G8_LAYOUT 0
 #endif
@@ -1058,6 +1069,7 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
 #else
     if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
 #endif
+
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
@@ -1088,7 +1100,11 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     uint32_t npkt = args.npkt;
     if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
-    for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < ngroups; grp += gridDim.x * kSingleWaves) {
+    const uint32_t slots = gridDim.x * kSingleWaves;  // waves of the grid
+    uint32_t main_groups = ngroups;
+    if (args.tail_slots && ngroups > slots && ngroups % slots)
+        main_groups = ngroups / slots * slots;  // full passes only: the tail kernel takes the rest
+    for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < main_groups; grp += slots) {
         const uint32_t p = grp * kPpw + lane / kLpp;
         // a bitsliced wave takes the group if every packet's counters stay below 2^8 (its
         // counter planes are one byte); otherwise the T-table path
@@ -1102,6 +1118,42 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
                                          srec, (wave >> 2) & 3u);
         else
             gcm_packet_group<OPEN, false>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg);
+    }
+}
+
+// The tail pass (NEB_SINGLE_TAIL): the packets after gcm_single_kernel's full passes over
+// args.tail_slots waves, 4 per wave with 16 lanes each: the two-table AES (64 KiB), Horner stride
+// H^16 on its position tables, the final tree on the Shoup tables of H, H^2, H^4, H^8 (GhShoup).
+constexpr int kTailWaves = 8;
+struct TailLds {
+    uint2 ttab[256 * 32];   // 64 KiB T-table pairs, 32 copies
+    uint4 shoup[4 * 16];    // 1 KiB
+    uint4 pos[8 * 16];      // 2 KiB
+};
+template <bool OPEN>
+__global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(GcmArgs args) {
+    __shared__ TailLds lds;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint32_t npkt = args.npkt;
+    if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
+    const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw, slots = args.tail_slots;
+    if (ngroups <= slots || ngroups % slots == 0u) return;  // no partial pass: nothing to do
+    const uint32_t p0 = ngroups / slots * slots * kPpw;
+    const uint32_t tgroups = (npkt - p0 + 3u) / 4u;
+    if (blockIdx.x * kTailWaves >= tgroups) return;
+    const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
+    for (uint32_t i = tid; i < 256u * 32u; i += kTailWaves * kWave) lds.ttab[i] = ttab_entry(i);
+    if (tid < 64u) lds.shoup[tid] = ld_rec4(srec, kRecShoup + 64u * ((1u << (tid >> 4)) - 1u) + 4u * (tid & 15u));
+    if (tid < 128u) lds.pos[tid] = ld_rec4(srec, kRecPos16 + 4u * tid);
+    uint32_t rks[60];
+    load_round_keys(srec, rks);
+    __syncthreads();
+    const TLook T{lds.ttab, ttab_lane_base(lane)};
+    const GhShoup gh{lds.shoup, lds.pos};
+    const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
+    for (uint32_t t = blockIdx.x * kTailWaves + wave; t < tgroups; t += gridDim.x * kTailWaves) {
+        const uint32_t p = p0 + 4u * t + (lane >> 4);
+        gcm_packet_group<OPEN, false>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, 4u);
     }
 }
 
@@ -1447,10 +1499,28 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
                                            int hdr_from_dst) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst};
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
-    return open ? launch_grid(neb::gcm_single_kernel<true>, neb::kSingleThreads, groups, cu_count, s, a)
-                : launch_grid(neb::gcm_single_kernel<false>, neb::kSingleThreads, groups, cu_count, s, a);
+    const void* kern = open ? (const void*)neb::gcm_single_kernel<true> : (const void*)neb::gcm_single_kernel<false>;
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, neb::kSingleThreads, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const uint32_t grid = std::min((groups + neb::kSingleWaves - 1u) / neb::kSingleWaves, (uint32_t)(per_cu * cu_count));
+    const uint32_t slots = grid * neb::kSingleWaves;
+    // a partial last pass (at most n packets; the real count may be on the device) goes to the
+    // tail kernel, 16 lanes per packet
+    const bool tail = NEB_SINGLE_TAIL && !NEB_GHASH8 && groups > slots && (d_n || groups % slots);
+    if (tail) a.tail_slots = slots;
+    hipError_t e = open ? launch_grid(neb::gcm_single_kernel<true>, neb::kSingleThreads, groups, cu_count, s, a)
+                        : launch_grid(neb::gcm_single_kernel<false>, neb::kSingleThreads, groups, cu_count, s, a);
+    if (e != hipSuccess || !tail) return e;
+    const uint32_t tail_pkts = n - groups / slots * slots * neb::kPpw;  // the largest tail n allows
+    const uint32_t tgrid = ((tail_pkts + 3u) / 4u + neb::kTailWaves - 1u) / neb::kTailWaves;
+    if (open)
+        hipLaunchKernelGGL(neb::gcm_single_tail_kernel<true>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL(neb::gcm_single_tail_kernel<false>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), 0, s, a);
+    return hipGetLastError();
 }
 
 // Mixed keys: the batch has been regrouped into chunks by neb_sched_build.
@@ -1459,7 +1529,7 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, int cu_count,
                                             hipStream_t s, int hdr_from_dst) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst};
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
     neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks};
     // one wave per chunk up to the occupancy cap (tails make chunks outnumber n / 16); the chunk
     // count is only known on the device: workgroups past it exit before filling their tables

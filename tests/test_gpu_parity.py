@@ -334,6 +334,35 @@ def test_full_c2_roundtrip_property(engine):
     assert np.array_equal(s2[idx], r2[idx])
 
 
+@pytest.mark.parametrize("extra", [1, 37, 4 * 16 * 64 + 5])
+def test_single_key_partial_last_pass(engine, oracle_mod, extra):
+    """One key, a batch just past one pass of the single-key kernel's waves (64 Ki packets on one
+    MI355X): the packets of the partial last pass go to the tail kernel, 16 lanes per packet. Every
+    packet, ragged sizes, sealed and opened, bit-exact against the oracle."""
+    import torch
+    from nebula_amd.batch import DeviceBatch, install_keys
+
+    n = 65536 + extra
+    b = W.make_batch(L.ALG_AESGCM, n, 1, sizes=(0, 1, 16, 17, 95, 130, 257), ratio=(1, 1, 1, 1, 2, 2, 1),
+                     seed=97 + extra, name="tail")
+    ref, _ = oracle_seal(oracle_mod, b)
+    ciphers = install_keys(engine, b)
+    try:
+        db = DeviceBatch(engine, b, ciphers)
+        db.seal()
+        torch.cuda.synchronize()
+        assert (db.status_host() == 0).all()
+        assert np.array_equal(db.arena_host(), ref)
+        db.open()
+        torch.cuda.synchronize()
+        assert (db.status_host() == 0).all()
+        ref_o, _ = oracle_open(oracle_mod, b, ref)
+        assert np.array_equal(db.arena_host(), ref_o)
+    finally:
+        for c in ciphers:
+            c.destroy()
+
+
 @pytest.mark.parametrize("arena_kind", ["pinned", "pageable"])
 @pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
 def test_host_pipeline_matches_device(engine, oracle_mod, alg, arena_kind):
