@@ -277,7 +277,7 @@ struct TxSegOp {
     }
 };
 
-template <uint32_t IT>
+template <uint32_t IT, bool PARSED>
 __global__ __launch_bounds__(kTxPlanThreads) void tx_plan_small_kernel(
     const neb_tx_packet* __restrict__ pk, uint32_t n, const uint8_t* __restrict__ in, neb_tx_tunnel* __restrict__ tun,
     uint32_t ntun, const uint32_t* __restrict__ keys, uint32_t max_keys, int alg, uint64_t out_cap, uint32_t max_wires,
@@ -306,13 +306,20 @@ __global__ __launch_bounds__(kTxPlanThreads) void tx_plan_small_kernel(
     // blocked 8 through the LDS (the output bytes of one read fit 32 bits: at most 65535 segments of
     // at most 160 bytes)
     for (uint32_t i = t; i < n; i += kTxPlanThreads) {
-        const neb_tx_packet P = pk[i];
-        const TxParsed r = tx_parse_one(P, in, tun, ntun, keys, max_keys, alg);
-        ws.plan[i] = r.plan;
-        pk_status[i] = r.st;
-        s_nseg[i] = r.plan.nseg;
-        s_end[i] = (uint32_t)(r.scan & kTxBytesMask);
-        s_key[i] = r.st == NEB_STATUS_OK ? P.tunnel : ntun;
+        if constexpr (PARSED) {  // tx_parse_kernel ran first, grid-wide
+            const uint64_t sc = ws.scan_in[i];
+            s_nseg[i] = (uint32_t)(sc >> 40);
+            s_end[i] = (uint32_t)(sc & kTxBytesMask);
+            s_key[i] = ws.tun_key[i];
+        } else {
+            const neb_tx_packet P = pk[i];
+            const TxParsed r = tx_parse_one(P, in, tun, ntun, keys, max_keys, alg);
+            ws.plan[i] = r.plan;
+            pk_status[i] = r.st;
+            s_nseg[i] = r.plan.nseg;
+            s_end[i] = (uint32_t)(r.scan & kTxBytesMask);
+            s_key[i] = r.st == NEB_STATUS_OK ? P.tunnel : ntun;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -761,14 +768,23 @@ extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const u
     int bits = 1;
     while (bits < 32 && (1ull << bits) <= ntun) bits++;
     if (NEB_TX_SMALL_PLAN && n <= neb::kTxPlanSmallMax) {
+        // Parsing is a chain of dependent header loads per read: past one read per lane of the one
+        // workgroup it runs grid-wide first (1457 reads: plan 24.8 -> the two kernels below).
+        const bool pre = n > neb::kTxPlanThreads;
+        if (pre) {
+            const uint32_t tpb = 256;
+            hipLaunchKernelGGL(neb::tx_parse_kernel, dim3((n + tpb - 1) / tpb), dim3(tpb), 0, s, d_pk, n, d_in, d_tun,
+                               ntun, d_keys, max_keys, alg, *ws, d_pk_status);
+        }
         // the block sort and scans cost by items per thread: 2 up to 2048 reads
+        auto plan = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(1), dim3(neb::kTxPlanThreads), 0, s, d_pk, n, d_in, d_tun, ntun, d_keys,
+                               max_keys, alg, out_cap, max_wires, bits, *ws, d_pk_status, d_nwires);
+        };
         if (n <= 2u * neb::kTxPlanThreads)
-            hipLaunchKernelGGL(neb::tx_plan_small_kernel<2>, dim3(1), dim3(neb::kTxPlanThreads), 0, s, d_pk, n, d_in,
-                               d_tun, ntun, d_keys, max_keys, alg, out_cap, max_wires, bits, *ws, d_pk_status, d_nwires);
+            pre ? plan(neb::tx_plan_small_kernel<2, true>) : plan(neb::tx_plan_small_kernel<2, false>);
         else
-            hipLaunchKernelGGL(neb::tx_plan_small_kernel<neb::kTxPlanItems>, dim3(1), dim3(neb::kTxPlanThreads), 0, s,
-                               d_pk, n, d_in, d_tun, ntun, d_keys, max_keys, alg, out_cap, max_wires, bits, *ws,
-                               d_pk_status, d_nwires);
+            plan(neb::tx_plan_small_kernel<neb::kTxPlanItems, true>);
         hipLaunchKernelGGL(neb::tx_segmap_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, max_wires, out_cap, *ws);
         return hipGetLastError();
     }

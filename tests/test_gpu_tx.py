@@ -187,6 +187,26 @@ def test_tx_batch_random_superpackets(engine, oracle_mod):
     _check(engine, oracle_mod, L.ALG_AESGCM, P, _tunnels(rng, n=8, keyless=()), out_cap=8 << 20, max_wires=8192)
 
 
+@pytest.mark.parametrize("n", [1500, 3000])
+def test_tx_batch_pre_parsed_plan(engine, oracle_mod, n):
+    """1024 < reads <= 8192: parsed grid-wide first, then planned by one workgroup (2 and 8 reads
+    per lane); keyless tunnels, invalid reads and an output that keeps only a prefix."""
+    import segment_oracle as S
+
+    rng = random.Random(n)
+    P = []
+    for i in range(n):
+        if i % 211 == 3:
+            d, _, cs = build_tcpv4_super(rng.choice([3000, 9000]))
+            P.append(_pk(d, rng.randrange(8), 1, S.GSO_TCPV4, 1448, cs, 16))
+        elif i % 97 == 5:
+            P.append(_pk(b"", rng.randrange(8)))
+        else:
+            P.append(_pk(bytes(rng.getrandbits(8) for _ in range(rng.randrange(20, 120))), rng.randrange(9)))
+    tun = _tunnels(rng, n=8, keyless=(2,))
+    _check(engine, oracle_mod, L.ALG_AESGCM, P, tun, out_cap=n * 150, max_wires=16384)
+
+
 @pytest.mark.parametrize("cut", [False, True])
 def test_tx_batch_large_plan_path(engine, oracle_mod, cut):
     """More TUN reads than one workgroup plans (kTxPlanSmallMax = 8192): the device-wide planning
