@@ -303,7 +303,11 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
         P5 A = {{0, 0, 0, 0, 0}};
         for (uint32_t rho = 0; rho < rmax; rho++) {
             if (rho >= nrounds) continue;
+#ifdef NEB_CH_ABLATE_CHACHA  // timing study only: wrong keystream
+            if (rho > kappa) ks = make_uint4(ks.x + rho, ks.y ^ rho, ks.z + j, ks.w ^ dn);
+#else
             if (rho > kappa) ks = chacha_quad(kConst[w], ka, kc, w == 0u ? 4u * (rho - kappa) + j : dn, w);
+#endif
             const int32_t i = (int32_t)(16u * rho + l) - (int32_t)phi;  // poly block index
             if (i < 0 || i >= (int32_t)n) continue;
             P5 mi;
@@ -324,7 +328,11 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
             } else {
                 mi = p5_from_words(d.aad_len, 0u, d.len, 0u, 1u);
             }
+#ifdef NEB_CH_ABLATE_POLY  // timing study only: wrong tag
+            A = p5_add(A, mi);
+#else
             A = p5_add(p5_mul(A, r16), mi);
+#endif
         }
         if (!run) {
             if (valid && l == 15u) args.status[p] = (int32_t)st;

@@ -9,7 +9,7 @@ mkdir -p ../build_abl && rm -f ../build_abl/lib_*.so
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result -Wno-unused-value $defs \
-     -shared -x hip csrc/aes_gcm.hip -x hip csrc/chacha_poly.hip -x hip csrc/sched.hip -x hip csrc/tx.hip -x hip csrc/engine.cpp -x hip csrc/window.cpp -o ../build_abl/lib_$name.so &
+     -shared -x hip csrc/aes_gcm.hip -x hip csrc/chacha_poly.hip -x hip csrc/sched.hip -x hip csrc/tx.hip -x hip csrc/rxwin.hip -x hip csrc/engine.cpp -x hip csrc/window.cpp -o ../build_abl/lib_$name.so &
   echo $name >> ../build_abl/variants.txt
 done
 wait
