@@ -298,3 +298,43 @@ def test_rx_batch_invalid_descriptor_touches_nothing(engine, oracle_mod):
         assert (w.current, w.lost, w.dupe, w.out_of_window) == (2, 0, 0, 0)
     finally:
         c.destroy()
+
+
+def test_device_windows_api_errors(engine):
+    """neb_dwindows_* and neb_rx_open_batch refuse what Bits / the host call refuse: a length that
+    is not a power of two, a slot out of range, a host window of another length, storing an absent
+    slot, a bad algorithm, a window set of another engine."""
+    import ctypes as C
+
+    from nebula_amd.connection_state import Bits, DeviceWindows
+    from nebula_amd.noiseutil import Engine
+
+    lib = L.lib()
+    h = C.c_void_p()
+    assert lib.neb_dwindows_create(engine.handle, 4, 1000, C.byref(h)) == L.ERR_INVALID
+    assert lib.neb_dwindows_create(engine.handle, 0, 1024, C.byref(h)) == L.ERR_INVALID
+    dw = DeviceWindows(engine, 4, 1024)
+    try:
+        w = Bits(1024)
+        w.Update(5)
+        assert lib.neb_dwindows_load(dw.handle, 4, w.handle) == L.ERR_INVALID       # slot out of range
+        assert lib.neb_dwindows_load(dw.handle, 0, Bits(2048).handle) == L.ERR_INVALID  # other length
+        assert lib.neb_dwindows_store(dw.handle, 1, w.handle) == L.ERR_INVALID      # absent slot
+        dw.load(1, w)
+        back = Bits(1024)
+        dw.store(1, back)
+        assert back.current == 5 and back.snapshot() == w.snapshot()
+        dw.load(1, None)
+        assert lib.neb_dwindows_store(dw.handle, 1, back.handle) == L.ERR_INVALID
+        assert lib.neb_rx_open_batch(engine.handle, 7, dw.handle, None, 0, None, None, L.KEYS_MIXED, None) == \
+            L.ERR_INVALID
+        assert lib.neb_rx_open_batch(engine.handle, L.ALG_AESGCM, dw.handle, None, 0, None, None, L.KEYS_MIXED,
+                                     None) == L.OK  # empty batch
+        other = Engine(engine.device, 16)
+        try:
+            assert lib.neb_rx_open_batch(other.handle, L.ALG_AESGCM, dw.handle, None, 0, None, None, L.KEYS_MIXED,
+                                         None) == L.ERR_INVALID
+        finally:
+            other.close()
+    finally:
+        dw.destroy()
