@@ -116,7 +116,7 @@ NEB_API const char* neb_last_error(void);
 /* Install a 32-byte key: AES-256 key schedule + H = E_K(0^128) + H^1..H^16 (AESGCM), or the raw
  * ChaCha20 key (ChaChaPoly), computed on the device into the engine's key table. */
 NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out);
-/* Waits for every asynchronous batch this engine has enqueued (on any stream) to finish, then
+/* Waits for the engine's device to drain (every asynchronous batch enqueued on any stream), then
  * clears the key record and frees its slot. A batch enqueued after the key is destroyed gets
  * NEB_STATUS_BAD_KEY for its packets (the kernels check the slot's algorithm tag). */
 NEB_API int neb_cipher_destroy(neb_cipher* c);

@@ -223,24 +223,7 @@ struct neb_engine {
         std::vector<RxSlot> slot;
     } rx;
 
-    // Asynchronous batches (neb_seal_batch / neb_open_batch / neb_tx_seal_batch) read key records
-    // after the call returns: the last launch on each caller stream is recorded here, and
-    // neb_cipher_destroy waits for all of them before it clears and frees a slot.
-    std::mutex fl_mu;
-    std::vector<std::pair<hipStream_t, hipEvent_t>> inflight;
 };
-
-// Record the end of the work just enqueued on caller stream s (see neb_engine::inflight).
-static hipError_t note_inflight(neb_engine* e, hipStream_t s) {
-    std::lock_guard<std::mutex> g(e->fl_mu);
-    for (auto& f : e->inflight)
-        if (f.first == s) return hipEventRecord(f.second, s);
-    hipEvent_t ev = nullptr;
-    hipError_t err = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (err != hipSuccess) return err;
-    e->inflight.emplace_back(s, ev);
-    return hipEventRecord(ev, s);
-}
 
 struct neb_cipher {
     neb_engine* e;
@@ -360,10 +343,6 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
     if (e->tx.done) { hipEventSynchronize(e->tx.done); hipEventDestroy(e->tx.done); }
     if (e->tx.mem) hipFree(e->tx.mem);
     if (e->tx.d_io) hipFree(e->tx.d_io);
-    for (auto& f : e->inflight) {
-        hipEventSynchronize(f.second);
-        hipEventDestroy(f.second);
-    }
     for (auto& r : e->rx.slot) {
         if (r.stream) { hipStreamSynchronize(r.stream); hipStreamDestroy(r.stream); }
         if (r.ev) hipEventDestroy(r.ev);
@@ -447,10 +426,11 @@ NEB_API int neb_cipher_destroy(neb_cipher* c) {
     if (!c) return NEB_ERR_INVALID;
     neb_engine* e = c->e;
     hipSetDevice(e->device);
-    {  // batches still queued on caller streams may read this record: let them finish first
-        std::lock_guard<std::mutex> g(e->fl_mu);
-        for (auto& f : e->inflight) hipEventSynchronize(f.second);
-    }
+    // Asynchronous batches (neb_seal_batch / neb_open_batch / neb_tx_seal_batch / neb_rx_open_batch)
+    // still queued on caller streams may read this record: the whole device drains first. A
+    // destroy is rare; an event recorded after every launch instead cost 2-4 µs per kernel
+    // (profiles/r2_micro/ab_inflight_events.log).
+    hipDeviceSynchronize();
     {
         std::lock_guard<std::mutex> g(e->io_mu);
         hipMemsetAsync(e->d_keys + (size_t)c->key_id * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, e->stream);
@@ -635,7 +615,6 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
     hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream, as for any HIP launch
     hipError_t err = launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s);
-    if (err == hipSuccess) err = note_inflight(e, s);
     if (err != hipSuccess) {
         set_error("batch launch", err);
         return NEB_ERR_HIP;
@@ -663,7 +642,6 @@ int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_
                          uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s) {
     if (n == 0) return NEB_OK;
     hipError_t err = launch_batch(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, s, d_n);
-    if (err == hipSuccess) err = note_inflight(e, s);
     if (err != hipSuccess) {
         set_error("batch launch", err);
         return NEB_ERR_HIP;
@@ -1008,7 +986,6 @@ NEB_API int neb_tx_seal_batch(neb_engine* e, int alg, neb_tx_tunnel* d_tunnels, 
     std::lock_guard<std::mutex> g(e->tx.mu);
     rc = tx_run(e, alg, d_tunnels, ntunnels, d_packets, npackets, d_in, d_out, out_cap, d_wires, d_wire_status,
                 max_wires, d_nwires, d_packet_status, key_hint, s);
-    if (rc == NEB_OK) HIP_TRY(note_inflight(e, s));
     return rc;
 }
 
