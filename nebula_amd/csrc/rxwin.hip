@@ -22,7 +22,7 @@
 // here), are finished on the host with the sequential code in rounds (window.cpp exact_rounds).
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
+#include <algorithm>
 
 #include "../../include/nebula_aead.h"
 #include "rxwin.hpp"
@@ -38,36 +38,123 @@ __device__ __forceinline__ bool rx_bit(const uint64_t* bits, uint64_t mask, uint
     return (bits[p >> 6] >> (p & 63)) & 1u;
 }
 
-// per packet: its window (or W: none), arrival index, counter
-__global__ void rx_keys_kernel(const neb_desc* __restrict__ desc, uint32_t n, RxDevWin win, RxDevWs ws) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const neb_desc d = desc[i];
-    ws.keyw[i] = (d.key_id < win.count && win.present[d.key_id]) ? d.key_id : win.count;
-    ws.idx[i] = i;
-    ws.ctr[i] = d.counter;
-    ws.adm[i] = 0;
-    ws.verdict[i] = NEB_STATUS_OK;
+// ---- the stable sort of the packets by window (LSD radix, arrival order kept) ----------------
+// At most kRxSortBlocks workgroups of 256 x items packets each, so every workgroup of a pass can
+// read all the workgroups' digit counts itself (no scan launch) and the next pass's counts are
+// gathered per output workgroup in LDS. One pass is two launches (the first fused into the keys
+// kernel), every further pass one more: 2 launches up to 256 windows, 3 up to 16 Ki.
+struct RxSort {
+    uint32_t n, items, per_blk, nblk;  // per_blk = 256 x items
+    uint32_t passes;
+    uint32_t shift[kRxSortMaxPasses];
+    uint32_t bits[kRxSortMaxPasses];
+};
+
+// Per packet: its window (or count: none) and counter, and the first pass's digit counts per
+// workgroup (packet e = b * per_blk + j * 256 + t). Also clears the window flags, the admitted
+// count and the later passes' digit counts (the grid covers the packets and the windows).
+__global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict__ desc, RxDevWin win, RxDevWs ws,
+                                                      RxSort so) {
+    __shared__ uint32_t hist[256];
+    const uint32_t t = threadIdx.x, b = blockIdx.x;
+    hist[t] = 0;
+    for (uint32_t x = t; x < so.per_blk; x += 256) {
+        const size_t wi = (size_t)b * so.per_blk + x;
+        if (wi < win.count) ws.wflag[wi] = 0;
+    }
+    if (b == 0 && t == 0) *ws.nsub = 0;
+    if (b >= so.nblk) return;
+    for (uint32_t p = 1; p < so.passes; p++) ws.sort_hist[((size_t)p * kRxSortBlocks + b) * 256 + t] = 0;
+    __syncthreads();
+    const uint32_t mask = (1u << so.bits[0]) - 1u;
+    for (uint32_t j = 0; j < so.items; j++) {
+        const uint32_t e = b * so.per_blk + j * 256u + t;
+        if (e >= so.n) break;
+        const neb_desc d = desc[e];
+        const uint32_t w = (d.key_id < win.count && win.present[d.key_id]) ? d.key_id : win.count;
+        ws.keyw[e] = w;
+        ws.ctr[e] = d.counter;
+        atomicAdd(&hist[(w >> so.shift[0]) & mask], 1u);
+    }
+    __syncthreads();
+    ws.sort_hist[(size_t)b * 256 + t] = hist[t];
 }
 
-// run order: counters, run bounds, touched / risky windows
-__global__ void rx_runs_kernel(uint32_t n, RxDevWin win, RxDevWs ws) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const uint32_t w = ws.run_w[k];
-    const uint32_t i = ws.run_i[k];
-    const uint64_t c = ws.ctr[i];
-    ws.run_c[k] = c;
-    if (w >= win.count) return;
-    // flag words are written by the run's head and by risky packets only (one window's whole batch
-    // on one address would serialise)
-    uint32_t fl = c >= kRxRiskyCounter ? kRxRisky : 0u;
-    if (k == 0u || ws.run_w[k - 1u] != w) {
-        ws.rstart[w] = k;
-        fl |= kRxTouched | (win.cur[w] >= kRxRiskyCounter ? kRxRisky : 0u);
+// One pass: every packet of the workgroup to base[digit] + (its digit's count in earlier
+// workgroups) + (its rank among the workgroup's packets of that digit, in arrival order: a round
+// of 256 at a time, ranks within a wave from ballots, waves in order through LDS). Unless this is
+// the last pass, the next digit is counted per output workgroup in LDS and added to its counts.
+template <bool FIRST>
+__global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p, uint32_t* hist_all,
+                                                           const uint32_t* __restrict__ src_k,
+                                                           const uint32_t* __restrict__ src_v, uint32_t* dst_k,
+                                                           uint32_t* dst_v) {
+    __shared__ uint32_t gbase[256], run[256], wcnt[4][256], wtot[4];
+    __shared__ uint32_t agg[kRxSortBlocks << kRxSortDigit];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
+    const uint32_t* hist = hist_all + (size_t)p * kRxSortBlocks * 256;
+    const bool next = p + 1 < so.passes;
+    const uint32_t nb2 = next ? 1u << so.bits[p + 1] : 0u;
+    // digit t: the count in earlier workgroups, and the total (exclusive scan over digits below)
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t q = 0; q < so.nblk; q++) {
+        const uint32_t h = hist[(size_t)q * 256 + t];
+        tot += h;
+        pre += q < b ? h : 0u;
     }
-    if (k + 1u == n || ws.run_w[k + 1u] != w) ws.rend[w] = k + 1u;
-    if (fl) atomicOr(&ws.wflag[w], fl);
+    uint32_t x = tot;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63u) wtot[wv] = x;
+    run[t] = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < 4; v++) wcnt[v][t] = 0;
+    for (uint32_t i = t; i < so.nblk * nb2; i += 256) agg[i] = 0;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t v = 0; v < wv; v++) wbase += wtot[v];
+    gbase[t] = wbase + x - tot + pre;
+    __syncthreads();
+    const uint32_t sh = so.shift[p], nbits = so.bits[p], mask = (1u << nbits) - 1u;
+    const uint32_t sh2 = next ? so.shift[p + 1] : 0u, mask2 = nb2 - 1u;
+    const uint64_t lt = (1ull << lane) - 1u;
+    for (uint32_t j = 0; j < so.items; j++) {
+        const uint32_t e = b * so.per_blk + j * 256u + t;
+        const bool valid = e < so.n;
+        const uint32_t key = valid ? src_k[e] : 0u;
+        const uint32_t val = FIRST ? e : (valid ? src_v[e] : 0u);
+        const uint32_t dg = (key >> sh) & mask;
+        uint64_t eq = __ballot(valid);
+        for (uint32_t bit = 0; bit < nbits; bit++) {
+            const uint64_t bb = __ballot((dg >> bit) & 1u);
+            eq &= ((dg >> bit) & 1u) ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(eq & lt);
+        if (valid && rank == 0) wcnt[wv][dg] = (uint32_t)__popcll(eq);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = gbase[dg] + run[dg] + rank;
+            for (uint32_t v = 0; v < wv; v++) pos += wcnt[v][dg];
+            dst_k[pos] = key;
+            dst_v[pos] = val;
+            if (next) atomicAdd(&agg[(pos / so.per_blk) * nb2 + ((key >> sh2) & mask2)], 1u);
+        }
+        __syncthreads();
+        run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+#pragma unroll
+        for (uint32_t v = 0; v < 4; v++) wcnt[v][t] = 0;
+        __syncthreads();
+    }
+    if (next) {
+        uint32_t* h2 = hist_all + (size_t)(p + 1) * kRxSortBlocks * 256;
+        for (uint32_t i = t; i < so.nblk * nb2; i += 256) {
+            const uint32_t c = agg[i];
+            if (c) atomicAdd(&h2[(i / nb2) * 256u + (i & (nb2 - 1u))], c);
+        }
+    }
 }
 
 __device__ __forceinline__ uint32_t rx_hash(uint32_t w, uint64_t c, uint32_t lg) {
@@ -76,48 +163,208 @@ __device__ __forceinline__ uint32_t rx_hash(uint32_t w, uint64_t c, uint32_t lg)
     return (uint32_t)(h >> (64 - lg));
 }
 
-// the slot of packet i's (window, counter) key: claimed by the first to arrive at it, found by
-// comparing the owner's key (exact, no hash comparison); the table has at least 2n slots
+// The slot of packet i's (window, counter) key: claimed by the first to arrive at it, found by
+// comparing the owner's key (exact, no hash comparison); the table has at least 2n slots. An
+// entry whose generation is not this batch's is empty.
 __device__ __forceinline__ uint32_t rx_slot(const RxDevWs& ws, uint32_t i, bool insert) {
     const uint32_t w = ws.keyw[i];
     const uint64_t c = ws.ctr[i];
     const uint32_t tmask = (1u << ws.tab_lg) - 1u;
+    const uint64_t mine = ((uint64_t)ws.gen << 32) | (i + 1u);
     uint32_t h = rx_hash(w, c, ws.tab_lg);
     for (;;) {
-        const uint32_t o = insert ? atomicCAS(&ws.tab_owner[h], 0u, i + 1u) : ws.tab_owner[h];
-        if (o == 0u) return h;  // claimed (insert); a lookup always finds its own key first
-        if (o == i + 1u || (ws.keyw[o - 1u] == w && ws.ctr[o - 1u] == c)) return h;
+        uint64_t o = ws.tab_owner[h];
+        if (insert) {
+            while ((uint32_t)(o >> 32) != ws.gen) {  // empty: claim it
+                const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(ws.tab_owner + h), o, mine);
+                if (seen == o) return h;
+                o = seen;
+            }
+        }
+        // (a lookup always finds its own key before an empty slot)
+        const uint32_t oi = (uint32_t)o - 1u;
+        if (o == mine || (ws.keyw[oi] == w && ws.ctr[oi] == c)) return h;
         h = (h + 1u) & tmask;
     }
 }
 
-__global__ void rx_first_insert_kernel(uint32_t n, RxDevWs ws) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicMin(&ws.tab_min[rx_slot(ws, i, true)], i);
+// (head, max) pairs of the segmented max scan: a head starts a new run
+struct RxSeg {
+    uint32_t f;
+    uint64_t v;
+};
+__device__ __forceinline__ RxSeg rx_seg(RxSeg a, RxSeg b) { return {a.f | b.f, b.f ? b.v : max(a.v, b.v)}; }
+
+// Run order (sorted by window, arrival order kept), kRxBlock elements per workgroup: the counters
+// in run order, touched / risky windows, every packet's key into the first-occurrence table, and
+// the segmented inclusive max of the counters within the workgroup (blk_max / blk_fh let the
+// admission finish the scan across workgroups).
+__global__ __launch_bounds__(kRxThreads) void rx_scan_kernel(uint32_t n, RxDevWin win, RxDevWs ws) {
+    __shared__ uint64_t s_v[kRxThreads / 64];
+    __shared__ uint32_t s_f[kRxThreads / 64];
+    __shared__ uint32_t s_fh;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t b0 = blockIdx.x * kRxBlock, k0 = b0 + t * kRxItems;
+    if (t == 0) s_fh = kRxBlock;
+    uint64_t c[kRxItems];
+    uint32_t hd[kRxItems];
+    RxSeg agg{0u, 0ull};
+#pragma unroll
+    for (uint32_t j = 0; j < kRxItems; j++) {
+        const uint32_t k = k0 + j;
+        c[j] = 0;
+        hd[j] = 0;
+        if (k >= n) continue;
+        const uint32_t w = ws.run_w[k];
+        const uint32_t i = ws.run_i[k];
+        c[j] = ws.ctr[i];
+        ws.run_c[k] = c[j];
+        hd[j] = k == 0u || ws.run_w[k - 1u] != w;
+        agg = rx_seg(agg, {hd[j], c[j]});
+        if (w >= win.count) continue;
+        // flag words are written by the run's head and by risky packets only (one window's whole
+        // batch on one address would serialise)
+        uint32_t fl = c[j] >= kRxRiskyCounter ? kRxRisky : 0u;
+        if (hd[j]) fl |= kRxTouched | (win.cur[w] >= kRxRiskyCounter ? kRxRisky : 0u);
+        if (fl) atomicOr(&ws.wflag[w], fl);
+        atomicMax(reinterpret_cast<unsigned long long*>(ws.tab_min + rx_slot(ws, i, true)),
+                  ((unsigned long long)ws.gen << 32) | (0xFFFFFFFFu - i));
+    }
+    __syncthreads();  // s_fh
+#pragma unroll
+    for (uint32_t j = 0; j < kRxItems; j++)
+        if (hd[j]) {
+            atomicMin(&s_fh, t * kRxItems + j);
+            break;
+        }
+    // exclusive prefix of the thread aggregates: within the wave, then across the waves
+    RxSeg x = agg;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t f = __shfl_up(x.f, o);
+        const uint64_t v = __shfl_up(x.v, o);
+        if (lane >= o) x = rx_seg({f, v}, x);
+    }
+    if (lane == 63u) {
+        s_f[wv] = x.f;
+        s_v[wv] = x.v;
+    }
+    RxSeg ex{__shfl_up(x.f, 1), __shfl_up(x.v, 1)};
+    if (lane == 0) ex = {0u, 0ull};
+    __syncthreads();
+    RxSeg wp{0u, 0ull};
+    for (uint32_t q = 0; q < wv; q++) wp = rx_seg(wp, {s_f[q], s_v[q]});
+    RxSeg run = rx_seg(wp, ex);
+#pragma unroll
+    for (uint32_t j = 0; j < kRxItems; j++) {
+        const uint32_t k = k0 + j;
+        run = rx_seg(run, {hd[j], c[j]});
+        if (k < n) ws.incl[k] = run.v;
+        if (k + 1u == n || k == b0 + kRxBlock - 1u) {  // the workgroup's last element
+            ws.blk_max[blockIdx.x] = run.v;
+            ws.blk_fh[blockIdx.x] = s_fh;
+        }
+    }
 }
 
-// which packets the sequential receive would decrypt, if every tag verified (safe windows)
-__global__ void rx_admit_kernel(uint32_t n, RxDevWin win, RxDevWs ws, int32_t* __restrict__ status) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;  // (whole waves: the ballot below sees only live lanes)
-    const uint32_t w = ws.run_w[k];
-    const uint32_t i = ws.run_i[k];
-    if (w >= win.count) {
-        status[i] = NEB_STATUS_BAD_KEY;  // no window: no ConnectionState for this index
-        return;
+// Which packets the sequential receive would decrypt, if every tag verified (safe windows),
+// compacted into sub_map / sub_desc (one atomic per workgroup; order is immaterial to the open);
+// the run's last packet sets its window's final current and the range of counters that leave it.
+__global__ __launch_bounds__(kRxThreads) void rx_admit_kernel(const neb_desc* __restrict__ desc, uint32_t n,
+                                                                RxDevWin win, RxDevWs ws,
+                                                                int32_t* __restrict__ status) {
+    __shared__ uint64_t s_pre;
+    __shared__ uint32_t s_cnt[kRxThreads / 64];
+    __shared__ uint32_t s_base;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t b = blockIdx.x, b0 = b * kRxBlock, k0 = b0 + t * kRxItems;
+    const uint32_t fh = ws.blk_fh[b];
+    // the max over the run that continues into this workgroup: back over earlier workgroups to
+    // (and including) the first one holding a run head
+    if (wv == 0) {
+        uint64_t pre = 0;
+        if (fh > 0u)
+            for (int64_t base = (int64_t)b - 1; base >= 0; base -= 64) {
+                const int64_t bb = base - (int64_t)lane;
+                const bool valid = bb >= 0;
+                const bool has = valid && ws.blk_fh[bb] < kRxBlock;
+                const uint64_t stop = __ballot(has);
+                const uint32_t last = stop ? (uint32_t)__builtin_ctzll(stop) : 63u;
+                uint64_t m = (valid && lane <= last) ? ws.blk_max[bb] : 0ull;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) m = max(m, (uint64_t)__shfl_xor(m, o));
+                pre = max(pre, m);
+                if (stop) break;
+            }
+        if (lane == 0) s_pre = pre;
     }
-    if (ws.wflag[w] & kRxRisky) return;  // decided on the host
-    const uint64_t cur0 = win.cur[w];
-    const uint64_t prev = k == ws.rstart[w] ? cur0 : max(cur0, ws.incl[k - 1u]);
-    const uint64_t c = ws.run_c[k];
-    const uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
-    bool ok = c > prev;
-    if (!ok && rx_in_window(c, prev, win.length)) ok = !(c <= cur0 && rx_bit(bits, win.length - 1u, c));
-    ok = ok && ws.tab_min[rx_slot(ws, i, false)] == i;  // the first occurrence of (window, counter)
-    ws.adm[i] = ok;
-    // admitted count (wflag[count]): every packet admitted lets the open skip the compaction
-    const uint64_t ball = __ballot(ok);
-    if (ok && __lane_id() == (uint32_t)__builtin_ctzll(ball)) atomicAdd(&ws.wflag[win.count], (uint32_t)__popcll(ball));
+    __syncthreads();
+    const uint64_t pre = s_pre;
+    auto incl_at = [&](uint32_t k) -> uint64_t {  // the run's inclusive max at k (k >= b0 - 1)
+        if (k < b0) return pre;
+        const uint64_t v = ws.incl[k];
+        return k - b0 >= fh ? v : max(pre, v);
+    };
+    uint32_t okm = 0, ids[kRxItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kRxItems; j++) {
+        const uint32_t k = k0 + j;
+        if (k >= n) continue;
+        const uint32_t w = ws.run_w[k];
+        const uint32_t i = ws.run_i[k];
+        ws.verdict[i] = NEB_STATUS_OK;
+        ws.adm[i] = 0;
+        if (w >= win.count) {
+            status[i] = NEB_STATUS_BAD_KEY;  // no window: no ConnectionState for this index
+            continue;
+        }
+        const uint64_t cur0 = win.cur[w];
+        if (k + 1u == n || ws.run_w[k + 1u] != w) {  // the run's last packet: the window's finish
+            const uint64_t len = win.length, cur = max(cur0, incl_at(k));
+            ws.curnew[w] = cur;
+            ws.exit_lo[w] = cur0 >= len ? cur0 - len + 1u : 1u;  // counter 0 is never lost
+            ws.exit_hi[w] = cur >= len ? cur - len : 0u;          // lo > hi: none left
+            ws.recv[w] = 0;
+        }
+        if (ws.wflag[w] & kRxRisky) continue;  // decided on the host
+        const bool head = k == 0u || ws.run_w[k - 1u] != w;
+        const uint64_t prev = head ? cur0 : max(cur0, incl_at(k - 1u));
+        const uint64_t c = ws.run_c[k];
+        const uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
+        bool ok = c > prev;
+        if (!ok && rx_in_window(c, prev, win.length)) ok = !(c <= cur0 && rx_bit(bits, win.length - 1u, c));
+        // the first occurrence of (window, counter)
+        ok = ok && ws.tab_min[rx_slot(ws, i, false)] == (((uint64_t)ws.gen << 32) | (0xFFFFFFFFu - i));
+        ids[j] = i;
+        if (ok) {
+            ws.adm[i] = 1;
+            okm |= 1u << j;
+        }
+    }
+    // workgroup prefix of the admitted counts
+    const uint32_t take = (uint32_t)__popc(okm);
+    uint32_t x = take;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63u) s_cnt[wv] = x;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t tot = 0;
+        for (uint32_t q = 0; q < kRxThreads / 64; q++) tot += s_cnt[q];
+        s_base = tot ? atomicAdd(ws.nsub, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t j0 = s_base + x - take;
+    for (uint32_t q = 0; q < wv; q++) j0 += s_cnt[q];
+#pragma unroll
+    for (uint32_t j = 0; j < kRxItems; j++)
+        if (okm >> j & 1u) {
+            ws.sub_map[j0] = ids[j];
+            ws.sub_desc[j0++] = desc[ids[j]];
+        }
 }
 
 __global__ void rx_gather_desc_kernel(const neb_desc* __restrict__ desc, RxDevWs ws) {
@@ -136,18 +383,6 @@ __global__ void rx_verdict_kernel(uint32_t n, RxDevWs ws, int all) {
 }
 
 __device__ __forceinline__ bool rx_fast(uint32_t fl) { return (fl & kRxTouched) && !(fl & (kRxRisky | kRxSlow)); }
-
-// per window: the final current and the range of counters that leave the window
-__global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
-    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= win.count || !rx_fast(ws.wflag[w])) return;
-    const uint64_t cur0 = win.cur[w], len = win.length;
-    const uint64_t cur = max(cur0, ws.incl[ws.rend[w] - 1u]);
-    ws.curnew[w] = cur;
-    ws.exit_lo[w] = cur0 >= len ? cur0 - len + 1u : 1u;  // counter 0 is never lost
-    ws.exit_hi[w] = cur >= len ? cur - len : 0u;          // lo > hi: none left
-    ws.recv[w] = 0;
-}
 
 // per packet of a fast window: its status; its counter into the scratch bitmap, and into the
 // received count when it leaves the window — one atomic per (wave, window, word) instead of one per packet: a
@@ -221,35 +456,46 @@ __device__ __forceinline__ uint64_t rx_ring_mask(uint64_t q0, uint32_t nb, uint6
     return m;
 }
 
-// per bitmap word of a fast window: the slots of the counters new in (cur0, cur] are cleared and
-// the admitted counters ORed in; the old window's counters that leave it are counted as received
-// where their old bit is set (tools/rxwin_model.py finish_ranges, checked against the oracle)
-__global__ void rx_final_word_kernel(RxDevWin win, RxDevWs ws) {
+// Per fast window, lanes over its bitmap words (min(words, 64) lanes a window, so a wave holds
+// one or more whole windows): the slots of the counters new in (cur0, cur] are cleared and the
+// admitted counters ORed in; the old window's counters that leave it are counted as received
+// where their old bit is set (tools/rxwin_model.py finish_ranges, checked against the oracle);
+// then the window's lost count and current.
+__global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
+    const uint32_t lanes_lg = win.words_lg < 6u ? win.words_lg : 6u, L = 1u << lanes_lg;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ((size_t)win.count << win.words_lg)) return;
-    const uint32_t w = (uint32_t)(t >> win.words_lg), q = (uint32_t)(t & (win.words - 1u));
-    if (!rx_fast(ws.wflag[w])) return;
-    const uint64_t len = win.length, mask = len - 1u, cur0 = win.cur[w], cur = ws.curnew[w];
-    const uint32_t nb = len < 64u ? (uint32_t)len : 64u;
-    const uint64_t q0 = (uint64_t)q * 64u;
-    const uint64_t base = (cur >= len && cur - len > cur0) ? cur - len : cur0;
-    const uint64_t clear = rx_ring_mask(q0, nb, (base + 1u) & mask, cur - base, len);
-    const uint64_t lo = ws.exit_lo[w], ehi = min(ws.exit_hi[w], cur0);
-    const uint64_t leaving = ehi >= lo ? rx_ring_mask(q0, nb, lo & mask, ehi - lo + 1u, len) : 0ull;
-    const uint64_t old = win.bits[t];
-    win.bits[t] = (old & ~clear) | ws.scratch[t];
-    ws.scratch[t] = 0;  // zero again for the next batch (zeroed once at allocation)
-    const uint32_t r = (uint32_t)__popcll(old & leaving);
-    if (r) atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)r);
-}
-
-__global__ void rx_commit_window_kernel(RxDevWin win, RxDevWs ws) {
-    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= win.count || !rx_fast(ws.wflag[w])) return;
-    const uint64_t lo = ws.exit_lo[w], hi = ws.exit_hi[w];
-    const uint64_t exits = hi >= lo ? hi - lo + 1u : 0u;
-    win.lost[w] += (int64_t)(exits - ws.recv[w]);
-    win.cur[w] = ws.curnew[w];
+    const size_t wl = t >> lanes_lg;
+    const uint32_t sub = (uint32_t)t & (L - 1u);
+    const uint32_t w = wl < win.count ? (uint32_t)wl : 0u;
+    const bool fast = wl < win.count && rx_fast(ws.wflag[w]);
+    uint64_t r = 0;
+    uint64_t cur = 0, lo = 1, hi = 0;
+    if (fast) {
+        const uint64_t len = win.length, mask = len - 1u, cur0 = win.cur[w];
+        cur = ws.curnew[w];
+        lo = ws.exit_lo[w];
+        hi = ws.exit_hi[w];
+        const uint32_t nb = len < 64u ? (uint32_t)len : 64u;
+        const uint64_t base = (cur >= len && cur - len > cur0) ? cur - len : cur0;
+        const uint64_t ehi = min(hi, cur0);
+        uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
+        uint64_t* scr = ws.scratch + ((size_t)w << win.words_lg);
+        for (uint32_t q = sub; q < win.words; q += L) {
+            const uint64_t q0 = (uint64_t)q * 64u;
+            const uint64_t clear = rx_ring_mask(q0, nb, (base + 1u) & mask, cur - base, len);
+            const uint64_t leaving = ehi >= lo ? rx_ring_mask(q0, nb, lo & mask, ehi - lo + 1u, len) : 0ull;
+            const uint64_t old = bits[q];
+            bits[q] = (old & ~clear) | scr[q];
+            scr[q] = 0;  // zero again for the next batch (zeroed once at allocation)
+            r += (uint32_t)__popcll(old & leaving);
+        }
+    }
+    for (uint32_t o = L >> 1; o > 0; o >>= 1) r += __shfl_xor(r, (int)o);  // within the window's lanes
+    if (fast && sub == 0) {
+        const uint64_t exits = hi >= lo ? hi - lo + 1u : 0u;
+        win.lost[w] += (int64_t)(exits - ws.recv[w] - r);
+        win.cur[w] = cur;
+    }
 }
 
 }  // namespace neb
@@ -259,54 +505,47 @@ using neb::RxDevWs;
 
 static inline dim3 rx_grid(size_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
-// Device-side bytes of the hipCUB passes for n packets.
-extern "C" size_t neb_rxdev_cub_bytes(uint32_t n) {
-    size_t a = 0, b = 0, c = 0, d = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-    hipcub::DeviceScan::InclusiveScanByKey(nullptr, c, (const uint32_t*)nullptr, (const uint64_t*)nullptr,
-                                           (uint64_t*)nullptr, hipcub::Max(), (int)n, hipcub::Equality());
-    hipcub::DeviceSelect::Flagged(nullptr, d, (const uint32_t*)nullptr, (const uint8_t*)nullptr, (uint32_t*)nullptr,
-                                  (uint32_t*)nullptr, (int)n);
-    return std::max(std::max(a, b), std::max(c, d));
-}
-
 static int rx_bits_for(uint32_t v) {
     int bits = 1;
     while (bits < 32 && (1ull << bits) <= v) bits++;
     return bits;
 }
 
-// Phase 1: group by window, prefix maxima, first occurrences, admission for the safe windows.
+// Phase 1: group by window, prefix maxima, first occurrences, admission for the safe windows, and
+// the admitted packets' descriptors compacted (count in *ws->nsub).
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const RxDevWin* win, const RxDevWs* ws,
                                      int32_t* d_status, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ws->wflag, 0, ((size_t)win->count + 1u) * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(neb::rx_keys_kernel, rx_grid(n), dim3(256), 0, s, d_desc, n, *win, *ws);
-    const int wbits = rx_bits_for(win->count);
-    size_t cb = ws->cub_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(ws->cub_tmp, cb, ws->keyw, ws->run_w, ws->idx, ws->run_i, (int)n, 0, wbits,
-                                           s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(neb::rx_runs_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws);
-    cb = ws->cub_bytes;
-    e = hipcub::DeviceScan::InclusiveScanByKey(ws->cub_tmp, cb, ws->run_w, ws->run_c, ws->incl, hipcub::Max(), (int)n,
-                                               hipcub::Equality(), s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(ws->tab_owner, 0, (size_t)4 << ws->tab_lg, s);
-    if (e == hipSuccess) e = hipMemsetAsync(ws->tab_min, 0xFF, (size_t)4 << ws->tab_lg, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(neb::rx_first_insert_kernel, rx_grid(n), dim3(256), 0, s, n, *ws);
-    hipLaunchKernelGGL(neb::rx_admit_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
-    return hipGetLastError();
-}
-
-// Phase 2: the admitted packets' descriptors, compacted in arrival order (count in *ws->nsub).
-extern "C" hipError_t neb_rxdev_compact(const neb_desc* d_desc, uint32_t n, const RxDevWs* ws, hipStream_t s) {
-    size_t cb = ws->cub_bytes;
-    hipError_t e = hipcub::DeviceSelect::Flagged(ws->cub_tmp, cb, ws->idx, ws->adm, ws->sub_map, ws->nsub, (int)n, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(neb::rx_gather_desc_kernel, rx_grid(n), dim3(256), 0, s, d_desc, *ws);
+    neb::RxSort so{};
+    so.n = n;
+    so.items = (n + 256u * neb::kRxSortBlocks - 1) / (256u * neb::kRxSortBlocks);
+    so.per_blk = 256u * so.items;
+    so.nblk = (n + so.per_blk - 1) / so.per_blk;
+    const int bits = rx_bits_for(win->count);  // keys 0..count (count: no window)
+    so.passes = bits <= 8 ? 1u : (uint32_t)(bits + neb::kRxSortDigit - 1) / neb::kRxSortDigit;
+    for (uint32_t p = 0, sh = 0; p < so.passes; p++) {
+        so.shift[p] = sh;
+        so.bits[p] = (uint32_t)(bits - (int)sh + (int)(so.passes - p) - 1) / (so.passes - p);
+        sh += so.bits[p];
+    }
+    const uint32_t kgrid = std::max<uint32_t>(so.nblk, (win->count + so.per_blk - 1) / so.per_blk);
+    hipLaunchKernelGGL(neb::rx_keys_kernel, dim3(kgrid), dim3(256), 0, s, d_desc, *win, *ws, so);
+    // pass p writes the run arrays when (passes - 1 - p) is even, so the last pass ends there
+    for (uint32_t p = 0; p < so.passes; p++) {
+        const bool to_run = ((so.passes - 1 - p) & 1u) == 0;
+        uint32_t* dk = to_run ? ws->run_w : ws->tmp_k;
+        uint32_t* dv = to_run ? ws->run_i : ws->tmp_v;
+        const uint32_t* sk = p == 0 ? ws->keyw : (to_run ? ws->tmp_k : ws->run_w);
+        const uint32_t* sv = p == 0 ? nullptr : (to_run ? ws->tmp_v : ws->run_i);
+        if (p == 0)
+            hipLaunchKernelGGL(neb::rx_sort_pass_kernel<true>, dim3(so.nblk), dim3(256), 0, s, so, p, ws->sort_hist,
+                               sk, sv, dk, dv);
+        else
+            hipLaunchKernelGGL(neb::rx_sort_pass_kernel<false>, dim3(so.nblk), dim3(256), 0, s, so, p, ws->sort_hist,
+                               sk, sv, dk, dv);
+    }
+    const dim3 blocks((n + neb::kRxBlock - 1) / neb::kRxBlock);
+    hipLaunchKernelGGL(neb::rx_scan_kernel, blocks, dim3(neb::kRxThreads), 0, s, n, *win, *ws);
+    hipLaunchKernelGGL(neb::rx_admit_kernel, blocks, dim3(neb::kRxThreads), 0, s, d_desc, n, *win, *ws, d_status);
     return hipGetLastError();
 }
 
@@ -320,10 +559,9 @@ extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const RxDevWin* win, const RxDevWs* ws, int32_t* d_status,
                                        int all, hipStream_t s) {
     hipLaunchKernelGGL(neb::rx_verdict_kernel, rx_grid(n), dim3(256), 0, s, n, *ws, all);
-    hipLaunchKernelGGL(neb::rx_final_window_kernel, rx_grid(win->count), dim3(256), 0, s, *win, *ws);
-    const size_t nw = (size_t)win->count << win->words_lg;
     hipLaunchKernelGGL(neb::rx_final_packet_agg_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
-    hipLaunchKernelGGL(neb::rx_final_word_kernel, rx_grid(nw), dim3(256), 0, s, *win, *ws);
-    hipLaunchKernelGGL(neb::rx_commit_window_kernel, rx_grid(win->count), dim3(256), 0, s, *win, *ws);
+    const uint32_t lanes_lg = win->words_lg < 6u ? win->words_lg : 6u;
+    hipLaunchKernelGGL(neb::rx_final_window_kernel, rx_grid((size_t)win->count << lanes_lg), dim3(256), 0, s, *win,
+                       *ws);
     return hipGetLastError();
 }

@@ -15,6 +15,12 @@ namespace neb {
 // and 2^62 messages is far beyond any tunnel's life; forged counters may, and are then exact too.
 constexpr uint64_t kRxRiskyCounter = 1ull << 62;
 enum : uint32_t { kRxTouched = 1u, kRxRisky = 2u, kRxSlow = 4u };
+// run-order elements per workgroup of the scan and admission kernels (one per thread: their
+// per-packet chains of dependent loads and atomics are latency-bound)
+constexpr uint32_t kRxThreads = 256, kRxItems = 1, kRxBlock = kRxThreads * kRxItems;
+// the stable sort by window (rxwin.hip): at most kRxSortBlocks workgroups of 256 x items packets,
+// digits of at most 8 bits for one pass, else passes of at most kRxSortDigit bits
+constexpr uint32_t kRxSortBlocks = 64, kRxSortDigit = 7, kRxSortMaxPasses = 5;
 
 struct RxDevWin {  // a set of windows of one length in device memory (neb_dwindows)
     uint32_t count;
@@ -32,43 +38,47 @@ struct RxDevWin {  // a set of windows of one length in device memory (neb_dwind
 struct RxDevWs {
     // per packet (arrival index)
     uint32_t* keyw;  // window, or count for none
-    uint32_t* idx;
     uint64_t* ctr;
     uint8_t* adm;
     int32_t* verdict;
+    // the sort: per pass, per workgroup digit counts; ping-pong keys / arrival indices
+    uint32_t* sort_hist;  // kRxSortMaxPasses x kRxSortBlocks x 256
+    uint32_t* tmp_k;
+    uint32_t* tmp_v;
     // run order (sorted by window, arrival order kept)
     uint32_t* run_w;
     uint32_t* run_i;
     uint64_t* run_c;
-    uint64_t* incl;  // segmented inclusive max of the counters
-    // first occurrences: an open-addressing table keyed by (window, counter), 2^tab_lg slots;
-    // a slot's owner (arrival index + 1) names its key through keyw / ctr
-    uint32_t* tab_owner;
-    uint32_t* tab_min;  // the earliest arrival with that key
+    uint64_t* incl;     // segmented inclusive max of the counters within each block of kRxBlock
+    uint64_t* blk_max;  // per block: incl at its last element
+    uint32_t* blk_fh;   // per block: position of its first run head (kRxBlock: none)
+    // first occurrences: an open-addressing table keyed by (window, counter), 2^tab_lg slots,
+    // tagged with the batch generation (an entry of an older batch is empty, so the table is
+    // never cleared between batches); a slot's owner (gen:32 | arrival index + 1) names its key
+    // through keyw / ctr
+    uint64_t* tab_owner;
+    uint64_t* tab_min;  // gen:32 | ~(the earliest arrival with that key), by atomicMax
     uint32_t tab_lg;
+    uint32_t gen;
     // admitted packets, compacted
     uint32_t* sub_map;
     neb_desc* sub_desc;
     int32_t* sub_status;
     uint32_t* nsub;
     // per window
-    uint32_t* wflag;  // count + 1: [count] = packets admitted
-    uint32_t* rstart;
-    uint32_t* rend;
+    uint32_t* wflag;
     uint64_t* curnew;
     uint64_t* exit_lo;
     uint64_t* exit_hi;
     uint64_t* recv;
     uint64_t* scratch;  // count x words
-    void* cub_tmp;
-    size_t cub_bytes;
 };
 
 inline size_t rx_align(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Carve an RxDevWs for n packets over `count` windows of `words` bitmap words out of base
 // (nullptr: only size it). Returns the bytes needed.
-inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, size_t cub_bytes, uint8_t* base, RxDevWs* ws) {
+inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* base, RxDevWs* ws) {
     size_t off = 0;
     auto take = [&](size_t bytes) {
         uint8_t* p = base ? base + off : nullptr;
@@ -77,42 +87,41 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, size_t cu
     };
     RxDevWs w{};
     w.keyw = (uint32_t*)take((size_t)n * 4);
-    w.idx = (uint32_t*)take((size_t)n * 4);
     w.ctr = (uint64_t*)take((size_t)n * 8);
     w.adm = (uint8_t*)take(n);
     w.verdict = (int32_t*)take((size_t)n * 4);
+    w.sort_hist = (uint32_t*)take((size_t)kRxSortMaxPasses * kRxSortBlocks * 256 * 4);
+    w.tmp_k = (uint32_t*)take((size_t)n * 4);
+    w.tmp_v = (uint32_t*)take((size_t)n * 4);
     w.run_w = (uint32_t*)take((size_t)n * 4);
     w.run_i = (uint32_t*)take((size_t)n * 4);
     w.run_c = (uint64_t*)take((size_t)n * 8);
     w.incl = (uint64_t*)take((size_t)n * 8);
+    const size_t nblk = ((size_t)n + kRxBlock - 1) / kRxBlock;
+    w.blk_max = (uint64_t*)take(nblk * 8);
+    w.blk_fh = (uint32_t*)take(nblk * 4);
     w.tab_lg = 1;
     while ((1ull << w.tab_lg) < 2ull * n) w.tab_lg++;
-    w.tab_owner = (uint32_t*)take((size_t)4 << w.tab_lg);
-    w.tab_min = (uint32_t*)take((size_t)4 << w.tab_lg);
+    w.tab_owner = (uint64_t*)take((size_t)8 << w.tab_lg);
+    w.tab_min = (uint64_t*)take((size_t)8 << w.tab_lg);
     w.sub_map = (uint32_t*)take((size_t)n * 4);
     w.sub_desc = (neb_desc*)take((size_t)n * sizeof(neb_desc));
     w.sub_status = (int32_t*)take((size_t)n * 4);
     w.nsub = (uint32_t*)take(4);
-    w.wflag = (uint32_t*)take(((size_t)count + 1) * 4);
-    w.rstart = (uint32_t*)take((size_t)count * 4);
-    w.rend = (uint32_t*)take((size_t)count * 4);
+    w.wflag = (uint32_t*)take((size_t)count * 4);
     w.curnew = (uint64_t*)take((size_t)count * 8);
     w.exit_lo = (uint64_t*)take((size_t)count * 8);
     w.exit_hi = (uint64_t*)take((size_t)count * 8);
     w.recv = (uint64_t*)take((size_t)count * 8);
     w.scratch = (uint64_t*)take((size_t)count * words * 8);
-    w.cub_tmp = take(cub_bytes);
-    w.cub_bytes = cub_bytes;
     if (ws) *ws = w;
     return off;
 }
 
 }  // namespace neb
 
-extern "C" size_t neb_rxdev_cub_bytes(uint32_t n);
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const neb::RxDevWin* win,
                                      const neb::RxDevWs* ws, int32_t* d_status, hipStream_t s);
 extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
-extern "C" hipError_t neb_rxdev_compact(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const neb::RxDevWin* win, const neb::RxDevWs* ws,
                                        int32_t* d_status, int all, hipStream_t s);

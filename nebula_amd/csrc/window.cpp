@@ -714,18 +714,24 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
     hipStream_t s = (hipStream_t)stream;
     auto& v = d->win;
     if (n > d->ws_n) {
-        const size_t cub = neb_rxdev_cub_bytes(n);
-        const size_t bytes = neb::rx_ws_layout(n, v.count, v.words, cub, nullptr, nullptr);
+        const size_t bytes = neb::rx_ws_layout(n, v.count, v.words, nullptr, nullptr);
         RX_HIP(hipStreamSynchronize(s));
         if (d->ws_mem) hipFree(d->ws_mem);
         d->ws_mem = nullptr;
         d->ws_n = 0;
         RX_HIP(hipMalloc((void**)&d->ws_mem, bytes));
-        neb::rx_ws_layout(n, v.count, v.words, cub, d->ws_mem, &d->ws);
+        neb::rx_ws_layout(n, v.count, v.words, d->ws_mem, &d->ws);
         // the scratch bitmap is zeroed once here and again by each batch as it is consumed
         RX_HIP(hipMemsetAsync(d->ws.scratch, 0, ((size_t)v.count << v.words_lg) * 8, s));
+        d->ws.gen = UINT32_MAX;  // the first batch clears the first-occurrence table
         d->ws_bytes = bytes;
         d->ws_n = n;
+    }
+    // a new generation per batch empties the first-occurrence table; cleared for real at wrap
+    if (++d->ws.gen == 0) {
+        RX_HIP(hipMemsetAsync(d->ws.tab_owner, 0, (size_t)8 << d->ws.tab_lg, s));
+        RX_HIP(hipMemsetAsync(d->ws.tab_min, 0, (size_t)8 << d->ws.tab_lg, s));
+        d->ws.gen = 1;
     }
     const neb::RxDevWs& ws = d->ws;
 
@@ -739,8 +745,7 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
     // 1. group by window, prefix maxima, first occurrences; admission for the safe windows
     RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
     const auto t1 = now();
-    // 2. one open of every admitted packet, compacted in arrival order
-    RX_HIP(neb_rxdev_compact(d_desc, n, &ws, s));
+    // 2. one open of every admitted packet (compacted by the plan)
     rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, ws.sub_status, key_hint, s);
     if (rc != NEB_OK) return rc;
     const auto t2 = now();

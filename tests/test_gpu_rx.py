@@ -57,7 +57,7 @@ def _expected(oracle_mod, R, alg, keys, arrivals, arena, pts, window_len, seeds,
 
 
 def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=None, installed=None, seed=1,
-         lens=None, device=False, strict=False):
+         lens=None, device=False, strict=False, count=None):
     import replay_oracle as R
     from nebula_amd.connection_state import Bits, rx_open_batch
     from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
@@ -89,7 +89,9 @@ def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=N
 
             from nebula_amd.connection_state import DeviceWindows, rx_open_batch_device
             dev = torch.device("cuda", engine.device)
-            dw = DeviceWindows(engine, engine.max_keys, window_len)
+            if count == "fit":  # just the slots in use
+                count = max(slot_of.values()) + 1
+            dw = DeviceWindows(engine, count or engine.max_keys, window_len)
             try:
                 for t, w in ewins.items():
                     dw.load(slot_of[t], w)
@@ -231,6 +233,16 @@ def test_rx_device_parallel_form(engine, oracle_mod, length):
     arr = _random_arrivals(rng, 6000, 5, 0.0, jump=3 * length + 2)
     _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=5, window_len=length, seed=9, lens=[0, 16, 60],
          seeds={0: 2, 1: 2, 2: 2, 3: 2, 4: 2}, device=True, strict=True)
+
+
+@pytest.mark.parametrize("count", ["fit", 40000])
+def test_rx_device_sort_passes(engine, oracle_mod, count):
+    """The stable sort by window in one pass (a window set of fewer than 256 slots: keys of at most
+    8 bits) and in three (40 000 slots: 16-bit keys), then the parallel form."""
+    rng = random.Random(5)
+    arr = _random_arrivals(rng, 5000, 6, 0.0, jump=200)
+    _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=6, window_len=1024, seed=11, lens=[0, 16, 60],
+         device=True, strict=True, count=count)
 
 
 def test_rx_device_one_big_window(engine, oracle_mod):
