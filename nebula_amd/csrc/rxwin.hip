@@ -67,14 +67,31 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
     for (uint32_t p = 1; p < so.passes; p++) ws.sort_hist[((size_t)p * kRxSortBlocks + b) * 256 + t] = 0;
     __syncthreads();
     const uint32_t mask = (1u << so.bits[0]) - 1u;
-    for (uint32_t j = 0; j < so.items; j++) {
-        const uint32_t e = b * so.per_blk + j * 256u + t;
-        if (e >= so.n) break;
-        const neb_desc d = desc[e];
-        const uint32_t w = (d.key_id < win.count && win.present[d.key_id]) ? d.key_id : win.count;
-        ws.keyw[e] = w;
-        ws.ctr[e] = d.counter;
-        atomicAdd(&hist[(w >> so.shift[0]) & mask], 1u);
+    constexpr uint32_t R = kRxSortLoad;
+    for (uint32_t j0 = 0; j0 < so.items; j0 += R) {
+        uint32_t kid[R], pres[R];
+        uint64_t ctr[R];
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t e = b * so.per_blk + (j0 + r) * 256u + t;
+            kid[r] = win.count;
+            ctr[r] = 0;
+            if (j0 + r < so.items && e < so.n) {
+                kid[r] = desc[e].key_id;
+                ctr[r] = desc[e].counter;
+            }
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) pres[r] = kid[r] < win.count ? win.present[kid[r]] : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t e = b * so.per_blk + (j0 + r) * 256u + t;
+            if (j0 + r >= so.items || e >= so.n) break;
+            const uint32_t w = pres[r] ? kid[r] : win.count;
+            ws.keyw[e] = w;
+            ws.ctr[e] = ctr[r];
+            atomicAdd(&hist[(w >> so.shift[0]) & mask], 1u);
+        }
     }
     __syncthreads();
     ws.sort_hist[(size_t)b * 256 + t] = hist[t];
@@ -97,6 +114,7 @@ __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p
     const uint32_t nb2 = next ? 1u << so.bits[p + 1] : 0u;
     // digit t: the count in earlier workgroups, and the total (exclusive scan over digits below)
     uint32_t pre = 0, tot = 0;
+#pragma unroll 8
     for (uint32_t q = 0; q < so.nblk; q++) {
         const uint32_t h = hist[(size_t)q * 256 + t];
         tot += h;
@@ -121,32 +139,44 @@ __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p
     const uint32_t sh = so.shift[p], nbits = so.bits[p], mask = (1u << nbits) - 1u;
     const uint32_t sh2 = next ? so.shift[p + 1] : 0u, mask2 = nb2 - 1u;
     const uint64_t lt = (1ull << lane) - 1u;
-    for (uint32_t j = 0; j < so.items; j++) {
-        const uint32_t e = b * so.per_blk + j * 256u + t;
-        const bool valid = e < so.n;
-        const uint32_t key = valid ? src_k[e] : 0u;
-        const uint32_t val = FIRST ? e : (valid ? src_v[e] : 0u);
-        const uint32_t dg = (key >> sh) & mask;
-        uint64_t eq = __ballot(valid);
-        for (uint32_t bit = 0; bit < nbits; bit++) {
-            const uint64_t bb = __ballot((dg >> bit) & 1u);
-            eq &= ((dg >> bit) & 1u) ? bb : ~bb;
-        }
-        const uint32_t rank = (uint32_t)__popcll(eq & lt);
-        if (valid && rank == 0) wcnt[wv][dg] = (uint32_t)__popcll(eq);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = gbase[dg] + run[dg] + rank;
-            for (uint32_t v = 0; v < wv; v++) pos += wcnt[v][dg];
-            dst_k[pos] = key;
-            dst_v[pos] = val;
-            if (next) atomicAdd(&agg[(pos / so.per_blk) * nb2 + ((key >> sh2) & mask2)], 1u);
-        }
-        __syncthreads();
-        run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    // rounds of 256 packets, keys loaded kRxSortLoad rounds ahead
+    constexpr uint32_t R = kRxSortLoad;
+    for (uint32_t j0 = 0; j0 < so.items; j0 += R) {
+        uint32_t key[R], val[R];
 #pragma unroll
-        for (uint32_t v = 0; v < 4; v++) wcnt[v][t] = 0;
-        __syncthreads();
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t e = b * so.per_blk + (j0 + r) * 256u + t;
+            const bool valid = j0 + r < so.items && e < so.n;
+            key[r] = valid ? src_k[e] : 0u;
+            val[r] = FIRST ? e : (valid ? src_v[e] : 0u);
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            if (j0 + r >= so.items) break;  // uniform
+            const uint32_t e = b * so.per_blk + (j0 + r) * 256u + t;
+            const bool valid = e < so.n;
+            const uint32_t dg = (key[r] >> sh) & mask;
+            uint64_t eq = __ballot(valid);
+            for (uint32_t bit = 0; bit < nbits; bit++) {
+                const uint64_t bb = __ballot((dg >> bit) & 1u);
+                eq &= ((dg >> bit) & 1u) ? bb : ~bb;
+            }
+            const uint32_t rank = (uint32_t)__popcll(eq & lt);
+            if (valid && rank == 0) wcnt[wv][dg] = (uint32_t)__popcll(eq);
+            __syncthreads();
+            if (valid) {
+                uint32_t pos = gbase[dg] + run[dg] + rank;
+                for (uint32_t v = 0; v < wv; v++) pos += wcnt[v][dg];
+                dst_k[pos] = key[r];
+                dst_v[pos] = val[r];
+                if (next) atomicAdd(&agg[(pos / so.per_blk) * nb2 + ((key[r] >> sh2) & mask2)], 1u);
+            }
+            __syncthreads();
+            run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+#pragma unroll
+            for (uint32_t v = 0; v < 4; v++) wcnt[v][t] = 0;
+            __syncthreads();
+        }
     }
     if (next) {
         uint32_t* h2 = hist_all + (size_t)(p + 1) * kRxSortBlocks * 256;
@@ -339,6 +369,8 @@ __global__ __launch_bounds__(kRxThreads) void rx_admit_kernel(const neb_desc* __
         if (ok) {
             ws.adm[i] = 1;
             okm |= 1u << j;
+        } else {
+            status[i] = NEB_STATUS_REPLAY;  // (a slow window's statuses are rewritten on the host)
         }
     }
     // workgroup prefix of the admitted counts
@@ -372,47 +404,41 @@ __global__ void rx_gather_desc_kernel(const neb_desc* __restrict__ desc, RxDevWs
     if (j < *ws.nsub) ws.sub_desc[j] = desc[ws.sub_map[j]];
 }
 
-// tag verdicts back per packet; a failed one sends its window to the sequential host pass
-__global__ void rx_verdict_kernel(uint32_t n, RxDevWs ws, int all) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= (all ? n : *ws.nsub)) return;
-    const uint32_t i = all ? j : ws.sub_map[j];  // all: every packet was opened in arrival order
-    const int32_t st = ws.sub_status[j];
-    ws.verdict[i] = st;
-    if (st != NEB_STATUS_OK) atomicOr(&ws.wflag[ws.keyw[i]], kRxSlow);
-}
-
 __device__ __forceinline__ bool rx_fast(uint32_t fl) { return (fl & kRxTouched) && !(fl & (kRxRisky | kRxSlow)); }
 
-// per packet of a fast window: its status; its counter into the scratch bitmap, and into the
-// received count when it leaves the window — one atomic per (wave, window, word) instead of one per packet: a
-// single tunnel's batch would otherwise serialise tens of thousands of atomics on one address.
-// Every lane runs to the end (the shuffles need the whole wave).
-__global__ void rx_final_packet_agg_kernel(uint32_t n, RxDevWin win, RxDevWs ws, int32_t* __restrict__ status) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+// Per admitted packet (compacted order): its tag verdict into its status (a failure sends the
+// window to the sequential host pass, which rewrites that window's statuses), its counter into
+// the scratch bitmap when it stays in the final window, and into the received count when it
+// leaves it. The window's fast / slow state is not known yet: the finish applies the scratch and
+// the count to fast windows only and clears the scratch of the others. One atomic per (wave,
+// window, word) instead of one per packet (a single tunnel's batch would otherwise serialise
+// tens of thousands of atomics on one address); every lane runs to the end (the shuffles need
+// the whole wave).
+__global__ void rx_settle_kernel(RxDevWin win, RxDevWs ws, int32_t* __restrict__ status) {
+    __shared__ unsigned long long s_recv;
+    if (threadIdx.x == 0) s_recv = 0;
+    __syncthreads();
+    const uint32_t nsub = *ws.nsub;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t w = win.count;
-    uint64_t c = 0;
-    bool adm = false;
-    if (k < n) {
-        w = ws.run_w[k];
-        if (w < win.count && rx_fast(ws.wflag[w])) {
-            const uint32_t i = ws.run_i[k];
-            adm = ws.adm[i];
-            status[i] = adm ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
-            c = ws.run_c[k];
-        } else {
-            w = win.count;
-        }
-    }
-    uint64_t cur = 0, lo = 1, hi = 0;
-    if (adm) {
+    uint64_t c = 0, cur = 0, lo = 1, hi = 0;
+    bool live = j < nsub, ok = false;
+    if (live) {
+        const uint32_t i = ws.sub_map[j];
+        const int32_t st = ws.sub_status[j];
+        w = ws.keyw[i];
+        c = ws.ctr[i];
+        ws.verdict[i] = st;
+        status[i] = st;
+        ok = st == NEB_STATUS_OK;
+        if (!ok) atomicOr(&ws.wflag[w], kRxSlow);
         cur = ws.curnew[w];
         lo = ws.exit_lo[w];
         hi = ws.exit_hi[w];
     }
     const uint64_t len = win.length;
-    const bool in_final = adm && (cur < len || c > cur - len);
-    const bool leaves = adm && c >= lo && c <= hi;
+    const bool in_final = ok && (cur < len || c > cur - len);
+    const bool leaves = ok && c >= lo && c <= hi;
     const uint64_t p = c & (len - 1u);
     // word key of this lane's bit; lanes of one (window, word) OR their bits into one atomic
     const uint64_t wkey = in_final ? (((uint64_t)w << 32) | (p >> 6)) : ~0ull;
@@ -428,15 +454,25 @@ __global__ void rx_final_packet_agg_kernel(uint32_t n, RxDevWin win, RxDevWs ws,
             atomicOr(reinterpret_cast<unsigned long long*>(ws.scratch + ((size_t)w << win.words_lg) + (p >> 6)), bits);
         pending &= ~__ballot(mine);
     }
+    // counters leaving the window: one atomic per (wave, window), through LDS for the window of
+    // the workgroup's first packet
+    const uint32_t j0 = blockIdx.x * blockDim.x;
+    const uint32_t w0 = j0 < nsub ? ws.keyw[ws.sub_map[j0]] : win.count;
     uint64_t pend2 = __ballot(leaves);
     while (pend2) {
         const uint32_t leader = __builtin_ctzll(pend2);
         const uint32_t lw = __shfl(w, (int)leader);
         const uint64_t same = __ballot(leaves && w == lw);
-        if (__lane_id() == leader)
-            atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)__popcll(same));
+        if (__lane_id() == leader) {
+            if (w == w0)
+                atomicAdd(&s_recv, (unsigned long long)__popcll(same));
+            else
+                atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)__popcll(same));
+        }
         pend2 &= ~same;
     }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_recv) atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w0), s_recv);
 }
 
 // bits of the slots [a, b) within the word whose first slot is q0 (nb slots)
@@ -467,9 +503,15 @@ __global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
     const size_t wl = t >> lanes_lg;
     const uint32_t sub = (uint32_t)t & (L - 1u);
     const uint32_t w = wl < win.count ? (uint32_t)wl : 0u;
-    const bool fast = wl < win.count && rx_fast(ws.wflag[w]);
+    const uint32_t fl = wl < win.count ? ws.wflag[w] : 0u;
+    const bool fast = rx_fast(fl);
+    if ((fl & kRxTouched) && (fl & (kRxRisky | kRxSlow)) && sub == 0) *ws.need_host = 1u;  // a plain store
     uint64_t r = 0;
     uint64_t cur = 0, lo = 1, hi = 0;
+    if ((fl & kRxTouched) && !fast) {  // the settle may have set bits of a window finished on the host
+        uint64_t* scr = ws.scratch + ((size_t)w << win.words_lg);
+        for (uint32_t q = sub; q < win.words; q += L) scr[q] = 0;
+    }
     if (fast) {
         const uint64_t len = win.length, mask = len - 1u, cur0 = win.cur[w];
         cur = ws.curnew[w];
@@ -555,11 +597,11 @@ extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const
     return hipGetLastError();
 }
 
-// Phase 3: verdicts, then the parallel finish of every window whose admitted packets all verified.
+// Phase 3: verdicts and the admitted counters' bits, then the parallel finish of every window
+// whose admitted packets all verified.
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const RxDevWin* win, const RxDevWs* ws, int32_t* d_status,
-                                       int all, hipStream_t s) {
-    hipLaunchKernelGGL(neb::rx_verdict_kernel, rx_grid(n), dim3(256), 0, s, n, *ws, all);
-    hipLaunchKernelGGL(neb::rx_final_packet_agg_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
+                                       hipStream_t s) {
+    hipLaunchKernelGGL(neb::rx_settle_kernel, rx_grid(n), dim3(256), 0, s, *win, *ws, d_status);
     const uint32_t lanes_lg = win->words_lg < 6u ? win->words_lg : 6u;
     hipLaunchKernelGGL(neb::rx_final_window_kernel, rx_grid((size_t)win->count << lanes_lg), dim3(256), 0, s, *win,
                        *ws);

@@ -20,7 +20,7 @@ enum : uint32_t { kRxTouched = 1u, kRxRisky = 2u, kRxSlow = 4u };
 constexpr uint32_t kRxThreads = 256, kRxItems = 1, kRxBlock = kRxThreads * kRxItems;
 // the stable sort by window (rxwin.hip): at most kRxSortBlocks workgroups of 256 x items packets,
 // digits of at most 8 bits for one pass, else passes of at most kRxSortDigit bits
-constexpr uint32_t kRxSortBlocks = 64, kRxSortDigit = 7, kRxSortMaxPasses = 5;
+constexpr uint32_t kRxSortBlocks = 64, kRxSortDigit = 7, kRxSortMaxPasses = 5, kRxSortLoad = 4;
 
 struct RxDevWin {  // a set of windows of one length in device memory (neb_dwindows)
     uint32_t count;
@@ -72,6 +72,7 @@ struct RxDevWs {
     uint64_t* exit_hi;
     uint64_t* recv;
     uint64_t* scratch;  // count x words
+    uint32_t* need_host;  // pinned host word: set to 1 when a touched window is risky or slow
 };
 
 inline size_t rx_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -124,4 +125,4 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const n
                                      const neb::RxDevWs* ws, int32_t* d_status, hipStream_t s);
 extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const neb::RxDevWin* win, const neb::RxDevWs* ws,
-                                       int32_t* d_status, int all, hipStream_t s);
+                                       int32_t* d_status, hipStream_t s);

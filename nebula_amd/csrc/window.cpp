@@ -574,6 +574,7 @@ struct neb_dwindows {
     size_t ws_bytes = 0;
     neb::RxDevWs ws{};
     uint32_t ws_n = 0;
+    uint32_t* h_host = nullptr;  // pinned, mapped: the finish sets it when a window needs the host
 };
 
 namespace {
@@ -640,6 +641,12 @@ NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, 
         delete d;
         return NEB_ERR_HIP;
     }
+    if (hipHostMalloc((void**)&d->h_host, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess) {
+        d->h_host = nullptr;
+        hipFree(d->mem);
+        delete d;
+        return NEB_ERR_HIP;
+    }
     uint8_t* m = d->mem;
     v.present = (uint32_t*)m;
     m += b_present;
@@ -664,6 +671,7 @@ NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
         hipDeviceSynchronize();
         if (d->ws_mem) hipFree(d->ws_mem);
         if (d->mem) hipFree(d->mem);
+        if (d->h_host) hipHostFree(d->h_host);
     }
     delete d;
     return NEB_OK;
@@ -733,6 +741,8 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
         RX_HIP(hipMemsetAsync(d->ws.tab_min, 0, (size_t)8 << d->ws.tab_lg, s));
         d->ws.gen = 1;
     }
+    *d->h_host = 0;
+    d->ws.need_host = d->h_host;
     const neb::RxDevWs& ws = d->ws;
 
     static const bool prof = std::getenv("NEB_RX_PROF") != nullptr;
@@ -750,14 +760,17 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
     if (rc != NEB_OK) return rc;
     const auto t2 = now();
     // 3. the parallel finish of every window whose admitted packets all verified
-    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, 0, s));
+    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, s));
     const auto t3 = now();
-    std::vector<uint32_t> flag;
-    if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
     RX_HIP(hipStreamSynchronize(s));
     if (prof)
         std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, open %.1f, finish %.1f us, wait %.1f us\n", n, us(t0, t1),
                      us(t1, t2), us(t2, t3), us(t3, now()));
+    // the finish flags, in pinned host memory, whether any window needs the sequential finish
+    if (__atomic_load_n(d->h_host, __ATOMIC_ACQUIRE) == 0) return NEB_OK;
+    std::vector<uint32_t> flag;
+    if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
+    RX_HIP(hipStreamSynchronize(s));
     std::vector<uint32_t> run_w, run_i;
     std::vector<uint64_t> run_c;
     std::vector<uint8_t> adm;
