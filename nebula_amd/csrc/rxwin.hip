@@ -194,11 +194,9 @@ __device__ __forceinline__ uint32_t rx_hash(uint32_t w, uint64_t c, uint32_t lg)
 }
 
 // The slot of packet i's (window, counter) key: claimed by the first to arrive at it, found by
-// comparing the owner's key (exact, no hash comparison); the table has at least 2n slots. An
+// comparing the owner's key (exact, no hash comparison); the table has at least 4n slots. An
 // entry whose generation is not this batch's is empty.
-__device__ __forceinline__ uint32_t rx_slot(const RxDevWs& ws, uint32_t i, bool insert) {
-    const uint32_t w = ws.keyw[i];
-    const uint64_t c = ws.ctr[i];
+__device__ __forceinline__ uint32_t rx_slot(const RxDevWs& ws, uint32_t i, uint32_t w, uint64_t c, bool insert) {
     const uint32_t tmask = (1u << ws.tab_lg) - 1u;
     const uint64_t mine = ((uint64_t)ws.gen << 32) | (i + 1u);
     uint32_t h = rx_hash(w, c, ws.tab_lg);
@@ -257,7 +255,7 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_kernel(uint32_t n, RxDevWi
         uint32_t fl = c[j] >= kRxRiskyCounter ? kRxRisky : 0u;
         if (hd[j]) fl |= kRxTouched | (win.cur[w] >= kRxRiskyCounter ? kRxRisky : 0u);
         if (fl) atomicOr(&ws.wflag[w], fl);
-        atomicMax(reinterpret_cast<unsigned long long*>(ws.tab_min + rx_slot(ws, i, true)),
+        atomicMax(reinterpret_cast<unsigned long long*>(ws.tab_min + rx_slot(ws, i, w, c[j], true)),
                   ((unsigned long long)ws.gen << 32) | (0xFFFFFFFFu - i));
     }
     __syncthreads();  // s_fh
@@ -361,10 +359,12 @@ __global__ __launch_bounds__(kRxThreads) void rx_admit_kernel(const neb_desc* __
         const uint64_t prev = head ? cur0 : max(cur0, incl_at(k - 1u));
         const uint64_t c = ws.run_c[k];
         const uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
-        bool ok = c > prev;
-        if (!ok && rx_in_window(c, prev, win.length)) ok = !(c <= cur0 && rx_bit(bits, win.length - 1u, c));
-        // the first occurrence of (window, counter)
-        ok = ok && ws.tab_min[rx_slot(ws, i, false)] == (((uint64_t)ws.gen << 32) | (0xFFFFFFFFu - i));
+        bool ok = c > prev;  // above every earlier counter of the run: its first occurrence too
+        if (!ok && rx_in_window(c, prev, win.length)) {
+            ok = !(c <= cur0 && rx_bit(bits, win.length - 1u, c));
+            // the first occurrence of (window, counter)
+            ok = ok && ws.tab_min[rx_slot(ws, i, w, c, false)] == (((uint64_t)ws.gen << 32) | (0xFFFFFFFFu - i));
+        }
         ids[j] = i;
         if (ok) {
             ws.adm[i] = 1;

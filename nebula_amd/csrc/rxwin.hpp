@@ -52,7 +52,7 @@ struct RxDevWs {
     uint64_t* incl;     // segmented inclusive max of the counters within each block of kRxBlock
     uint64_t* blk_max;  // per block: incl at its last element
     uint32_t* blk_fh;   // per block: position of its first run head (kRxBlock: none)
-    // first occurrences: an open-addressing table keyed by (window, counter), 2^tab_lg slots,
+    // first occurrences: an open-addressing table keyed by (window, counter), 2^tab_lg >= 4n slots,
     // tagged with the batch generation (an entry of an older batch is empty, so the table is
     // never cleared between batches); a slot's owner (gen:32 | arrival index + 1) names its key
     // through keyw / ctr
@@ -102,7 +102,7 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
     w.blk_max = (uint64_t*)take(nblk * 8);
     w.blk_fh = (uint32_t*)take(nblk * 4);
     w.tab_lg = 1;
-    while ((1ull << w.tab_lg) < 2ull * n) w.tab_lg++;
+    while ((1ull << w.tab_lg) < 4ull * n) w.tab_lg++;  // at most a quarter full
     w.tab_owner = (uint64_t*)take((size_t)8 << w.tab_lg);
     w.tab_min = (uint64_t*)take((size_t)8 << w.tab_lg);
     w.sub_map = (uint32_t*)take((size_t)n * 4);
