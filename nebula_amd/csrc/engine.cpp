@@ -43,6 +43,7 @@ struct SchedSpace {
     uint32_t n_cap = 0;
     neb::SchedWs ws{};
     hipEvent_t done = nullptr;
+    bool dirty = true;  // the bin counts need a clear (new buffer, or a batch that failed to launch)
     std::mutex mu;
 };
 
@@ -460,7 +461,13 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
         hipError_t err = hipEventCreateWithFlags(&sp.done, hipEventDisableTiming);
         if (err != hipSuccess) return err;
     }
-    if (n <= sp.n_cap && sp.mem) return hipSuccess;
+    if (n <= sp.n_cap && sp.mem && !sp.dirty) return hipSuccess;
+    if (n <= sp.n_cap && sp.mem) {  // the bins are cleared as they are consumed, except after a failure
+        hipError_t err = hipEventSynchronize(sp.done);
+        if (err == hipSuccess) err = hipMemset(sp.ws.counters, 0, (neb::kSchedCounters + 2u * neb::sched_nbins(e->max_keys)) * 4u);
+        if (err == hipSuccess) sp.dirty = false;
+        return err;
+    }
     const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
     const uint32_t nb = neb::sched_nbins(e->max_keys);
     const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys);
@@ -492,6 +499,9 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     sp.ws.max_chunks = mc;
     sp.bytes = bytes;
     sp.n_cap = cap;
+    err = hipMemset(sp.ws.counters, 0, b_counters);  // once: the binning clears its counts as it uses them
+    if (err != hipSuccess) return err;
+    sp.dirty = false;
     return hipSuccess;
 }
 
@@ -515,6 +525,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                         sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count, s, hdr_from_dst);
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
+        if (err != hipSuccess) sp.dirty = true;
         return err;
     }
     return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n, e->cu_count,

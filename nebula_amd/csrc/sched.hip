@@ -20,6 +20,9 @@ __device__ __forceinline__ uint32_t size_class(const neb_desc& d, uint32_t lpp) 
 // execute at the memory side (MI355X_MICROARCH.md, global atomics), ≈55 µs per 1 Mi packets each.
 __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn,
                                   uint32_t max_keys, uint32_t lpp, SchedWs ws) {
+    // the cursors are cleared here (the previous batch's crypto kernel has finished with them);
+    // the bin counts were cleared by the previous batch's pass 2 as it read them
+    if (blockIdx.x == 0 && threadIdx.x < kSchedCounters) ws.counters[threadIdx.x] = 0;
     if (dn) n = min(n, *dn);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const neb_desc d = desc[i];
@@ -41,6 +44,7 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t nb = sched_nbins(max_keys);
     const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
     const uint32_t c = b < nb ? ws.hist[b] : 0u;
+    if (c) ws.hist[b] = 0;  // clear for the next batch
     const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
     const uint32_t nwide = NEB_WIDE_CHUNKS ? c / kWidePkts : 0u;
     const uint32_t rest = c - nwide * kWidePkts;
@@ -95,9 +99,6 @@ __global__ void sched_scatter_kernel(uint32_t n, const uint32_t* dn, SchedWs ws)
 extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
                                       uint32_t lpp, const neb::SchedWs* ws, hipStream_t s) {
     const uint32_t nb = neb::sched_nbins(max_keys);
-    // counters, hist and fill are contiguous: one memset per batch
-    hipError_t e = hipMemsetAsync(ws->counters, 0, (neb::kSchedCounters + 2u * nb) * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
     hipLaunchKernelGGL(neb::sched_hist_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp, *ws);

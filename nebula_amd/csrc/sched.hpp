@@ -70,6 +70,8 @@ __host__ __device__ inline uint32_t sched_max_chunks(uint32_t n, uint32_t max_ke
 
 }  // namespace neb
 
-// Host launcher (sched.hip): zero the counters and run the three binning passes on stream s.
+// Host launcher (sched.hip): the three binning passes on stream s. The workspace's counters and
+// bin counts must be zero before the first batch (pass 1 clears the cursors and pass 2 the bin
+// counts it reads, so a batch leaves them zero for the next).
 extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
                                       uint32_t lpp, const neb::SchedWs* ws, hipStream_t s);
