@@ -25,6 +25,8 @@
 //  * GHASH, mixed keys: each packet's round keys and Shoup tables for H, H^2, H^4, H^8, H^16
 //    (NLP = 2) are staged in the wave's LDS slice per packet group.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include <type_traits>
@@ -801,14 +803,68 @@ struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position table
     }
 };
 
+// ---- the TX checksum in the seal (CS; tx.hip kTxCsumFlag) ----------------------------------
+// The TX segment kernel leaves in the L4 checksum field the partial sum of everything but the
+// payload bytes the seal reads from the TUN read ([hdr, len)); the seal adds those bytes' 16-bit
+// words as it encrypts them. The field's block was encrypted with the partial (round 0): the
+// packet's last lane then stores the field's final ciphertext bytes and moves the tag by the
+// change, S' = S ^ Δ·H^e (GHASH is linear; e = n + 1 - the field block's index), with the Shoup
+// tables of H^(2^j), j < 10, in LDS (e < 1024: segments under 16 KB).
+// desc.flags = hdr | field << 12 | kind << 24 | parity << 26 (kind 1: TCP or a plain packet, 2:
+// UDP, whose computed zero goes out as 0xFFFF; parity: the checksum start's, for the word pairing).
+constexpr uint32_t kCsHdrMask = 0xFFFu;
+__device__ __forceinline__ uint32_t le16_sum(uint4 v) {
+    return (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) + (v.z >> 16) +
+           (v.w & 0xFFFFu) + (v.w >> 16);
+}
+__device__ __forceinline__ uint32_t block_byte(uint4 v, uint32_t q) {
+    const uint32_t w = q < 4u ? v.x : q < 8u ? v.y : q < 12u ? v.z : v.w;
+    return (w >> (8u * (q & 3u))) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t cs_fold16(uint32_t s) {
+    s = (s & 0xFFFFu) + (s >> 16);
+    s = (s & 0xFFFFu) + (s >> 16);
+    return s;
+}
+// The tag lane: the final checksum from the packet's payload sum `acc` (little-endian words) and
+// the field word `fk` (partial << 16 | keystream bytes there); stores the field's ciphertext and
+// returns Δ·H^e for the tag.
+__device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uint32_t na, uint32_t acc, uint32_t fk,
+                                              uint8_t* arena, const uint4* pow2) {
+    const uint32_t kind = (d.flags >> 24) & 3u, f = (d.flags >> 12) & 0xFFFu;
+    uint32_t sum = cs_fold16(acc);
+    if (!((d.flags >> 26) & 1u)) sum = ((sum & 0xFFu) << 8) | (sum >> 8);  // big-endian words
+    const uint32_t fval = fk >> 16, ks16 = fk & 0xFFFFu;
+    uint32_t c = ~cs_fold16(sum + fval) & 0xFFFFu;
+    if (kind == 2u && c == 0u) c = 0xFFFFu;
+    const uint32_t delta = fval ^ c;
+    __threadfence_block();  // the field's block was stored by a lane of this wave in an earlier round
+    uint8_t* ct = arena + d.dst_off + f;
+    ct[0] = (uint8_t)((ks16 ^ c) >> 8);
+    ct[1] = (uint8_t)(ks16 ^ c);
+    // Δ as a GHASH block (big-endian words): bytes q and q + 1 (q < 15: the segment kernel keeps
+    // the field inside one block)
+    const uint32_t q = f & 15u, q1 = q + 1u;
+    const uint32_t hi = (delta >> 8) << (24u - 8u * (q & 3u)), lo = (delta & 0xFFu) << (24u - 8u * (q1 & 3u));
+    uint4 corr = make_uint4(((q >> 2) == 0u ? hi : 0u) | ((q1 >> 2) == 0u ? lo : 0u),
+                            ((q >> 2) == 1u ? hi : 0u) | ((q1 >> 2) == 1u ? lo : 0u),
+                            ((q >> 2) == 2u ? hi : 0u) | ((q1 >> 2) == 2u ? lo : 0u),
+                            ((q >> 2) == 3u ? hi : 0u) | ((q1 >> 2) == 3u ? lo : 0u));
+    const uint32_t e = n - na - (f >> 4);  // n + 1 - (na + f / 16 + 1)
+    for (uint32_t j = 0; j < 10u; j++)
+        if ((e >> j) & 1u) corr = gf_mul_shoup(corr, j * 256u, pow2);
+    return corr;
+}
+
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
-template <bool OPEN, bool BS, class GH, class TL, class EJ = Ej0Reg>
+template <bool OPEN, bool BS, bool CS = false, class GH, class TL, class EJ = Ej0Reg>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
                                                  uint32_t lane, uint32_t lg, EJ ej0 = EJ{},
-                                                 const uint32_t* bs_rec = nullptr, uint32_t bs_phase = 0) {
+                                                 const uint32_t* bs_rec = nullptr, uint32_t bs_phase = 0,
+                                                 const uint4* cs_pow = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
@@ -817,7 +873,11 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
     if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
     const bool run = valid && st == NEB_STATUS_OK;
-    const uint32_t hdr = args.hdr_from_dst ? d.flags : 0u;
+    const uint32_t hdr = args.hdr_from_dst ? d.flags & kCsHdrMask : 0u;
+    // CS: this lane's payload word sum, and (the field's lane) partial << 16 | keystream bytes
+    uint32_t cs_acc = 0, cs_fk = 0;
+    const bool cs_on = CS && !OPEN && ((d.flags >> 24) & 3u) != 0u;
+    const uint32_t cs_f = (d.flags >> 12) & 0xFFFu;
     PktShape sh;
     sh.na = (d.aad_len + 15u) >> 4;
     sh.m = (d.len + 15u) >> 4;
@@ -849,6 +909,9 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
             if (__all(full)) {
                 const uint8_t* sp = args.arena + d.src_off + off;
                 const uint4 in = __all(((uint32_t)(uintptr_t)sp & 3u) == 0u) ? load_u4_a4(sp) : load_shifted16(sp);
+                if constexpr (CS) {
+                    if (cs_on) cs_acc += le16_sum(in);
+                }
                 const uint4 out = xor4(in, ks);
                 *reinterpret_cast<uint4*>(args.arena + d.dst_off + off) = out;
                 A = xor4(G, bswap4(OPEN ? in : out));
@@ -856,6 +919,21 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
             }
 #endif
             const uint4 in = gcm_lane_load(d, b, args.arena, hdr);
+            if constexpr (CS) {
+                if (cs_on && b.is_ct) {
+                    const uint32_t off = 16u * (b.k - 1u);
+                    const uint32_t hi = min(16u, d.len - off), lo = hdr > off ? min(hdr - off, 16u) : 0u;
+                    if (lo < hi) {  // the bytes of [hdr, len) in this block
+                        const uint4 v = mask_block(in, hi);
+                        cs_acc += le16_sum(xor4(v, mask_block(v, lo)));
+                    }
+                    if (cs_f - off < 16u) {
+                        const uint32_t q = cs_f - off;
+                        cs_fk = (block_byte(in, q) << 24) | (block_byte(in, q + 1u) << 16) | (block_byte(ks, q) << 8) |
+                                block_byte(ks, q + 1u);
+                    }
+                }
+            }
             A = xor4(G, gcm_lane_io<OPEN>(d, b, in, ks, args.arena, ej0));
         };
         auto horner = [&](uint32_t r) -> uint4 {
@@ -935,7 +1013,16 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
         else rounds(std::integral_constant<int, 0>{});
     }
-    const uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
+    if constexpr (CS) {
+        for (uint32_t sft = 1; sft < LPP; sft <<= 1) {
+            cs_acc += (uint32_t)__shfl_xor((int)cs_acc, (int)sft);
+            cs_fk |= (uint32_t)__shfl_xor((int)cs_fk, (int)sft);
+        }
+    }
+    uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
+    if constexpr (CS) {
+        if (run && cs_on && l == LPP - 1u) V = xor4(V, gcm_csum_fix(d, sh.n, sh.na, cs_acc, cs_fk, args.arena, cs_pow));
+    }
     if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
     if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
 }
@@ -1024,9 +1111,14 @@ struct SingleLds {
 };
 #endif
 
-template <bool OPEN>
+struct SingleLdsCs : SingleLds {
+    uint4 pow2[10 * 16];  // 2.5 KiB  Shoup tables of H^(2^j), j < 10 (the TX checksum correction)
+};
+
+// CS: the TX seal with the L4 checksums (gcm_csum_fix)
+template <bool OPEN, bool CS = false>
 __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_kernel(GcmArgs args) {
-    __shared__ SingleLds lds;
+    __shared__ std::conditional_t<CS, SingleLdsCs, SingleLds> lds;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
@@ -1070,6 +1162,11 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
 #endif
 
+    const uint4* cs_pow = nullptr;
+    if constexpr (CS) {
+        if (tid < 160u) lds.pow2[tid] = ld_rec4(srec, rec_shoup_pow2(tid >> 4) + 4u * (tid & 15u));
+        cs_pow = lds.pow2;
+    }
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
@@ -1117,18 +1214,26 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
             gcm_packet_group<OPEN, true>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, Ej0Reg{},
                                          srec, (wave >> 2) & 3u);
         else
-            gcm_packet_group<OPEN, false>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg);
+            gcm_packet_group<OPEN, false, CS>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg,
+                                              Ej0Reg{}, nullptr, 0u, cs_pow);
     }
 }
 
 // The tail pass (NEB_SINGLE_TAIL): the packets after gcm_single_kernel's full passes over
-// args.tail_slots waves, 4 per wave with 16 lanes each: the two-table AES (64 KiB), Horner stride
-// H^16 on its position tables, the final tree on the Shoup tables of H, H^2, H^4, H^8 (GhShoup).
+// args.tail_slots waves, 2^kTailLg lanes per packet: the two-table AES (64 KiB), Horner stride
+// H^(2^kTailLg) on its position tables, the final tree on the Shoup tables of H .. H^(2^(kTailLg-1))
+// (GhShoup). A tail is small and runs on few waves, so its time is one packet's latency: at 64
+// lanes a 1300-B packet takes 2 rounds instead of 6 at 16.
+#ifndef NEB_TAIL_LG
+#define NEB_TAIL_LG 6
+#endif
+constexpr uint32_t kTailLg = NEB_TAIL_LG, kTailPpw = kWave >> kTailLg;
+static_assert(kTailLg == 4 || kTailLg == 6, "tail tables exist for 16 and 64 lanes");
 constexpr int kTailWaves = 8;
 struct TailLds {
-    uint2 ttab[256 * 32];   // 64 KiB T-table pairs, 32 copies
-    uint4 shoup[4 * 16];    // 1 KiB
-    uint4 pos[8 * 16];      // 2 KiB
+    uint2 ttab[256 * 32];      // 64 KiB T-table pairs, 32 copies
+    uint4 shoup[kTailLg * 16]; // 1-1.5 KiB
+    uint4 pos[8 * 16];         // 2 KiB
 };
 template <bool OPEN>
 __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(GcmArgs args) {
@@ -1139,21 +1244,29 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw, slots = args.tail_slots;
     if (ngroups <= slots || ngroups % slots == 0u) return;  // no partial pass: nothing to do
     const uint32_t p0 = ngroups / slots * slots * kPpw;
-    const uint32_t tgroups = (npkt - p0 + 3u) / 4u;
+    const uint32_t tgroups = (npkt - p0 + kTailPpw - 1u) / kTailPpw;
     if (blockIdx.x * kTailWaves >= tgroups) return;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
+#ifndef NEB_ABLATE_TAIL_STAGE  // (ablation: wrong results, timing only)
     for (uint32_t i = tid; i < 256u * 32u; i += kTailWaves * kWave) lds.ttab[i] = ttab_entry(i);
-    if (tid < 64u) lds.shoup[tid] = ld_rec4(srec, kRecShoup + 64u * ((1u << (tid >> 4)) - 1u) + 4u * (tid & 15u));
-    if (tid < 128u) lds.pos[tid] = ld_rec4(srec, kRecPos16 + 4u * tid);
+#endif
+    if (tid < 16u * kTailLg) {  // M[v] of H^(2^j), j < kTailLg
+        const uint32_t j = tid >> 4, v = tid & 15u;
+        lds.shoup[tid] = ld_rec4(srec, rec_shoup_pow2(j) + 4u * v);
+    }
+    if (tid < 128u) lds.pos[tid] = ld_rec4(srec, (kTailLg == 6u ? kRecPos64 : kRecPos16) + 4u * tid);
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
     const TLook T{lds.ttab, ttab_lane_base(lane)};
     const GhShoup gh{lds.shoup, lds.pos};
     const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
+#ifdef NEB_ABLATE_TAIL_WORK  // (ablation: wrong results, timing only)
+    return;
+#endif
     for (uint32_t t = blockIdx.x * kTailWaves + wave; t < tgroups; t += gridDim.x * kTailWaves) {
-        const uint32_t p = p0 + 4u * t + (lane >> 4);
-        gcm_packet_group<OPEN, false>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, 4u);
+        const uint32_t p = p0 + kTailPpw * t + (lane >> kTailLg);
+        gcm_packet_group<OPEN, false>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, kTailLg);
     }
 }
 
@@ -1463,6 +1576,56 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         uint32_t* o = rec + kRecPos1 + 4u * t;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
+    // H^32 .. H^512 by squaring (the tail kernel's 64-lane packets, the TX seal's checksum
+    // correction): P·Q is the XOR of basis[i] = x^i·Q over the set bits i of P (lane i < 128), as
+    // for H^2..H^16 above
+    auto basis_of = [&](uint4 q, uint32_t cnt) {
+        __syncthreads();  // basis[] is free again
+        if (t == 0u)
+            for (uint32_t i = 0; i < cnt; i++) {
+                basis[i] = q;
+                q = gf_mulx(q);
+            }
+        __syncthreads();
+    };
+    auto mul_by_basis = [&](uint4 P) -> uint4 {
+        uint4 c = make_uint4(0, 0, 0, 0);
+        if (t < 128u) {
+            const uint32_t w = t < 32u ? P.x : (t < 64u ? P.y : (t < 96u ? P.z : P.w));
+            if ((w >> (31u - (t & 31u))) & 1u) c = basis[t];
+        }
+        for (int m = 32; m >= 1; m >>= 1) c = xor4(c, shfl_xor4(c, m));
+        if (t == 0u || t == 64u) part[t >> 6] = c;
+        __syncthreads();
+        const uint4 r = xor4(part[0], part[1]);
+        __syncthreads();
+        return r;
+    };
+    basis_of(hp[15], 128u);
+    const uint4 h32 = mul_by_basis(hp[15]);
+    basis_of(h32, 128u);
+    const uint4 h64 = mul_by_basis(h32);
+    basis_of(h64, 128u);
+    const uint4 h128 = mul_by_basis(h64);
+    if (t < 128u) {  // the position tables of H^64 (basis[0, 32))
+        const uint32_t r = t >> 4, v = t & 15u;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        for (uint32_t j = 0; j < 4; j++)
+            if ((v >> (3 - j)) & 1u) e = xor4(e, basis[4 * r + j]);
+        uint32_t* o = rec + kRecPos64 + 4u * t;
+        o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
+    }
+    basis_of(h128, 128u);
+    const uint4 h256 = mul_by_basis(h128);
+    basis_of(h256, 128u);
+    const uint4 h512 = mul_by_basis(h256);
+    if (t < 80u) {  // Shoup tables of H^32, H^64, H^128, H^256, H^512
+        const uint32_t k = t >> 4, v = t & 15u;
+        const uint4 P = k == 0u ? h32 : k == 1u ? h64 : k == 2u ? h128 : k == 3u ? h256 : h512;
+        const uint4 e = gf_tab_entry(P, v);
+        uint32_t* o = rec + rec_shoup_pow2(5u + k) + 4u * v;
+        o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
+    }
 }
 
 }  // namespace neb
@@ -1494,6 +1657,24 @@ static hipError_t launch_grid(K kern, int threads, uint32_t work_waves, int cu_c
     return hipGetLastError();
 }
 
+// Waves of gcm_single_kernel's grid for a batch of at most n packets (a full pass is that many
+// groups of kPpw packets; the packets after the last full pass go to the tail kernel). The TX
+// segment kernel uses it to know which segments the tail seals (without the checksum).
+extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int hdr_from_dst) {
+    const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
+    const void* kern = open ? (const void*)neb::gcm_single_kernel<true>
+                            : hdr_from_dst == 2 ? (const void*)neb::gcm_single_kernel<false, true>
+                                                : (const void*)neb::gcm_single_kernel<false>;
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, neb::kSingleThreads, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    uint32_t cap = (uint32_t)(per_cu * cu_count);
+    // test hook: a smaller grid, so that small batches have a partial last pass (the tail kernel)
+    if (const char* g = std::getenv("NEB_SINGLE_MAX_GRID")) cap = std::max(1u, std::min(cap, (uint32_t)std::atoi(g)));
+    const uint32_t grid = std::min((groups + neb::kSingleWaves - 1u) / neb::kSingleWaves, cap);
+    return grid * neb::kSingleWaves;
+}
+
 // One tunnel key (key_hint) for every descriptor.
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
@@ -1501,21 +1682,26 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
                                            int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
-    const void* kern = open ? (const void*)neb::gcm_single_kernel<true> : (const void*)neb::gcm_single_kernel<false>;
-    int per_cu = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, neb::kSingleThreads, 0) != hipSuccess || per_cu < 1)
-        per_cu = 1;
-    const uint32_t grid = std::min((groups + neb::kSingleWaves - 1u) / neb::kSingleWaves, (uint32_t)(per_cu * cu_count));
-    const uint32_t slots = grid * neb::kSingleWaves;
+    const bool cs = !open && hdr_from_dst == 2;  // the TX seal with its checksums (tx.hip)
+    const uint32_t slots = neb_gcm_single_slots(n, cu_count, open, hdr_from_dst);
     // a partial last pass (at most n packets; the real count may be on the device) goes to the
     // tail kernel, 16 lanes per packet
     const bool tail = NEB_SINGLE_TAIL && !NEB_GHASH8 && groups > slots && (d_n || groups % slots);
     if (tail) a.tail_slots = slots;
-    hipError_t e = open ? launch_grid(neb::gcm_single_kernel<true>, neb::kSingleThreads, groups, cu_count, s, a)
-                        : launch_grid(neb::gcm_single_kernel<false>, neb::kSingleThreads, groups, cu_count, s, a);
+    const dim3 grid(slots / neb::kSingleWaves);
+    if (grid.x == 0) return hipSuccess;
+    if (open)
+        hipLaunchKernelGGL(neb::gcm_single_kernel<true>, grid, dim3(neb::kSingleThreads), 0, s, a);
+    else if (cs)
+        hipLaunchKernelGGL((neb::gcm_single_kernel<false, true>), grid, dim3(neb::kSingleThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(neb::gcm_single_kernel<false>, grid, dim3(neb::kSingleThreads), 0, s, a);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess || !tail) return e;
-    const uint32_t tail_pkts = n - groups / slots * slots * neb::kPpw;  // the largest tail n allows
-    const uint32_t tgrid = ((tail_pkts + 3u) / 4u + neb::kTailWaves - 1u) / neb::kTailWaves;
+    // the largest tail: under one pass, and n packets (a device count may leave a partial pass
+    // even when the bound n is a whole number of passes)
+    const uint32_t tail_pkts = std::min(n, slots * neb::kPpw);
+    const uint32_t tgrid = ((tail_pkts + neb::kTailPpw - 1u) / neb::kTailPpw + neb::kTailWaves - 1u) / neb::kTailWaves;
     if (open)
         hipLaunchKernelGGL(neb::gcm_single_tail_kernel<true>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), 0, s, a);
     else

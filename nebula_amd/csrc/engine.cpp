@@ -29,6 +29,10 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             uint32_t* d_counters, uint32_t max_chunks, int cu_count,
                                             hipStream_t s, int hdr_from_dst);
 extern "C" hipError_t neb_gcm_probe(void);
+extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int hdr_from_dst);
+#ifndef NEB_TX_CSUM_SEAL
+#define NEB_TX_CSUM_SEAL 1  // 0: the segment kernel sums every checksum (A/B)
+#endif
 extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
@@ -970,9 +974,14 @@ static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, c
     HIP_TRY(hipStreamWaitEvent(s, tx.done, 0));
     HIP_TRY(neb_tx_plan(d_pk, npk, d_in, d_tun, ntun, e->d_keys, e->max_keys, alg, &tx.ws, out_cap, max_wires,
                         d_pk_status, d_nwires, s));
-    HIP_TRY(neb_tx_segment(d_pk, npk, d_in, d_tun, d_out, &tx.ws, d_wires, d_nwires, max_wires, e->cu_count, s));
+    // one tunnel key with AES-GCM: the seal sums the payload into the L4 checksums itself, so the
+    // segment kernel does not read the payload (aes_gcm.hip gcm_csum_fix)
+    const bool cs = neb::kTxSealFromInput && NEB_TX_CSUM_SEAL && alg == NEB_ALG_AESGCM && key_hint != NEB_KEYS_MIXED;
+    const uint32_t cs_slots = cs ? neb_gcm_single_slots(max_wires, e->cu_count, 0, 2) : 0u;
+    HIP_TRY(neb_tx_segment(d_pk, npk, d_in, d_tun, d_out, &tx.ws, d_wires, d_nwires, max_wires, e->cu_count, cs_slots,
+                           s));
     HIP_TRY(launch_batch(e, alg, 0, tx.ws.seal_desc, max_wires, d_out, d_wire_status, key_hint, s, d_nwires, nullptr,
-                         neb::kTxSealFromInput));
+                         cs ? 2 : (int)neb::kTxSealFromInput));
     HIP_TRY(neb_tx_finish(d_tun, npk, ntun, &tx.ws, s));
     HIP_TRY(hipEventRecord(tx.done, s));
     return NEB_OK;

@@ -4,9 +4,9 @@
 
 namespace neb {
 
-// One key record per installed tunnel key (18.5 KiB): the first 512 B hold the key schedule and raw
-// H powers; the rest holds GHASH lookup tables precomputed at install time (AES-GCM only).
-constexpr uint32_t kKeyRecDwords = 4736;
+// One key record per installed tunnel key (21.75 KiB): the first 512 B hold the key schedule and
+// raw H powers; the rest holds GHASH lookup tables precomputed at install time (AES-GCM only).
+constexpr uint32_t kKeyRecDwords = 5568;
 constexpr uint32_t kKeyRecBytes = kKeyRecDwords * 4;
 
 // AES-256-GCM record
@@ -28,7 +28,18 @@ constexpr uint32_t kRecPos8 = kRecFull + 32 * 16 * 4;
 constexpr uint32_t kRecPos16 = kRecPos8 + 8 * 16 * 4;
 // position tables of H itself: the single-key kernel's final quad Horner (4 multiplies by H)
 constexpr uint32_t kRecPos1 = kRecPos16 + 8 * 16 * 4;
-static_assert(kRecPos1 + 8 * 16 * 4 == kKeyRecDwords, "record layout");
+// the Shoup table of H^32 and the position tables of H^64: the single-key tail kernel's packets of
+// 64 lanes (Horner stride H^64, final tree up to H^32)
+constexpr uint32_t kRecShoup32 = kRecPos1 + 8 * 16 * 4;
+constexpr uint32_t kRecPos64 = kRecShoup32 + 16 * 4;
+// Shoup tables of H^64, H^128, H^256, H^512: with M_1, M_2, M_4, M_8, M_16 and M_32 above, the
+// binary powers that take a block to any H^e, e < 1024 (the TX seal's checksum correction)
+constexpr uint32_t kRecShoupHi = kRecPos64 + 8 * 16 * 4;
+static_assert(kRecShoupHi + 4 * 16 * 4 == kKeyRecDwords, "record layout");
+// record offset of the Shoup table of H^(2^j), j = 0..9
+__host__ __device__ constexpr uint32_t rec_shoup_pow2(uint32_t j) {
+    return j < 5u ? kRecShoup + 64u * ((1u << j) - 1u) : (j == 5u ? kRecShoup32 : kRecShoupHi + 64u * (j - 6u));
+}
 // position tables of H^(2^lg), lg = 0, 2, 3, 4 (lg 0: the mixed-key kernel's one-lane chunks)
 __host__ __device__ constexpr uint32_t rec_pos_table(uint32_t lg) {
     return lg == 0u ? kRecPos1 : (lg == 2u ? kRecFull : (lg == 3u ? kRecPos8 : kRecPos16));

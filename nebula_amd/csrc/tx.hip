@@ -494,14 +494,28 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
     return v;
 }
 
-__global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_kernel(const neb_tx_packet* __restrict__ pk,
+// CSM (the seal sums the payloads, cs_slots != 0): no payload registers, so more waves per CU
+// (96 VGPRs, 5 blocks; 6 spills): the kernel is a chain of dependent loads per segment, bound by
+// how many segments are in flight
+#ifndef NEB_TX_CSM_BLOCKS
+#define NEB_TX_CSM_BLOCKS 5
+#endif
+template <bool CSM>
+__global__ __launch_bounds__(kTxWaves * 64, CSM ? NEB_TX_CSM_BLOCKS : NEB_TX_MINBLOCKS) void tx_segment_kernel(const neb_tx_packet* __restrict__ pk,
                                                                      const uint8_t* __restrict__ in,
                                                                      const neb_tx_tunnel* __restrict__ tun,
                                                                      uint8_t* __restrict__ out, TxWs ws,
                                                                      neb_tx_wire* __restrict__ wires,
-                                                                     const uint32_t* __restrict__ d_nwires) {
+                                                                     const uint32_t* __restrict__ d_nwires,
+                                                                     uint32_t cs_slots) {
     const uint32_t g = threadIdx.x & (kTxGroup - 1u);  // lane within the segment's group
     const uint32_t nw = __builtin_amdgcn_readfirstlane(*d_nwires);
+    // cs_slots != 0: the single-key seal sums the payload into the L4 checksums (aes_gcm.hip
+    // gcm_csum_fix), except for the segments after its last full pass of cs_slots waves x 16
+    // packets, which its tail kernel seals: those are summed here
+    const uint32_t ngroups = (nw + 15u) / 16u;
+    const uint32_t cs_p0 =
+        cs_slots == 0u ? 0u : (ngroups > cs_slots && ngroups % cs_slots) ? ngroups / cs_slots * cs_slots * 16u : nw;
     const uint32_t groups_per_block = blockDim.x / kTxGroup;
     const uint32_t first = blockIdx.x * groups_per_block + threadIdx.x / kTxGroup;
     const uint32_t rounds = (nw + gridDim.x * groups_per_block - 1u) / (gridDim.x * groups_per_block);
@@ -531,15 +545,22 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
         const uint32_t seg_len = hl + pl;
         uint8_t* dst = out + slot;
         const bool work = live && counter < kRejectAfterMessages;  // an exhausted one keeps only its header
+        // the seal's checksum: the field inside one 16-B block and inside the prefix the seal reads
+        // from the slot, the payload words paired like the checksum start's, e < 1024
+        const uint32_t fld = gsok ? (plan.kind == kTxTcp ? cs + 16u : cs + 6u) : cs + co;
+        const uint32_t hdr_b = gsok ? hl : plan.kind == kTxFinish ? cs + co + 2u : 0u;
+        const bool seal_cs = work && s < cs_p0 && plan.kind != kTxPass && (fld & 15u) != 15u &&
+                             ((hdr_b - cs) & 1u) == 0u && fld + 2u <= hdr_b && seg_len < 16384u;
 
         if (live && g == 0) {
             wires[s] = neb_tx_wire{slot, counter, seg_len + 32u, p, j, 0u};
             if constexpr (kTxSealFromInput) {
                 // plaintext byte x of the segment image: x < hdr from the slot (the patched header, or
                 // a plain packet up to its finished checksum), else the TUN read's byte in_off + a + x
-                const uint32_t hdr = gsok ? hl : plan.kind == kTxFinish ? cs + co + 2u : 0u;
+                const uint32_t kind = (plan.kind == kTxUdp || (plan.kind == kTxFinish && co == 6u)) ? 2u : 1u;
+                const uint32_t fl = seal_cs ? hdr_b | fld << 12 | kind << 24 | (cs & 1u) << 26 : hdr_b;
                 const uint64_t src = (uint64_t)((uintptr_t)(in + P.in_off + a) - (uintptr_t)out);
-                ws.seal_desc[s] = neb_desc{src, slot + 16u, slot, counter, seg_len, 16u, T.key_id, hdr};
+                ws.seal_desc[s] = neb_desc{src, slot + 16u, slot, counter, seg_len, 16u, T.key_id, fl};
             } else {
                 ws.seal_desc[s] = neb_desc{slot + 16u, slot + 16u, slot, counter, seg_len, 16u, T.key_id, 0u};
             }
@@ -609,15 +630,16 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
         }
 
         // ---- payload units: image positions hl + 16u; the L4 checksum covers [sum_lo, seg_len) ----
-        const bool need_sum = work && plan.kind != kTxPass;
+        // (seal_cs: a plain packet's prefix up to its checksum only; a segment's payload not at all)
+        const bool need_sum = work && plan.kind != kTxPass && (!seal_cs || plan.kind == kTxFinish);
         const uint32_t sum_lo = plan.kind == kTxFinish ? cs : hl;
         const uint32_t zlo = plan.kind == kTxFinish ? cs + co : 0u, zhi = plan.kind == kTxFinish ? cs + co + 2u : 0u;
         const uint8_t* psrc = src + hl + a;
-        const uint32_t nunits = work ? (pl + 15u) >> 4 : 0u;
+        const uint32_t nunits = !work ? 0u : seal_cs ? min((pl + 15u) >> 4, (hdr_b + 15u) >> 4) : (pl + 15u) >> 4;
         const bool in_regs = !kTxSealFromInput && nunits <= kTxGroup * kTxRegUnits;
         const bool flip = ((hl ^ sum_lo) & 1u) != 0u;  // units start at the parity of hl
         uint4 keep[kTxRegUnits];
-        if (kTxSealFromInput) {
+        if (kTxSealFromInput && !CSM) {
             // the checksum only: kTxRegUnits loads in flight per lane, then their sums
             if (need_sum) {
                 for (uint32_t u0 = 0; u0 < nunits; u0 += kTxGroup * kTxRegUnits) {
@@ -635,6 +657,7 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
                             if (plan.kind == kTxFinish) {
                                 v = zero_range(v, hl + 16u * u, 0u, sum_lo);
                                 v = zero_range(v, hl + 16u * u, zlo, zhi);
+                                if (seal_cs) v = zero_range(v, hl + 16u * u, hdr_b, 0xFFFFFFFFu);
                             }
                             const uint32_t su = unit_le_sum(v);
                             le += flip ? bswap16(fold16(su)) : su;
@@ -670,6 +693,7 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
                 if (plan.kind == kTxFinish) {
                     v = zero_range(v, hl + 16u * u, 0u, sum_lo);
                     v = zero_range(v, hl + 16u * u, zlo, zhi);
+                    if (seal_cs) v = zero_range(v, hl + 16u * u, hdr_b, 0xFFFFFFFFu);
                 }
                 const uint32_t su = unit_le_sum(v);
                 le += flip ? bswap16(fold16(su)) : su;
@@ -678,17 +702,19 @@ __global__ __launch_bounds__(kTxWaves * 64, NEB_TX_MINBLOCKS) void tx_segment_ke
         // the group total, folded and byte-swapped, is the big-endian RFC 1071 sum
         const uint32_t rel = bswap16(fold16(group_sum(le)));
         uint32_t csum = 0;
+        // (seal_cs: the partial sum, not complemented, for the seal to finish)
         if (plan.kind == kTxTcp) {
             uint64_t w = tcp_wide + rel;
             w = (w & 0xFFFFFFFFull) + (w >> 32);
             w = (w & 0xFFFFFFFFull) + (w >> 32);
-            csum = fold_complement((uint32_t)w);
+            csum = seal_cs ? fold16(w) : fold_complement((uint32_t)w);
         } else if (plan.kind == kTxUdp) {
-            csum = ~fold16((uint64_t)udp_seed + rel) & 0xFFFFu;
-            if (csum == 0u) csum = 0xFFFFu;  // RFC 768: a computed zero goes out as all ones
+            csum = seal_cs ? fold16((uint64_t)udp_seed + rel) : ~fold16((uint64_t)udp_seed + rel) & 0xFFFFu;
+            if (!seal_cs && csum == 0u) csum = 0xFFFFu;  // RFC 768: a computed zero goes out as all ones
         } else if (plan.kind == kTxFinish && work) {  // seeded with the partial sum left in the field
-            csum = ~fold16((uint64_t)rd16be(src + cs + co) + rel) & 0xFFFFu;
-            if (co == 6u && csum == 0u) csum = 0xFFFFu;
+            const uint64_t t = (uint64_t)rd16be(src + cs + co) + rel;
+            csum = seal_cs ? fold16(t) : ~fold16(t) & 0xFFFFu;
+            if (!seal_cs && co == 6u && csum == 0u) csum = 0xFFFFu;
         }
 
         // ---- store the image ----
@@ -814,15 +840,22 @@ extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const u
 extern "C" hipError_t neb_tx_segment(const neb_tx_packet* d_pk, uint32_t n, const uint8_t* d_in,
                                      const neb_tx_tunnel* d_tun, uint8_t* d_out, const neb::TxWs* ws,
                                      neb_tx_wire* d_wires, const uint32_t* d_nwires, uint32_t max_wires, int cu_count,
-                                     hipStream_t s) {
+                                     uint32_t cs_slots, hipStream_t s) {
     (void)n;
     const uint32_t per_block = neb::kTxWaves * 64u / neb::kTxGroup;
     const uint32_t want = (max_wires + per_block - 1) / per_block;
-    const uint32_t cap = (uint32_t)cu_count * 8u;
+#ifndef NEB_TX_SEG_CAP
+#define NEB_TX_SEG_CAP 8
+#endif
+    const uint32_t cap = (uint32_t)cu_count * NEB_TX_SEG_CAP;
     const uint32_t grid = want < cap ? want : cap;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(neb::tx_segment_kernel, dim3(grid), dim3(neb::kTxWaves * 64), 0, s, d_pk, d_in, d_tun, d_out,
-                       *ws, d_wires, d_nwires);
+    if (cs_slots)
+        hipLaunchKernelGGL(neb::tx_segment_kernel<true>, dim3(grid), dim3(neb::kTxWaves * 64), 0, s, d_pk, d_in, d_tun,
+                           d_out, *ws, d_wires, d_nwires, cs_slots);
+    else
+        hipLaunchKernelGGL(neb::tx_segment_kernel<false>, dim3(grid), dim3(neb::kTxWaves * 64), 0, s, d_pk, d_in, d_tun,
+                           d_out, *ws, d_wires, d_nwires, cs_slots);
     return hipGetLastError();
 }
 

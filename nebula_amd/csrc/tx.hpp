@@ -100,6 +100,6 @@ extern "C" hipError_t neb_tx_plan(const neb_tx_packet* d_pk, uint32_t n, const u
 extern "C" hipError_t neb_tx_segment(const neb_tx_packet* d_pk, uint32_t n, const uint8_t* d_in,
                                      const neb_tx_tunnel* d_tun, uint8_t* d_out, const neb::TxWs* ws,
                                      neb_tx_wire* d_wires, const uint32_t* d_nwires, uint32_t max_wires, int cu_count,
-                                     hipStream_t s);
+                                     uint32_t cs_slots, hipStream_t s);
 extern "C" hipError_t neb_tx_finish(neb_tx_tunnel* d_tun, uint32_t n, uint32_t ntun, const neb::TxWs* ws,
                                     hipStream_t s);

@@ -244,3 +244,41 @@ def test_tx_batch_byte_skewed_reads(engine, oracle_mod, alg, single):
     tun = _tunnels(rng, n=1 if single else 3, keyless=())
     _check(engine, oracle_mod, alg, P, tun, out_cap=4 << 20, max_wires=4096, key_hint=0 if single else None,
            skew=list(range(16)))
+
+
+@pytest.mark.parametrize("grid", [None, 1])
+def test_tx_single_key_checksums_in_seal(engine, oracle_mod, grid, monkeypatch):
+    """One AES-GCM tunnel key: the seal sums the payloads into the L4 checksums itself (aes_gcm.hip
+    gcm_csum_fix) — TSO v4/v6, USO v4/v6, FinishChecksum on TCP and UDP, an odd checksum start, and a
+    field straddling two blocks (summed by the segment kernel instead). With `grid`, a 1-workgroup
+    seal grid (NEB_SINGLE_MAX_GRID) leaves a partial last pass to the tail kernel, whose segments
+    the segment kernel sums."""
+    import segment_oracle as S
+    from test_segment_oracle import build_udpv4_single
+
+    if grid is not None:
+        monkeypatch.setenv("NEB_SINGLE_MAX_GRID", str(grid))
+    rng = random.Random(77)
+    P = []
+    for i in range(24):
+        d, _, cs = build_tcpv4_super(rng.choice([3000, 20000, 14477]))
+        P.append(_pk(d, 0, 1, S.GSO_TCPV4, rng.choice([1448, 1200, 536]), cs, 16))
+        if i % 4 == 0:
+            d, _, cs = build_tcpv6_super(rng.choice([900, 9000]), tcp_opts=rng.choice([0, 12]))
+            P.append(_pk(d, 0, 1, S.GSO_TCPV6, 1000, cs, 16))
+            d, _, cs = build_udpv4_super(rng.choice([100, 5000]))
+            P.append(_pk(d, 0, 1, S.GSO_UDP_L4, 1200, cs, 6))
+            d, _, cs = build_udpv6_super(3000)
+            P.append(_pk(d, 0, 1, S.GSO_UDP_L4, 333, cs, 6))
+            P.append(_pk(build_udpv4_single(S, bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 300)))), 0,
+                         S.F_NEEDS_CSUM, 0, 0, 20, 6))                                    # FinishChecksum, UDP
+            d, _, cs = build_tcpv4_super(rng.randrange(1, 700))
+            P.append(_pk(d, 0, S.F_NEEDS_CSUM, 0, 0, 20, 16))                             # FinishChecksum, TCP
+            P.append(_pk(bytes(rng.getrandbits(8) for _ in range(200)), 0, S.F_NEEDS_CSUM, 0, 0, 21, 6))  # odd start
+            P.append(_pk(bytes(rng.getrandbits(8) for _ in range(90)), 0, S.F_NEEDS_CSUM, 0, 0, 9, 6))    # straddles
+            P.append(_pk(bytes(rng.getrandbits(8) for _ in range(777)), 0))                                # plain
+    tun = _tunnels(rng, n=1, keyless=())
+    r = _check(engine, oracle_mod, L.ALG_AESGCM, P, tun, out_cap=4 << 20, max_wires=4096, key_hint=0,
+               skew=[0, 4, 8, 3])
+    if grid is not None:
+        assert len(r.wires) > 16 * 16 * grid  # past one full pass of the capped grid
