@@ -159,7 +159,10 @@ def main():
 
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
+    # one process per GPU; more ranks than devices (a rehearsal on a smaller box) share them round-robin
+    ndev = torch.cuda.device_count()
+    device = local % ndev if ndev else local
+    torch.cuda.set_device(device)
     # control plane only (barrier / max of timings) over gloo; no data-path collective
     ctrl = Control(world)
     barrier = ctrl.barrier
@@ -179,7 +182,7 @@ def main():
     log(f"[rank {rank}] batch {b.name}: {b.n} pkts, {b.payload_bytes / 1e6:.1f} MB payload "
         f"({time.time() - t0:.1f}s to build)")
 
-    eng = Engine(local, max_keys=max(4096, b.nkeys))
+    eng = Engine(device, max_keys=max(4096, b.nkeys))
     ciphers = install_keys(eng, b)
     payload = float(b.payload_bytes)
     alg_bytes = float(b.algorithmic_bytes)
