@@ -56,8 +56,10 @@ struct RxSort {
 __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict__ desc, RxDevWin win, RxDevWs ws,
                                                       RxSort so) {
     __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_mixed;
     const uint32_t t = threadIdx.x, b = blockIdx.x;
     hist[t] = 0;
+    if (t == 0) s_mixed = 0;
     for (uint32_t x = t; x < so.per_blk; x += 256) {
         const size_t wi = (size_t)b * so.per_blk + x;
         if (wi < win.count) ws.wflag[wi] = 0;
@@ -67,6 +69,13 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
     for (uint32_t p = 1; p < so.passes; p++) ws.sort_hist[((size_t)p * kRxSortBlocks + b) * 256 + t] = 0;
     __syncthreads();
     const uint32_t mask = (1u << so.bits[0]) - 1u;
+    // the first packet's window: a batch whose packets all name it needs no sort
+    uint32_t w0 = win.count;
+    {
+        const uint32_t k0 = desc[0].key_id;
+        if (k0 < win.count && win.present[k0]) w0 = k0;
+    }
+    bool differs = false;
     constexpr uint32_t R = kRxSortLoad;
     for (uint32_t j0 = 0; j0 < so.items; j0 += R) {
         uint32_t kid[R], pres[R];
@@ -90,25 +99,42 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
             const uint32_t w = pres[r] ? kid[r] : win.count;
             ws.keyw[e] = w;
             ws.ctr[e] = ctr[r];
+            differs |= w != w0;
             atomicAdd(&hist[(w >> so.shift[0]) & mask], 1u);
         }
     }
+    if (differs) s_mixed = 1u;
     __syncthreads();
     ws.sort_hist[(size_t)b * 256 + t] = hist[t];
+    if (t == 0 && s_mixed) *ws.mixed = ws.gen;  // read by the sort passes (the next launches)
 }
 
 // One pass: every packet of the workgroup to base[digit] + (its digit's count in earlier
 // workgroups) + (its rank among the workgroup's packets of that digit, in arrival order: a round
 // of 256 at a time, ranks within a wave from ballots, waves in order through LDS). Unless this is
 // the last pass, the next digit is counted per output workgroup in LDS and added to its counts.
+// A batch whose packets all name one window (the keys kernel did not mark this generation mixed:
+// one tunnel's flush) is already in run order: pass 0 writes the identity into the run arrays and
+// the later passes do nothing.
 template <bool FIRST>
 __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p, uint32_t* hist_all,
                                                            const uint32_t* __restrict__ src_k,
                                                            const uint32_t* __restrict__ src_v, uint32_t* dst_k,
-                                                           uint32_t* dst_v) {
+                                                           uint32_t* dst_v, const uint32_t* mixed, uint32_t gen,
+                                                           uint32_t* run_w, uint32_t* run_i) {
     __shared__ uint32_t gbase[256], run[256], wcnt[4][256], wtot[4];
     __shared__ uint32_t agg[kRxSortBlocks << kRxSortDigit];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
+    if (__builtin_amdgcn_readfirstlane(*mixed) != gen) {
+        if (FIRST) {
+            const uint32_t e1 = min(so.n, (b + 1u) * so.per_blk);
+            for (uint32_t e = b * so.per_blk + t; e < e1; e += 256u) {
+                run_w[e] = src_k[e];
+                run_i[e] = e;
+            }
+        }
+        return;
+    }
     const uint32_t* hist = hist_all + (size_t)p * kRxSortBlocks * 256;
     const bool next = p + 1 < so.passes;
     const uint32_t nb2 = next ? 1u << so.bits[p + 1] : 0u;
@@ -580,10 +606,10 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
         const uint32_t* sv = p == 0 ? nullptr : (to_run ? ws->tmp_v : ws->run_i);
         if (p == 0)
             hipLaunchKernelGGL(neb::rx_sort_pass_kernel<true>, dim3(so.nblk), dim3(256), 0, s, so, p, ws->sort_hist,
-                               sk, sv, dk, dv);
+                               sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i);
         else
             hipLaunchKernelGGL(neb::rx_sort_pass_kernel<false>, dim3(so.nblk), dim3(256), 0, s, so, p, ws->sort_hist,
-                               sk, sv, dk, dv);
+                               sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i);
     }
     const dim3 blocks((n + neb::kRxBlock - 1) / neb::kRxBlock);
     hipLaunchKernelGGL(neb::rx_scan_kernel, blocks, dim3(neb::kRxThreads), 0, s, n, *win, *ws);

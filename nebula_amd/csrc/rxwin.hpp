@@ -73,6 +73,9 @@ struct RxDevWs {
     uint64_t* recv;
     uint64_t* scratch;  // count x words
     uint32_t* need_host;  // pinned host word: set to 1 when a touched window is risky or slow
+    // the generation of the last batch whose packets named more than one window (written by the
+    // keys kernel); any other value lets the sort passes write the identity order (one window)
+    uint32_t* mixed;
 };
 
 inline size_t rx_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -115,6 +118,7 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
     w.exit_hi = (uint64_t*)take((size_t)count * 8);
     w.recv = (uint64_t*)take((size_t)count * 8);
     w.scratch = (uint64_t*)take((size_t)count * words * 8);
+    w.mixed = (uint32_t*)take(4);
     if (ws) *ws = w;
     return off;
 }

@@ -731,6 +731,7 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
         neb::rx_ws_layout(n, v.count, v.words, d->ws_mem, &d->ws);
         // the scratch bitmap is zeroed once here and again by each batch as it is consumed
         RX_HIP(hipMemsetAsync(d->ws.scratch, 0, ((size_t)v.count << v.words_lg) * 8, s));
+        RX_HIP(hipMemsetAsync(d->ws.mixed, 0, 4, s));  // no generation is 0
         d->ws.gen = UINT32_MAX;  // the first batch clears the first-occurrence table
         d->ws_bytes = bytes;
         d->ws_n = n;

@@ -350,3 +350,83 @@ def test_device_windows_api_errors(engine):
             other.close()
     finally:
         dw.destroy()
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_rx_device_batches_one_and_many_windows(engine, oracle_mod, strict):
+    """Consecutive batches on one device window set, alternating between batches whose packets all
+    name one window (run order = arrival order: the sort writes the identity) and batches that name
+    several — including one whose only other window is its last packet's, one whose first packet
+    names an absent window, and one that names only an absent window. Per-packet receive is
+    sequential, so the batches together must equal the oracle's loop over their concatenation."""
+    import replay_oracle as R
+    import torch
+
+    from nebula_amd.connection_state import Bits, DeviceWindows, rx_open_batch_device
+    from nebula_amd.noiseutil import CipherAESGCM
+
+    rng = random.Random(404)
+    ntun, wl = 3, 1024
+    keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(ntun)]
+    installed = {0, 1}  # tunnel 2: no key and no window
+    nxt = {0: 3, 1: 3, 2: 3}
+
+    def batch(tuns, n):
+        out = []
+        for _ in range(n):
+            t = rng.choice(tuns)
+            c = nxt[t] + rng.choice([0, 0, 1, 2]) - (1 if rng.random() < 0.1 else 0)
+            nxt[t] = max(nxt[t], c + 1)
+            out.append((t, c, not strict and rng.random() < 0.03))
+        return out
+
+    batches = [batch([0, 1], 300), batch([0], 500), batch([0], 200) + [(1, nxt[1], False)], batch([1], 400)]
+    if not strict:  # packets of an absent window (the strict mode's parallel form refuses a batch with them)
+        batches += [[(2, 3, False)] + batch([0], 100), batch([2], 50), batch([0, 1, 2], 300)]
+    batches += [batch([1], 250), batch([0, 1], 100)]
+    arrivals = [a for b in batches for a in b]
+    ciphers = {t: CipherAESGCM.Cipher(engine, keys[t]) for t in installed}
+    slot_of = {t: (ciphers[t].key_id if t in ciphers else engine.max_keys - 1 - t) for t in range(ntun)}
+    dw = None
+    try:
+        arena, desc, pts = _build(oracle_mod, L.ALG_AESGCM, keys, arrivals, 9, [0, 16, 40, 1300])
+        seeds = {0: 2, 1: 2}
+        exp_status, exp_arena, owins = _expected(oracle_mod, R, L.ALG_AESGCM, keys, arrivals, arena, pts, wl, seeds,
+                                                 installed)
+        d = desc.copy()
+        d["key_id"] = [slot_of[int(t)] for t in desc["key_id"]]
+        dev = torch.device("cuda", engine.device)
+        dw = DeviceWindows(engine, engine.max_keys, wl)
+        ewins = {}
+        for t, mi in seeds.items():
+            w = Bits(wl)
+            for i in range(1, mi + 1):
+                w.Update(i)
+            ewins[t] = w
+            dw.load(slot_of[t], w)
+        d_arena = torch.from_numpy(arena).to(dev)
+        got = []
+        a = 0
+        for b in batches:
+            dd = torch.from_numpy(d[a:a + len(b)].view(np.uint8).copy()).to(dev)
+            st = torch.full((len(b),), -1, dtype=torch.int32, device=dev)
+            if strict:
+                os.environ["NEB_RXDEV_STRICT"] = "1"
+            try:
+                rx_open_batch_device(engine, L.ALG_AESGCM, dw, dd, d_arena, st)
+            finally:
+                os.environ.pop("NEB_RXDEV_STRICT", None)
+            got += st.cpu().tolist()
+            a += len(b)
+        assert got == exp_status
+        assert np.array_equal(d_arena.cpu().numpy(), exp_arena)
+        for t, w in ewins.items():
+            dw.store(slot_of[t], w)
+            o = owins[t]
+            assert (w.current, w.lost, w.dupe, w.out_of_window) == (o.current, o.lost, o.dupe, o.out_of_window)
+            assert [bool(x) for x in w.snapshot()] == o.snapshot()
+    finally:
+        if dw is not None:
+            dw.destroy()
+        for c in ciphers.values():
+            c.destroy()
