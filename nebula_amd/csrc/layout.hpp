@@ -4,9 +4,9 @@
 
 namespace neb {
 
-// One key record per installed tunnel key (21.75 KiB): the first 512 B hold the key schedule and
+// One key record per installed tunnel key (25.75 KiB): the first 512 B hold the key schedule and
 // raw H powers; the rest holds GHASH lookup tables precomputed at install time (AES-GCM only).
-constexpr uint32_t kKeyRecDwords = 5568;
+constexpr uint32_t kKeyRecDwords = 6592;
 constexpr uint32_t kKeyRecBytes = kKeyRecDwords * 4;
 
 // AES-256-GCM record
@@ -35,7 +35,11 @@ constexpr uint32_t kRecPos64 = kRecShoup32 + 16 * 4;
 // Shoup tables of H^64, H^128, H^256, H^512: with M_1, M_2, M_4, M_8, M_16 and M_32 above, the
 // binary powers that take a block to any H^e, e < 1024 (the TX seal's checksum correction)
 constexpr uint32_t kRecShoupHi = kRecPos64 + 8 * 16 * 4;
-static_assert(kRecShoupHi + 4 * 16 * 4 == kKeyRecDwords, "record layout");
+// position tables of H^2 and H^3: with those of H and H^4 above, the single-key kernel's final
+// multiplies each lane's accumulator by its own power (one multiply per lane, not four per quad)
+constexpr uint32_t kRecPos2 = kRecShoupHi + 4 * 16 * 4;
+constexpr uint32_t kRecPos3 = kRecPos2 + 8 * 16 * 4;
+static_assert(kRecPos3 + 8 * 16 * 4 == kKeyRecDwords, "record layout");
 // record offset of the Shoup table of H^(2^j), j = 0..9
 __host__ __device__ constexpr uint32_t rec_shoup_pow2(uint32_t j) {
     return j < 5u ? kRecShoup + 64u * ((1u << j) - 1u) : (j == 5u ? kRecShoup32 : kRecShoupHi + 64u * (j - 6u));

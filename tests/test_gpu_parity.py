@@ -334,10 +334,11 @@ def test_full_c2_roundtrip_property(engine):
     assert np.array_equal(s2[idx], r2[idx])
 
 
-@pytest.mark.parametrize("extra", [1, 37, 4 * 16 * 64 + 5])
+@pytest.mark.parametrize("extra", [1, 37, 4 * 16 * 64 + 5, 30001])
 def test_single_key_partial_last_pass(engine, oracle_mod, extra):
     """One key, a batch just past one pass of the single-key kernel's waves (64 Ki packets on one
-    MI355X): the packets of the partial last pass go to the tail kernel, 16 lanes per packet. Every
+    MI355X): the packets of the partial last pass go to the tail kernel (64 lanes per packet, a grid
+    of at most two workgroups per CU striding over them: 30001 takes 8 strides). Every
     packet, ragged sizes, sealed and opened, bit-exact against the oracle."""
     import torch
     from nebula_amd.batch import DeviceBatch, install_keys
