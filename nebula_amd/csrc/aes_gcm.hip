@@ -876,6 +876,41 @@ struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position table
     }
 };
 
+// Mixed-key chunks (gcm_chunk_kernel): the wave's slice holds the Shoup tables M_1, M_2, M_3, M_4
+// (record tables 0-3) and M_8 (NEB_CHUNK_FINAL_PERM), and the position tables of H^(2^lg). A 4-lane
+// chunk (16 packets, the layout of the single-key kernel) takes the permuted final of GhFullPerm on
+// the Shoup tables: b128 lane group g multiplies role g of every packet by M_(4-g), one multiply per
+// lane instead of the tree's three; 8- and 16-lane tails keep the tree (M_1, M_2, M_4, M_8).
+#ifndef NEB_CHUNK_FINAL_PERM
+#define NEB_CHUNK_FINAL_PERM 1
+#endif
+struct GhChunk {
+    static constexpr bool kBitslice = false;
+    const uint4* base;
+    const uint4* pos;
+    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
+    __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
+        if (lg == 2u) {  // wave-uniform
+            const uint32_t tab_off[4] = {3u * 256u, 2u * 256u, 256u, 0u};  // M_4, M_3, M_2, M_1
+            const FinalPermLanes fp = final_perm_lanes(lane, tab_off);
+            const uint4 a = shfl4(A, fp.src1);
+            uint4 v = shfl4(gf_mul_shoup(a, fp.off, base), fp.src2);
+            v = xor4(v, dpp4<0xB1>(v));
+            return xor4(v, dpp4<0x4E>(v));
+        }
+        uint4 V = A;
+        for (uint32_t i = 0; i < lg; i++) {
+            const uint32_t off = i == 3u ? 4u * 256u : ((1u << i) - 1u) * 256u;  // M_(2^i)
+            V = xor4(gf_mul_shoup(V, off, base), shfl_down4(V, 1u << i));
+        }
+        V = gf_mul_shoup(V, 0u, base);
+        return shfl4(V, lane & ~((1u << lg) - 1u));
+    }
+};
+#if NEB_CHUNK_FINAL_PERM
+static_assert(NEB_CHUNK_POS && !NEB_WIDE_CHUNKS, "GhChunk: position-table Horner, chunks of 4-16 lanes per packet");
+#endif
+
 // ---- the TX checksum in the seal (CS; tx.hip kTxCsumFlag) ----------------------------------
 // The TX segment kernel leaves in the L4 checksum field the partial sum of everything but the
 // payload bytes the seal reads from the TUN read ([hdr, len)); the seal adds those bytes' 16-bit
@@ -1440,7 +1475,11 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
     uint4* wtab = &lds.shoup[wave][0][0];
 #if NEB_CHUNK_POS
     uint4* wpos = &lds.pos[wave][0];
+#if NEB_CHUNK_FINAL_PERM
+    const GhChunk gh{wtab, wpos};
+#else
     const GhShoup gh{wtab, wpos};
+#endif
 #else
     const GhShoup gh{wtab, nullptr};
 #endif
@@ -1490,8 +1529,14 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
         uint32_t rks[60];
         load_round_keys(rec, rks);
         // stage the chunk key's Shoup tables H^(2^i), i = 0..4 (record tables 0, 1, 3, 7, 15)
+#if NEB_CHUNK_FINAL_PERM
+        // M_1..M_4 (record tables 0-3, contiguous) and M_8
+        wtab[lane] = ld_rec4(rec, kRecShoup + 4u * lane);
+        if (lane < 16u) wtab[64u + lane] = ld_rec4(rec, kRecShoup + 64u * 7u + 4u * lane);
+#else
         wtab[lane] = ld_rec4(rec, kRecShoup + 64u * ((1u << (lane >> 4)) - 1u) + 4u * (lane & 15u));
         if (lane < 16u) wtab[64u + lane] = ld_rec4(rec, kRecShoup + 64u * 15u + 4u * lane);
+#endif
 #if NEB_CHUNK_POS
         {  // the position tables of H^(2^lg)
             const uint32_t pt = rec_pos_table(lg);
