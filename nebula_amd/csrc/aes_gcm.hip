@@ -884,6 +884,16 @@ struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position table
 #ifndef NEB_CHUNK_FINAL_PERM
 #define NEB_CHUNK_FINAL_PERM 1
 #endif
+// (not inlined, its call saves every live register: 208-256 B of scratch per lane instead of 52-64)
+__device__ __forceinline__ uint4 chunk_tree_final(uint4 A, uint32_t lane, uint32_t lg, const uint4* base) {
+    uint4 V = A;
+    for (uint32_t i = 0; i < lg; i++) {
+        const uint32_t off = i == 3u ? 4u * 256u : ((1u << i) - 1u) * 256u;  // M_(2^i)
+        V = xor4(gf_mul_shoup(V, off, base), shfl_down4(V, 1u << i));
+    }
+    V = gf_mul_shoup(V, 0u, base);
+    return shfl4(V, lane & ~((1u << lg) - 1u));
+}
 struct GhChunk {
     static constexpr bool kBitslice = false;
     const uint4* base;
@@ -898,13 +908,7 @@ struct GhChunk {
             v = xor4(v, dpp4<0xB1>(v));
             return xor4(v, dpp4<0x4E>(v));
         }
-        uint4 V = A;
-        for (uint32_t i = 0; i < lg; i++) {
-            const uint32_t off = i == 3u ? 4u * 256u : ((1u << i) - 1u) * 256u;  // M_(2^i)
-            V = xor4(gf_mul_shoup(V, off, base), shfl_down4(V, 1u << i));
-        }
-        V = gf_mul_shoup(V, 0u, base);
-        return shfl4(V, lane & ~((1u << lg) - 1u));
+        return chunk_tree_final(A, lane, lg, base);
     }
 };
 #if NEB_CHUNK_FINAL_PERM
