@@ -178,6 +178,19 @@ __device__ __forceinline__ uint2 ttab4_entry(uint32_t i) {  // i = region*8192 +
     const uint32_t t1 = rotl8(t);                            // T1 = rotl8 T0, T3 = rotl8 T2
     return (i & 16u) ? make_uint2(t1, t) : make_uint2(t, t1);
 }
+// Write N entries of an LDS T-table image with THREADS threads: every source word is loaded
+// before any is stored, so the prologue pays one global-load latency instead of one per entry (a
+// strided loop left a load + vmcnt(0) + store per iteration: 16 serialised L2 round trips).
+template <uint32_t N, uint32_t THREADS, class F>
+__device__ __forceinline__ void fill_ttab(uint2* dst, uint32_t tid, F entry) {
+    static_assert(N % THREADS == 0, "whole rounds");
+    constexpr uint32_t K = N / THREADS;
+    uint2 v[K];
+#pragma unroll
+    for (uint32_t j = 0; j < K; j++) v[j] = entry(tid + j * THREADS);
+#pragma unroll
+    for (uint32_t j = 0; j < K; j++) dst[tid + j * THREADS] = v[j];
+}
 struct TLook4 {
     const uint2* ttab;
     uint32_t lb;
@@ -1241,6 +1254,21 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
+#if !NEB_GHASH8
+    // the record's GHASH tables: loaded before the T-table fill and stored after it, so their
+    // latency overlaps the fill's instead of following it
+    static_assert(kSingleThreads >= 512, "one full-table entry per thread");
+    uint4 r_full = make_uint4(0, 0, 0, 0), r_h = make_uint4(0, 0, 0, 0), r_p = make_uint4(0, 0, 0, 0);
+    if (tid < 512u) r_full = ld_rec4(srec, kRecFull + 4u * tid);
+#if NEB_SINGLE_POSH
+    if (tid < 128u) r_h = ld_rec4(srec, kRecPos1 + 4u * tid);
+#else
+    if (tid < 16u) r_h = ld_rec4(srec, kRecShoup + 4u * tid);
+#endif
+#if NEB_SINGLE_FINAL_PERM
+    if (tid < 256u) r_p = ld_rec4(srec, (tid < 128u ? kRecPos2 : kRecPos3) + 4u * (tid & 127u));
+#endif
+#endif
 #if NEB_GHASH8
 #if NEB_G8_LAYOUT
     const TLook T{lds.ttab, ttab_lane_base(lane)};
@@ -1248,7 +1276,7 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     static_assert(offsetof(SingleLds, ttab) == 65536u + 2048u, "T-table base: bit 16 + offset field");
     const TLook T{reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(&lds) + 2048), ttab_lane_base(lane, 1u << 16)};
 #endif
-    for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
+    fill_ttab<256u * 32u, kSingleThreads>(lds.ttab, tid, ttab_entry);
     // F8_P[b] = F4_2P[b >> 4] ^ F4_2P+1[b & 15] from the record's nibble table (layout.hpp)
 #if NEB_G8_LAYOUT
     for (uint32_t i = tid; i < 256u * 16u; i += kSingleThreads) {
@@ -1266,21 +1294,27 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
 #endif
 #elif NEB_T4
     const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
-    for (uint32_t i = tid; i < 2u * 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab4_entry(i);
+    fill_ttab<2u * 256u * 32u, kSingleThreads>(lds.ttab, tid, ttab4_entry);
 #else
     const TLook T{lds.ttab, ttab_lane_base(lane)};
-    for (uint32_t i = tid; i < 256u * 32u; i += kSingleThreads) lds.ttab[i] = ttab_entry(i);
+    fill_ttab<256u * 32u, kSingleThreads>(lds.ttab, tid, ttab_entry);
 #endif
 #if !NEB_GHASH8
-    for (uint32_t i = tid; i < 32u * 16u; i += kSingleThreads) lds.full[i] = ld_rec4(srec, kRecFull + 4u * i);
+    if (tid < 512u) lds.full[tid] = r_full;
+#if NEB_SINGLE_POSH
+    if (tid < 128u) lds.shoup_h[tid] = r_h;
+#else
+    if (tid < 16u) lds.shoup_h[tid] = r_h;
 #endif
+#if NEB_SINGLE_FINAL_PERM
+    if (tid < 256u) lds.pos23[tid >> 7][tid & 127u] = r_p;
+#endif
+#else
 #if NEB_SINGLE_POSH
     if (tid < 128u) lds.shoup_h[tid] = ld_rec4(srec, kRecPos1 + 4u * tid);
 #else
     if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
 #endif
-#if NEB_SINGLE_FINAL_PERM
-    if (tid < 256u) lds.pos23[tid >> 7][tid & 127u] = ld_rec4(srec, (tid < 128u ? kRecPos2 : kRecPos3) + 4u * (tid & 127u));
 #endif
 
     const uint4* cs_pow = nullptr;
@@ -1373,7 +1407,7 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     if (blockIdx.x * kTailWaves >= tgroups) return;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
 #ifndef NEB_ABLATE_TAIL_STAGE  // (ablation: wrong results, timing only)
-    for (uint32_t i = tid; i < 256u * 32u; i += kTailWaves * kWave) lds.ttab[i] = ttab_entry(i);
+    fill_ttab<256u * 32u, kTailWaves * kWave>(lds.ttab, tid, ttab_entry);
 #endif
     if (tid < 16u * kTailLg) {  // M[v] of H^(2^j), j < kTailLg
         const uint32_t j = tid >> 4, v = tid & 15u;
@@ -1471,9 +1505,9 @@ __global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs arg
     if (blockIdx.x * (uint32_t)kChunkWaves >= nch) return;  // uniform over the workgroup
 #endif
 #if NEB_CHUNK_T4
-    for (uint32_t i = tid; i < 2u * 256u * 32u; i += kChunkThreads) lds.ttab[i] = ttab4_entry(i);
+    fill_ttab<2u * 256u * 32u, kChunkThreads>(lds.ttab, tid, ttab4_entry);
 #else
-    for (uint32_t i = tid; i < 256u * 32u; i += kChunkThreads) lds.ttab[i] = ttab_entry(i);
+    fill_ttab<256u * 32u, kChunkThreads>(lds.ttab, tid, ttab_entry);
 #endif
     __syncthreads();
     uint4* wtab = &lds.shoup[wave][0][0];
