@@ -283,7 +283,7 @@ def main():
     value = total_payload / dt / GIB
     achieved = alg_bytes / (seal_ms * 1e-3) / 1e9  # GB/s, seal kernel
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
-    kern_tag = ("gcm_single_kernel<false>" if b.nkeys == 1 else "gcm_chunk_kernel<false>") if b.alg == 1 \
+    kern_tag = ("gcm_single_kernel<false, false>" if b.nkeys == 1 else "gcm_chunk_kernel<false>") if b.alg == 1 \
         else "chacha_batch_kernel<false>"
     out = {
         "metric": "GiB/s device-resident AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch"
