@@ -183,13 +183,14 @@ __device__ __forceinline__ uint2 ttab4_entry(uint32_t i) {  // i = region*8192 +
 // strided loop left a load + vmcnt(0) + store per iteration: 16 serialised L2 round trips).
 template <uint32_t N, uint32_t THREADS, class F>
 __device__ __forceinline__ void fill_ttab(uint2* dst, uint32_t tid, F entry) {
-    static_assert(N % THREADS == 0, "whole rounds");
-    constexpr uint32_t K = N / THREADS;
+    constexpr uint32_t K = (N + THREADS - 1) / THREADS;
+    constexpr bool kWhole = N % THREADS == 0;
     uint2 v[K];
 #pragma unroll
-    for (uint32_t j = 0; j < K; j++) v[j] = entry(tid + j * THREADS);
+    for (uint32_t j = 0; j < K; j++) v[j] = entry((tid + j * THREADS) % N);
 #pragma unroll
-    for (uint32_t j = 0; j < K; j++) dst[tid + j * THREADS] = v[j];
+    for (uint32_t j = 0; j < K; j++)
+        if (kWhole || tid + j * THREADS < N) dst[tid + j * THREADS] = v[j];
 }
 struct TLook4 {
     const uint2* ttab;
@@ -1436,11 +1437,17 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
 #ifndef NEB_CHUNK_T4
 #define NEB_CHUNK_T4 0
 #endif
+#ifndef NEB_CHUNK_WAVES
 #if NEB_CHUNK_T4 || NEB_CHUNK_POS
-constexpr int kChunkWaves = 16;  // one workgroup per CU (116 KiB of LDS; 148 KiB with T4)
+#define NEB_CHUNK_WAVES 16  // one workgroup per CU (116 KiB of LDS; 148 KiB with T4)
 #else
-constexpr int kChunkWaves = 8;
+#define NEB_CHUNK_WAVES 8
 #endif
+#endif
+#ifndef NEB_CHUNK_WPE
+#define NEB_CHUNK_WPE 4  // launch bound: waves per SIMD (4: at most 128 VGPRs)
+#endif
+constexpr int kChunkWaves = NEB_CHUNK_WAVES;
 constexpr int kChunkThreads = kChunkWaves * kWave;
 // E_K(J0) in LDS instead of a register removes the open kernel's in-loop spills (HBM traffic 280 ->
 // 238 MB per C3 launch) but made both chunk kernels 9% slower (171 -> 186 µs, rocprof A/B,
@@ -1486,7 +1493,7 @@ struct ChunkArgs {
 // Chunks come from a work cursor, full ones first (chunks[0, F)), then the tails stored from the
 // end of the array: waves that drew cheap chunks draw again, and the cheap chunks run last.
 template <bool OPEN>
-__global__ __launch_bounds__(kChunkThreads, 4) void gcm_chunk_kernel(GcmArgs args, ChunkArgs ca) {
+__global__ __launch_bounds__(kChunkThreads, NEB_CHUNK_WPE) void gcm_chunk_kernel(GcmArgs args, ChunkArgs ca) {
     __shared__ ChunkLds lds;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
