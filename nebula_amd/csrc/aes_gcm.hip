@@ -399,6 +399,24 @@ __device__ __forceinline__ uint4 gf_reduce(const uint32_t z[8]) {
     return make_uint4(x3(z[0], t0, of), t1, t2, t3);
 }
 
+// q·x^i, i < 128: q shifted right by i bits as a 256-bit product, then reduced (any lane, no loop).
+__device__ __forceinline__ uint4 gf_mul_xpow(uint4 q, uint32_t i) {
+    const uint32_t w = i >> 5, b = i & 31u;
+    const uint32_t src[4] = {q.x, q.y, q.z, q.w};
+    uint32_t y[8], z[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) v = (uint32_t)(k - j) == w ? src[j] : v;
+        y[k] = v;
+    }
+    z[0] = y[0] >> b;
+#pragma unroll
+    for (int k = 1; k < 8; k++) z[k] = shr64(y[k - 1], y[k], b);
+    return gf_reduce(z);
+}
+
 // (byte K of w) & 0xF0 in one VALU op (SDWA byte select); hipcc emits a shift + and for most K.
 template <int K>
 __device__ __forceinline__ uint32_t byte_hi_nibble(uint32_t w) {
@@ -1631,8 +1649,14 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
     __shared__ uint4 basis23[2][32]; // x^i · H^2, x^i · H^3
     __shared__ uint4 basis_h[128];  // x^i · H
     __shared__ uint4 part[2];
+    // the S-box in LDS for the key schedule and H = E_K(0) on lane 0: its ~330 dependent lookups
+    // from global memory cost ~25 µs per key
+    __shared__ uint8_t sb[256];
+    __shared__ uint8_t rk[240];  // the key schedule (in LDS: as a lane array it lived in scratch)
+    sb[threadIdx.x] = (uint8_t)(c_T0.t[threadIdx.x] >> 8);
+    __syncthreads();
     if (threadIdx.x == 0) {
-        uint8_t rk[240];
+        auto sbox_b = [&](uint32_t x) { return sb[x & 255u]; };
         for (int i = 0; i < 32; i++) rk[i] = key[i];
         uint8_t rcon = 1;
         for (int i = 8; i < 60; i++) {
@@ -1672,14 +1696,11 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         uint32_t h[4];
         for (int i = 0; i < 4; i++)
             h[i] = (uint32_t)s[4 * i] << 24 | (uint32_t)s[4 * i + 1] << 16 | (uint32_t)s[4 * i + 2] << 8 | s[4 * i + 3];
-        // basis_h[i] = x^i·H: a product P·H is the XOR of basis_h[i] over the set bits i of P
-        uint4 bh = make_uint4(h[0], h[1], h[2], h[3]);
-        for (int i = 0; i < 128; i++) {
-            basis_h[i] = bh;
-            bh = gf_mulx(bh);
-        }
-        hp[0] = basis_h[0];
+        hp[0] = make_uint4(h[0], h[1], h[2], h[3]);
     }
+    __syncthreads();
+    // basis_h[i] = x^i·H: a product P·H is the XOR of basis_h[i] over the set bits i of P
+    if (threadIdx.x < 128u) basis_h[threadIdx.x] = gf_mul_xpow(hp[0], threadIdx.x);
     __syncthreads();
     // H^2..H^16: H^k = H^(k-1)·H with lane i < 128 contributing basis_h[i] if bit i of H^(k-1) is
     // set, XOR-reduced across the two waves (the bit-serial form on one lane took ~100 µs).
@@ -1697,30 +1718,19 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         if (t == 0u) hp[k] = xor4(part[0], part[1]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < (int)kNumHPow; k++) {
-            const uint4 v = hp[k];
-            rec[kRecHPow + 4 * k] = v.x; rec[kRecHPow + 4 * k + 1] = v.y;
-            rec[kRecHPow + 4 * k + 2] = v.z; rec[kRecHPow + 4 * k + 3] = v.w;
-        }
-        uint4 b = hp[kFullPow - 1];
-        for (int i = 0; i < 128; i++) {
-            basis[i] = b;
-            b = gf_mulx(b);
-        }
-        uint4 b8 = hp[7], b16 = hp[15], b2 = hp[1], b3 = hp[2];
-        for (int i = 0; i < 32; i++) {
-            basis8[i] = b8;
-            basis16[i] = b16;
-            basis23[0][i] = b2;
-            basis23[1][i] = b3;
-            b8 = gf_mulx(b8);
-            b16 = gf_mulx(b16);
-            b2 = gf_mulx(b2);
-            b3 = gf_mulx(b3);
-        }
-        rec[kRecAlg] = NEB_ALG_AESGCM;
+    if (threadIdx.x < 64u) {
+        const uint4 v = hp[threadIdx.x >> 2];
+        const uint32_t c = threadIdx.x & 3u;
+        rec[kRecHPow + threadIdx.x] = c == 0u ? v.x : c == 1u ? v.y : c == 2u ? v.z : v.w;
     }
+    if (threadIdx.x < 128u) basis[threadIdx.x] = gf_mul_xpow(hp[kFullPow - 1], threadIdx.x);
+    if (threadIdx.x < 32u) {
+        basis8[threadIdx.x] = gf_mul_xpow(hp[7], threadIdx.x);
+        basis16[threadIdx.x] = gf_mul_xpow(hp[15], threadIdx.x);
+        basis23[0][threadIdx.x] = gf_mul_xpow(hp[1], threadIdx.x);
+        basis23[1][threadIdx.x] = gf_mul_xpow(hp[2], threadIdx.x);
+    }
+    if (threadIdx.x == 0) rec[kRecAlg] = NEB_ALG_AESGCM;
     __syncthreads();
     const uint32_t t = threadIdx.x;
     // Shoup tables: entry (k, v) for k = 1..16
@@ -1770,11 +1780,7 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
     // for H^2..H^16 above
     auto basis_of = [&](uint4 q, uint32_t cnt) {
         __syncthreads();  // basis[] is free again
-        if (t == 0u)
-            for (uint32_t i = 0; i < cnt; i++) {
-                basis[i] = q;
-                q = gf_mulx(q);
-            }
+        if (t < cnt) basis[t] = gf_mul_xpow(q, t);
         __syncthreads();
     };
     auto mul_by_basis = [&](uint4 P) -> uint4 {
