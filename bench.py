@@ -186,14 +186,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
     ap.add_argument("--mode", choices=["device", "host", "host-kcopy", "host-staged", "host-split", "tx", "rx",
-                                       "rx-device"],
+                                       "rx-device", "relay"],
                     default="device",
                     help="device: the headline; host: host-resident batch (pinned arena: zero-copy); "
                          "host-kcopy: the pinned arena staged by span-copy kernels; "
                          "host-staged: the same through hipMemcpyAsync staging; host-split: sources DMA-staged, "
                          "outputs stored by the kernel into the pinned arena; tx: the device TX batch "
                          "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows; "
-                         "rx-device: the same with the batch and the windows in device memory")
+                         "rx-device: the same with the batch and the windows in device memory; relay: GMAC-only "
+                         "seal+verify of 1348-B relayed packets (VerifyRelay), device-resident")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tx-superpackets", type=int, default=1457,
                     help="tx mode: 64 KiB TSO superpackets per batch (45 segments each; 1457 -> 65 565 wires, "
@@ -222,6 +223,8 @@ def main():
 
     cfg = args.config
     t0 = time.time()
+    if args.mode == "relay":
+        return bench_relay(args, ctrl, rank, world, device)
     b = W.make_batch(*{
         1: (L.ALG_AESGCM, 65536, 1),
         2: (L.ALG_AESGCM, 65536, 4096),
@@ -370,6 +373,49 @@ def main():
             log(f"cpu_baseline failed: {e!r}")
             out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
+
+
+def bench_relay(args, ctrl, rank, world, device):
+    """GMAC-only relay path: the relay seal (inside.go:491, empty plaintext) and
+    VerifyRelay (connection_state.go:121-148) of 64 Ki relayed packets, AD = 1348 B each, one key
+    (--config 1) or 4096 (--config 2). Every round of these waves is AAD-only, so the kernels skip
+    the AES except for E_K(J0). value = AD bytes sealed + verified per second."""
+    import torch
+
+    from nebula_amd import _lib as L
+    from nebula_amd import workload as W
+    from nebula_amd.batch import DeviceBatch, install_keys
+    from nebula_amd.noiseutil import Engine
+
+    nkeys = 4096 if args.config == 2 else 1
+    b = W.relay_batch(L.ALG_AESGCM, 65536, nkeys, seed=W.SEED ^ rank)
+    eng = Engine(device, max_keys=4096)
+    db = DeviceBatch(eng, b, install_keys(eng, b))
+    db.seal()
+    db.open()
+    torch.cuda.synchronize()
+    assert (db.status_host() == 0).all(), "relay round trip failed before timing"
+    for _ in range(args.warmup):
+        db.seal()
+        db.open()
+    torch.cuda.synchronize()
+    ctrl.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        db.seal()
+        db.open()
+    torch.cuda.synchronize()
+    dt = ctrl.max(time.perf_counter() - t0)
+    assert (db.status_host() == 0).all(), "relay verify failed inside the timed region"
+    if rank == 0:
+        ad = float(b.desc["aad_len"].astype(np.int64).sum())
+        print(json.dumps({
+            "metric": "GiB/s relay AD (GMAC-only AES-256-GCM seal + VerifyRelay), device-resident",
+            "value": round(2 * ad * args.steps * world / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"65536 relayed packets, AD 1348 B, empty plaintext, {nkeys} key(s)"},
+        }), flush=True)
 
 
 def tso_superpackets(nseg_total: int, mss: int = 1448, seed: int = 7):

@@ -1094,7 +1094,11 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 const LaneBlock b = lane_block(sh, r, l, lg);
                 const uint4 G = horner(r);
                 __builtin_amdgcn_sched_barrier(0);
-                io(b, G, gcm_lane_ks<CM>(b, c1, c2, cc, T, rk));
+                // a round with no ciphertext or length block in the wave needs no keystream: the
+                // AAD-only rounds of GMAC (relay verify, connection_state.go:121-148) skip the AES
+                uint4 ks = make_uint4(0, 0, 0, 0);
+                if (__any(b.is_ct || b.is_len)) ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
+                io(b, G, ks);
             }
         };
         if constexpr (BS && CM == 2 && kBsMode == 1) {

@@ -121,6 +121,27 @@ def make_batch(alg: int, npkt: int, nkeys: int, sizes=(1300,), ratio=(1,), seed:
     return Batch(alg, keys, remote_index, desc, arena, stride, name)
 
 
+def relay_batch(alg: int, npkt: int, nkeys: int, aad_len: int = 1348, seed: int = SEED, name: str = "relay") -> Batch:
+    """GMAC-only relay packets (ConnectionState.VerifyRelay, connection_state.go:121-148; the relay
+    seal at inside.go:491): the AD is the whole relayed packet but its last 16 bytes, the
+    ciphertext is empty and the tag follows the AD. 1348 B = outer header 16 + a 1332-B wire packet
+    (16 + 1300 + 16). Per-key counters in emission order as in make_batch."""
+    b = make_batch(alg, npkt, nkeys, sizes=(aad_len - 16,), seed=seed, name=name)
+    stride = -(-(aad_len + 16) // 64) * 64
+    arena = np.zeros(npkt * stride, np.uint8)
+    slots = arena.reshape(npkt, stride)
+    old = b.arena.reshape(npkt, b.stride)
+    slots[:, :aad_len] = old[:, :aad_len]  # header.Encode + the inner packet's bytes
+    desc = b.desc.copy()
+    base = np.arange(npkt, dtype=np.uint64) * np.uint64(stride)
+    desc["aad_off"] = base
+    desc["src_off"] = base + np.uint64(aad_len)  # the tag, right after the AD
+    desc["dst_off"] = base + np.uint64(aad_len)
+    desc["len"] = 0
+    desc["aad_len"] = aad_len
+    return Batch(alg, b.keys, b.remote_index, desc, arena, stride, name)
+
+
 # BASELINE.json configs
 def config(idx: int, scale: float = 1.0) -> Batch:
     """configs[idx] of BASELINE.json. `scale` shrinks the packet count for quick tests."""

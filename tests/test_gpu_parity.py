@@ -513,3 +513,33 @@ def test_cipher_destroy_waits_for_queued_batches(engine, oracle_mod):
         assert again.key_id == slot
     finally:
         again.destroy()
+
+
+@pytest.mark.parametrize("nkeys", [1, 64])
+def test_relay_gmac_batches(engine, oracle_mod, nkeys):
+    """GMAC-only relay packets (VerifyRelay, connection_state.go:121-148; the relay seal at
+    inside.go:491): every wave is AAD-only, so the kernels skip the AES in all rounds but the
+    length block's (E_K(J0)). A pure relay batch, then relay packets mixed into ordinary ones
+    (waves where some lanes need keystream), sealed and opened bit-exact against the oracle; a
+    flipped AD bit fails only its own packet."""
+    rb = W.relay_batch(L.ALG_AESGCM, 3000, nkeys, seed=314)
+    ref, _ = oracle_seal(oracle_mod, rb)
+    got, st = run_device(engine, rb, seal=True)
+    assert (st == 0).all()
+    assert np.array_equal(got, ref)
+    ref_o, _ = oracle_open(oracle_mod, rb, ref)
+    got_o, st_o = run_device(engine, rb, seal=False, arena=ref)
+    assert (st_o == 0).all()
+    assert np.array_equal(got_o, ref_o)
+    bad = ref.copy()
+    bad[int(rb.desc["aad_off"][17]) + 700] ^= 0x10
+    _, st_b = run_device(engine, rb, seal=False, arena=bad)
+    assert st_b[17] == L.STATUS_AUTH_FAILED and (np.delete(st_b, 17) == 0).all()
+    # mixed: relay and 1300-B packets interleaved in one batch
+    lens = [1300 if i % 3 else 0 for i in range(600)]
+    alens = [16 if i % 3 else 1348 for i in range(600)]
+    mb = _edge_batch(L.ALG_AESGCM, lens, alens, nkeys=nkeys, seed=316)
+    ref, _ = oracle_seal(oracle_mod, mb)
+    got, st = run_device(engine, mb, seal=True)
+    assert (st == 0).all()
+    assert np.array_equal(got, ref)
