@@ -15,6 +15,10 @@ for c in 1 2 3; do
   timeout -k 10 300 python bench.py --mode rx-device --steps 10 --warmup 2 --config $c > $OUT/rxd_c$c.json 2> $OUT/rxd_c$c.err || exit 1
   cat $OUT/rxd_c$c.json
 done
+for c in 1 2; do
+  timeout -k 10 300 python bench.py --mode relay --steps 20 --warmup 5 --config $c > $OUT/relay_c$c.json 2> $OUT/relay_c$c.err || exit 1
+  cat $OUT/relay_c$c.json
+done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_tx -o tx -- python3 $R/bench.py --mode tx --steps 10 --warmup 2 > $OUT/prof_tx.log 2>&1 || exit 1
 find $OUT/prof_tx -name "*kernel_stats.csv" -exec cat {} \;
