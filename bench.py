@@ -378,7 +378,7 @@ def main():
 def bench_relay(args, ctrl, rank, world, device):
     """GMAC-only relay path: the relay seal (inside.go:491, empty plaintext) and
     VerifyRelay (connection_state.go:121-148) of 64 Ki relayed packets, AD = 1348 B each, one key
-    (--config 1) or 4096 (--config 2). Every round of these waves is AAD-only, so the kernels skip
+    (--config 1) or 4096 (--config 2; --config 3: ChaCha20-Poly1305, 4096 keys). Every round of these waves is AAD-only, so the kernels skip
     the AES except for E_K(J0). value = AD bytes sealed + verified per second."""
     import torch
 
@@ -387,8 +387,9 @@ def bench_relay(args, ctrl, rank, world, device):
     from nebula_amd.batch import DeviceBatch, install_keys
     from nebula_amd.noiseutil import Engine
 
-    nkeys = 4096 if args.config == 2 else 1
-    b = W.relay_batch(L.ALG_AESGCM, 65536, nkeys, seed=W.SEED ^ rank)
+    nkeys = 4096 if args.config in (2, 3) else 1
+    alg = L.ALG_CHACHAPOLY if args.config == 3 else L.ALG_AESGCM
+    b = W.relay_batch(alg, 65536, nkeys, seed=W.SEED ^ rank)
     eng = Engine(device, max_keys=4096)
     db = DeviceBatch(eng, b, install_keys(eng, b))
     db.seal()
@@ -410,7 +411,8 @@ def bench_relay(args, ctrl, rank, world, device):
     if rank == 0:
         ad = float(b.desc["aad_len"].astype(np.int64).sum())
         print(json.dumps({
-            "metric": "GiB/s relay AD (GMAC-only AES-256-GCM seal + VerifyRelay), device-resident",
+            "metric": "GiB/s relay AD (" + ("Poly1305-only ChaCha20-Poly1305" if alg == L.ALG_CHACHAPOLY else
+                                           "GMAC-only AES-256-GCM") + " seal + VerifyRelay), device-resident",
             "value": round(2 * ad * args.steps * world / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "dtype": "u8", "data": "synthetic",

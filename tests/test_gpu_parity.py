@@ -515,14 +515,15 @@ def test_cipher_destroy_waits_for_queued_batches(engine, oracle_mod):
         again.destroy()
 
 
-@pytest.mark.parametrize("nkeys", [1, 64])
-def test_relay_gmac_batches(engine, oracle_mod, nkeys):
+@pytest.mark.parametrize("alg,nkeys", [(L.ALG_AESGCM, 1), (L.ALG_AESGCM, 64), (L.ALG_CHACHAPOLY, 64)])
+def test_relay_gmac_batches(engine, oracle_mod, alg, nkeys):
     """GMAC-only relay packets (VerifyRelay, connection_state.go:121-148; the relay seal at
     inside.go:491): every wave is AAD-only, so the kernels skip the AES in all rounds but the
-    length block's (E_K(J0)). A pure relay batch, then relay packets mixed into ordinary ones
+    length block's (E_K(J0)); ChaCha20-Poly1305 relay packets are Poly1305 over the AD. A pure
+    relay batch, then relay packets mixed into ordinary ones
     (waves where some lanes need keystream), sealed and opened bit-exact against the oracle; a
     flipped AD bit fails only its own packet."""
-    rb = W.relay_batch(L.ALG_AESGCM, 3000, nkeys, seed=314)
+    rb = W.relay_batch(alg, 3000, nkeys, seed=314)
     ref, _ = oracle_seal(oracle_mod, rb)
     got, st = run_device(engine, rb, seal=True)
     assert (st == 0).all()
@@ -538,7 +539,7 @@ def test_relay_gmac_batches(engine, oracle_mod, nkeys):
     # mixed: relay and 1300-B packets interleaved in one batch
     lens = [1300 if i % 3 else 0 for i in range(600)]
     alens = [16 if i % 3 else 1348 for i in range(600)]
-    mb = _edge_batch(L.ALG_AESGCM, lens, alens, nkeys=nkeys, seed=316)
+    mb = _edge_batch(alg, lens, alens, nkeys=nkeys, seed=316)
     ref, _ = oracle_seal(oracle_mod, mb)
     got, st = run_device(engine, mb, seal=True)
     assert (st == 0).all()
