@@ -234,6 +234,12 @@ struct ChachaArgs {
     uint32_t hdr_from_dst;     // TX batches: the first `flags` plaintext bytes from dst (GcmArgs)
 };
 
+// Payload and AAD blocks loaded one round ahead of their use (1) or in their round (0). Off: a
+// round ahead measured 2-3% slower on C4 (110.0 vs 107.1 µs per seal launch, rocprof A/B,
+// profiles/r2_s3/ab_chacha_prefetch): the kernel is bound by VALU issue, not by load latency.
+#ifndef NEB_CH_PREFETCH
+#define NEB_CH_PREFETCH 0
+#endif
 template <bool OPEN>
 __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs args) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -301,8 +307,30 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
 
         uint8_t* arena = args.arena;
         P5 A = {{0, 0, 0, 0, 0}};
+        // the lane's input block of round rho (AAD or payload; zero for the length block and
+        // outside the packet), loaded one round ahead so its latency overlaps a round of ChaCha
+        const uint32_t hdr = args.hdr_from_dst ? d.flags : 0u;
+        auto fetch = [&](uint32_t rho) -> uint4 {
+            uint4 b = make_uint4(0, 0, 0, 0);
+            const int32_t i = (int32_t)(16u * rho + l) - (int32_t)phi;
+            if (rho < nrounds && i >= 0 && i < (int32_t)(na + m)) {
+                if (i < (int32_t)na) {
+                    const uint32_t off = 16u * (uint32_t)i;
+                    b = load_block(arena + d.aad_off + off, min(16u, d.aad_len - off));
+                } else {
+                    const uint32_t off = 16u * ((uint32_t)i - na);
+                    const uint32_t nb = min(16u, d.len - off);
+                    b = off < hdr ? load_block_hdr(arena + d.dst_off + off, arena + d.src_off + off, nb, hdr - off)
+                                  : load_block(arena + d.src_off + off, nb);
+                }
+            }
+            return b;
+        };
+        uint4 cur = NEB_CH_PREFETCH ? fetch(0u) : make_uint4(0, 0, 0, 0);
         for (uint32_t rho = 0; rho < rmax; rho++) {
             if (rho >= nrounds) continue;
+            const uint4 blk = NEB_CH_PREFETCH ? cur : fetch(rho);
+            if (NEB_CH_PREFETCH) cur = fetch(rho + 1u);
 #ifdef NEB_CH_ABLATE_CHACHA  // timing study only: wrong keystream
             if (rho > kappa) ks = make_uint4(ks.x + rho, ks.y ^ rho, ks.z + j, ks.w ^ dn);
 #else
@@ -312,15 +340,11 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
             if (i < 0 || i >= (int32_t)n) continue;
             P5 mi;
             if (i < (int32_t)na) {
-                uint32_t off = 16u * (uint32_t)i;
-                uint4 b = load_block(arena + d.aad_off + off, min(16u, d.aad_len - off));
-                mi = p5_from_words(b.x, b.y, b.z, b.w, 1u);
+                mi = p5_from_words(blk.x, blk.y, blk.z, blk.w, 1u);
             } else if (i < (int32_t)(na + m)) {
                 uint32_t off = 16u * ((uint32_t)i - na);
                 uint32_t nb = min(16u, d.len - off);
-                const uint32_t hdr = args.hdr_from_dst ? d.flags : 0u;
-                uint4 in = off < hdr ? load_block_hdr(arena + d.dst_off + off, arena + d.src_off + off, nb, hdr - off)
-                                     : load_block(arena + d.src_off + off, nb);
+                const uint4 in = blk;
                 uint4 out = xor4c(in, mask_block(ks, nb));
                 store_block(arena + d.dst_off + off, out, nb);
                 uint4 c = OPEN ? in : out;
