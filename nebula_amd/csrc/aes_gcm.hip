@@ -1383,7 +1383,10 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     uint32_t main_groups = ngroups;
     if (args.tail_slots && ngroups > slots && ngroups % slots)
         main_groups = ngroups / slots * slots;  // full passes only: the tail kernel takes the rest
-    for (uint32_t grp = blockIdx.x * kSingleWaves + wave; grp < main_groups; grp += slots) {
+    // groups go to workgroups first (group g: workgroup g mod G, wave g / G), so a batch of fewer
+    // groups than waves spreads over as many CUs as it can instead of filling a few (a 2048-packet
+    // batch on 8 CUs ran as long as a whole 64 Ki pass)
+    for (uint32_t grp = blockIdx.x + wave * gridDim.x; grp < main_groups; grp += slots) {
         const uint32_t p = grp * kPpw + lane / kLpp;
         // a bitsliced wave takes the group if every packet's counters stay below 2^8 (its
         // counter planes are one byte); otherwise the T-table path
@@ -1410,6 +1413,13 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
 #define NEB_TAIL_LG 6
 #endif
 constexpr uint32_t kTailLg = NEB_TAIL_LG, kTailPpw = kWave >> kTailLg;
+// GcmArgs::tail_slots value for a batch small enough to run entirely in the tail kernel: one packet
+// per wave over 64 lanes is 2 rounds for 1300 B instead of 21, and a batch under a few thousand
+// packets is bound by one wave's latency, not by throughput
+constexpr uint32_t kTailAll = 0xFFFFFFFFu;
+#ifndef NEB_SMALL_BATCH
+#define NEB_SMALL_BATCH 4096  // packets (host-known count) up to which the tail kernel takes them all
+#endif
 static_assert(kTailLg == 4 || kTailLg == 6, "tail tables exist for 16 and 64 lanes");
 constexpr int kTailWaves = 8;
 struct TailLds {
@@ -1424,8 +1434,11 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     uint32_t npkt = args.npkt;
     if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw, slots = args.tail_slots;
-    if (ngroups <= slots || ngroups % slots == 0u) return;  // no partial pass: nothing to do
-    const uint32_t p0 = ngroups / slots * slots * kPpw;
+    uint32_t p0 = 0;  // kTailAll: a small batch, every packet here
+    if (slots != kTailAll) {
+        if (ngroups <= slots || ngroups % slots == 0u) return;  // no partial pass: nothing to do
+        p0 = ngroups / slots * slots * kPpw;
+    }
     const uint32_t tgroups = (npkt - p0 + kTailPpw - 1u) / kTailPpw;
     if (blockIdx.x * kTailWaves >= tgroups) return;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
@@ -1870,7 +1883,8 @@ extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int
     uint32_t cap = (uint32_t)(per_cu * cu_count);
     // test hook: a smaller grid, so that small batches have a partial last pass (the tail kernel)
     if (const char* g = std::getenv("NEB_SINGLE_MAX_GRID")) cap = std::max(1u, std::min(cap, (uint32_t)std::atoi(g)));
-    const uint32_t grid = std::min((groups + neb::kSingleWaves - 1u) / neb::kSingleWaves, cap);
+    // one workgroup per group up to the cap: a small batch runs one or a few groups per CU
+    const uint32_t grid = std::min(groups, cap);
     return grid * neb::kSingleWaves;
 }
 
@@ -1882,6 +1896,17 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
     const bool cs = !open && hdr_from_dst == 2;  // the TX seal with its checksums (tx.hip)
+    if (NEB_SINGLE_TAIL && !NEB_GHASH8 && !d_n && !cs && n <= (uint32_t)NEB_SMALL_BATCH) {
+        a.tail_slots = neb::kTailAll;
+        const uint32_t tgrid = std::min<uint32_t>(
+            ((n + neb::kTailPpw - 1u) / neb::kTailPpw + neb::kTailWaves - 1u) / neb::kTailWaves,
+            2u * (uint32_t)std::max(cu_count, 1));
+        if (open)
+            hipLaunchKernelGGL(neb::gcm_single_tail_kernel<true>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), 0, s, a);
+        else
+            hipLaunchKernelGGL(neb::gcm_single_tail_kernel<false>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), 0, s, a);
+        return hipGetLastError();
+    }
     const uint32_t slots = neb_gcm_single_slots(n, cu_count, open, hdr_from_dst);
     // a partial last pass (at most n packets; the real count may be on the device) goes to the
     // tail kernel, 16 lanes per packet
@@ -1921,9 +1946,10 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             hipStream_t s, int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
     neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks};
-    // one wave per chunk up to the occupancy cap (tails make chunks outnumber n / 16); the chunk
-    // count is only known on the device: workgroups past it exit before filling their tables
-    const uint32_t bound = max_chunks;
+    // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
+    // small batch's chunks spread over the CUs; the chunk count is only known on the device:
+    // workgroups past it exit before filling their tables
+    const uint32_t bound = max_chunks * (uint32_t)neb::kChunkWaves;
     return open ? launch_grid(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, a, ca)
                 : launch_grid(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, a, ca);
 }
