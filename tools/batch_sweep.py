@@ -64,6 +64,26 @@ def main():
         assert (s1 == 0).all() and (s2 == 0).all()
         out["host_pair_us"] = round(float(np.median(ts)) * 1e6, 1)
         out["host_seal_open_gibs"] = round(2 * b.payload_bytes / (out["host_pair_us"] * 1e-6) / 2**30, 2)
+        # the same with the descriptors and statuses in pinned memory too (neb_host_alloc), as a Go
+        # caller would keep them beside the arena: the kernels read and write them in place
+        import ctypes as C
+        dbuf = PinnedBuffer(d.nbytes)
+        sbuf = PinnedBuffer(4 * n)
+        dbuf.array[:] = d.view(np.uint8)
+        lib = L.lib()
+        ts = []
+        for k in range(3 + max(10, reps // 4)):
+            t0 = time.perf_counter()
+            for fn in (lib.neb_seal_batch_host, lib.neb_open_batch_host):
+                L.check(fn(eng.handle, b.alg, C.c_void_p(dbuf.ptr), n, C.c_void_p(buf.ptr), buf.nbytes,
+                           C.c_void_p(sbuf.ptr), hint), fn.__name__)
+            if k >= 3:
+                ts.append(time.perf_counter() - t0)
+        assert (sbuf.array.view(np.int32) == 0).all()
+        out["host_pinned_desc_pair_us"] = round(float(np.median(ts)) * 1e6, 1)
+        out["host_pinned_desc_seal_open_gibs"] = round(2 * b.payload_bytes / (out["host_pinned_desc_pair_us"] * 1e-6) / 2**30, 2)
+        dbuf.free()
+        sbuf.free()
         buf.free()
         for c in ciphers:
             c.destroy()
