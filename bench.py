@@ -12,9 +12,9 @@ timing is bracketed by a barrier + device sync on both sides and the max over ra
 Printed (rank 0, one JSON line): value = (payload sealed + payload opened, all ranks) / time.
 roofline: the seal kernel's algorithmic bytes (2p+32 per packet) / its mean launch time, from HIP
 events recorded on the kernel's stream inside the timed region; traffic = PMC-measured HBM bytes
-per launch from profiles/ when a counter pass for this kernel is committed there, else null.
+per launch of this config's seal kernel from profiles/pmc_configs.json, else null.
 cpu_baseline: rank 0, N = 1 only, the OpenSSL-EVP port of the per-packet loop (oracle/) on a
-bounded sample of the same batch, on this box's CPU share.
+bounded sample of the same batch, on every CPU of this process's affinity and on one thread.
 """
 from __future__ import annotations
 
@@ -91,53 +91,50 @@ class TimingEvent:
         return float(ms.value)
 
 
-def cpu_share() -> int:
+def cpu_cores() -> int:
+    """Every CPU this process may run on (sched_getaffinity): the whole host share the box grants."""
     try:
-        n = len(os.sched_getaffinity(0))
+        return max(1, len(os.sched_getaffinity(0)))
     except Exception:
-        n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+        return os.cpu_count() or 1
 
 
-def cpu_baseline(b, target_s: float = 6.0):
-    """OpenSSL-EVP port (oracle/evp_baseline.c) on a bounded sample: seal then open, each timed
-    for about target_s seconds (about 2 x target_s of CPU wall time in all)."""
+def cpu_baseline(b, target_s: float = 4.0):
+    """OpenSSL-EVP port (oracle/evp_baseline.c) on a bounded sample of the same batch: seal then
+    open, each timed for about target_s seconds, on every core this process may use (one pinned
+    thread per core), and again on one thread (1 and nproc threads)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
-    threads = cpu_share()
-    n = min(b.n, 8192)
+    threads = cpu_cores()
+    n = min(b.n, 16384)
     desc = b.desc[:n].copy()
-    arena = b.arena[: n * b.stride].copy()
+    lo = int(desc["aad_off"].min())
+    hi = int((desc["src_off"] + desc["len"].astype(np.uint64) + np.uint64(16)).max())
+    for f in ("src_off", "dst_off", "aad_off"):
+        desc[f] -= np.uint64(lo)
+    arena = b.arena[lo:hi].copy()
     keys = b.keys
-    # calibrate on a warm pool (the first pass pays thread start-up)
-    oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=1)
-    t1, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=8)
-    iters = max(1, int(target_s / max(t1 / 8, 1e-5)))
     sealed = arena.copy()
-    ts, st = oracle.evp_batch(b.alg, 0, keys, desc, sealed, threads=threads, iters=1)
+    _, st = oracle.evp_batch(b.alg, 0, keys, desc, sealed, threads=threads, iters=1)
     assert (st == 0).all()
-    work = sealed.copy()
-    to, st = oracle.evp_batch(b.alg, 1, keys, desc, work, threads=threads, iters=1)
-    assert (st == 0).all()
-    # timed: seal `iters` passes, open `iters` passes (open in place needs fresh ciphertext each pass:
-    # re-seal is not counted, so open runs on a copy that stays ciphertext by using out-of-place dst)
-    t_seal, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=threads, iters=iters)
+    # open out of place into a scratch copy, so the ciphertext stays intact across passes
     od = desc.copy()
-    scratch_off = np.uint64(len(sealed))
-    od["dst_off"] = od["src_off"] + scratch_off  # decrypt into a scratch copy, ciphertext stays intact
+    od["dst_off"] = od["src_off"] + np.uint64(len(sealed))
     big = np.concatenate([sealed, np.zeros_like(sealed)])
-    t_open, st = oracle.evp_batch(b.alg, 1, keys, od, big, threads=threads, iters=iters)
-    assert (st == 0).all()
     payload = float(desc["len"].astype(np.int64).sum())
-    gibs = 2 * payload * iters / (t_seal + t_open) / GIB
-    # one thread too (SURVEY.md §8d asks for 1 and n threads): about 1.5 s each way
-    t1s, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=1, iters=1)
-    it1 = max(1, int(1.5 / max(t1s, 1e-5)))
-    t1_seal, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=1, iters=it1)
-    t1_open, st = oracle.evp_batch(b.alg, 1, keys, od, big, threads=1, iters=it1)
-    assert (st == 0).all()
-    gibs1 = 2 * payload * it1 / (t1_seal + t1_open) / GIB
+
+    def rate(nthreads, secs):
+        oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=nthreads, iters=1)  # warm the pool
+        t1, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=nthreads, iters=2)
+        iters = max(1, int(secs / max(t1 / 2, 1e-5)))
+        t_seal, _ = oracle.evp_batch(b.alg, 0, keys, desc, arena.copy(), threads=nthreads, iters=iters)
+        t_open, st2 = oracle.evp_batch(b.alg, 1, keys, od, big, threads=nthreads, iters=iters)
+        assert (st2 == 0).all()
+        return 2 * payload * iters / (t_seal + t_open) / GIB, iters, t_seal + t_open
+
+    gibs, iters, tt = rate(threads, target_s)
+    gibs1, iters1, tt1 = rate(1, target_s / 3)
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -149,32 +146,21 @@ def cpu_baseline(b, target_s: float = 6.0):
     return {
         "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "value_1thread": round(gibs1, 3),
-        "sample": f"{n} x {int(desc['len'][0])} B packets of the same batch, seal x{iters} + open x{iters} "
-                  f"({t_seal + t_open:.1f} s), OpenSSL EVP {'AES-256-GCM' if b.alg == 1 else 'ChaCha20-Poly1305'} "
-                  f"(AES-NI/PCLMUL class, as Go's crypto/cipher), {threads} pinned threads on {model}",
+        "sample": f"{n} packets of the same batch ({payload / 1e6:.1f} MB payload), seal x{iters} + open x{iters} "
+                  f"({tt:.1f} s) on {threads} pinned threads (every CPU of this process's affinity), and "
+                  f"x{iters1} on 1 thread ({tt1:.1f} s); OpenSSL EVP "
+                  f"{'AES-256-GCM' if b.alg == 1 else 'ChaCha20-Poly1305'} (AES-NI/VAES + PCLMUL class, as Go's "
+                  f"crypto/cipher), {model}",
     }
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 counter passes
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
-    correction + WRITE_SIZE, KiB -> bytes). None when no pass for this kernel is committed."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_config(cfg_name: str):
+    """The committed counter pass of this config's dominant kernel (profiles/pmc_configs.json,
+    written by tools/pmc_config.py): HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction), LDS / VALU busy fractions, rocprof mean duration, and the pass it came from.
+    Keyed by config, so C3 and C5 (same kernel, different traffic) each report their own."""
     try:
-        d = json.load(open(p))
-        return d["kernels"][kernel]["hbm_bytes_per_launch"]
-    except Exception:
-        return None
-
-
-def pmc_busy(kernel: str):
-    """LDS-array and VALU busy fractions of `kernel` from the committed counter pass
-    (profiles/pmc_busy.json, tools/pmc_busy.py): the resources that actually bound the AEAD
-    kernels, reported beside the HBM roofline. None when none is committed."""
-    p = os.path.join(ROOT, "profiles", "pmc_busy.json")
-    try:
-        k = json.load(open(p))["kernels"][kernel]
-        return {"lds_busy": k["lds_busy"], "valu_busy": k["valu_busy"], "source": k["source"]}
+        return json.load(open(os.path.join(ROOT, "profiles", "pmc_configs.json")))[cfg_name]
     except Exception:
         return None
 
@@ -185,13 +171,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, help="BASELINE.json configs index (1 = headline)")
-    ap.add_argument("--mode", choices=["device", "host", "host-kcopy", "host-staged", "host-split", "tx", "rx",
-                                       "rx-device", "relay"],
+    ap.add_argument("--mode", choices=["device", "host", "host-staged", "tx", "rx", "rx-device", "relay"],
                     default="device",
                     help="device: the headline; host: host-resident batch (pinned arena: zero-copy); "
-                         "host-kcopy: the pinned arena staged by span-copy kernels; "
-                         "host-staged: the same through hipMemcpyAsync staging; host-split: sources DMA-staged, "
-                         "outputs stored by the kernel into the pinned arena; tx: the device TX batch "
+                         "host-staged: the same through hipMemcpyAsync staging; tx: the device TX batch "
                          "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows; "
                          "rx-device: the same with the batch and the windows in device memory; relay: GMAC-only "
                          "seal+verify of 1348-B relayed packets (VerifyRelay), device-resident")
@@ -245,11 +228,7 @@ def main():
 
     if args.mode == "host-staged":
         os.environ["NEB_HOST_MODE"] = "dma"  # read by the engine at its first host batch
-    if args.mode == "host-kcopy":
-        os.environ["NEB_HOST_MODE"] = "kcopy"
-    if args.mode == "host-split":
-        os.environ["NEB_HOST_MODE"] = "split"
-    if args.mode in ("host", "host-kcopy", "host-staged", "host-split"):
+    if args.mode in ("host", "host-staged"):
         from nebula_amd.batch import PinnedBuffer
 
         d = slot_desc(b, ciphers)
@@ -270,10 +249,7 @@ def main():
         if rank == 0:
             print(json.dumps({
                 "metric": {"host": "GiB/s host-resident (pinned arena, zero-copy: kernels load/store it over PCIe) ",
-                           "host-kcopy": "GiB/s host-resident (pinned arena, span-copy kernels in/out around seal/open) ",
                            "host-staged": "GiB/s host-resident (pinned hipMemcpyAsync H2D + kernel + D2H, 3 streams) ",
-                           "host-split": "GiB/s host-resident (pinned arena: hipMemcpyAsync H2D of the sources, kernel "
-                                         "stores into the arena) ",
                            }[args.mode]
                 + ("AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch" if cfg == 1 else
                    f"{'AES-256-GCM' if b.alg == L.ALG_AESGCM else 'ChaCha20-Poly1305'} seal+open ({workload_name})"),
@@ -341,6 +317,8 @@ def main():
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
     kern_tag = ("gcm_single_kernel<false, false>" if b.nkeys == 1 else "gcm_chunk_kernel<false>") if b.alg == 1 \
         else "chacha_batch_kernel<false>"
+    pmc = pmc_config(f"C{cfg + 1}")
+    lens = b.desc["len"].astype(np.int64)
     out = {
         "metric": "GiB/s device-resident AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch"
         if cfg == 1 else f"GiB/s device-resident {alg_name} seal+open ({workload_name})",
@@ -355,14 +333,20 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": workload_name, "packets_per_gpu": b.n, "payload_bytes_per_pkt":
-                   int(b.desc["len"].max()), "keys": b.nkeys, "cipher": alg_name,
+        "config": {"workload": workload_name, "packets_per_gpu": b.n,
+                   "payload_bytes_per_pkt": int(lens[0]) if (lens == lens[0]).all() else
+                   {"mean": round(float(lens.mean()), 1), "sizes": sorted(set(lens.tolist()))},
+                   "keys": b.nkeys, "cipher": alg_name,
                    "parallelism": f"{world} GPU(s), independent packet shards, no collective"},
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kern_tag),
-            "binding": pmc_busy(kern_tag),
-            "kernel": kern_tag, "kernel_ms": round(seal_ms, 4), "open_kernel_ms": round(open_ms, 4),
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+            "binding": {k: pmc[k] for k in ("lds_busy", "valu_busy", "mean_ns", "source") if k in pmc} if pmc else None,
+            "kernel": kern_tag,
+            # the seal call between HIP events on its stream: for mixed keys that is the binning
+            # passes (sched.hip) plus the chunk kernel, so `achieved` is a lower bound there
+            "kernel_ms": round(seal_ms, 4), "open_kernel_ms": round(open_ms, 4),
             "algorithmic_bytes_per_launch": int(alg_bytes),
         },
     }

@@ -36,6 +36,9 @@
  *                            receive batch (the recvmmsg flush, interface.go:381-413): window
  *                            Check → DecryptDanger → window Update, results identical to the
  *                            per-packet loop in arrival order
+ *   neb_queue_*              the flush points themselves (flushSendBatch interface.go:478-487,
+ *                            listenOut's flush :395-400) of every routine (interface.go:320-335),
+ *                            gathered into shared device batches
  */
 #ifndef NEBULA_AEAD_H
 #define NEBULA_AEAD_H
@@ -116,9 +119,12 @@ NEB_API const char* neb_last_error(void);
 /* Install a 32-byte key: AES-256 key schedule + H = E_K(0^128) + H^1..H^16 (AESGCM), or the raw
  * ChaCha20 key (ChaChaPoly), computed on the device into the engine's key table. */
 NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out);
-/* Waits for the engine's device to drain (every asynchronous batch enqueued on any stream), then
- * clears the key record and frees its slot. A batch enqueued after the key is destroyed gets
- * NEB_STATUS_BAD_KEY for its packets (the kernels check the slot's algorithm tag). */
+/* Waits for the asynchronous batches this engine enqueued that may read the key — the last
+ * single-key batch with it on each stream and the last mixed-key batch on each stream — then
+ * clears the key record and frees its slot. Other work on the device is not waited for. The caller
+ * stops enqueuing batches with the key before destroying it (as Go code stops using a
+ * CipherState it drops); a batch enqueued after the destroy gets NEB_STATUS_BAD_KEY for its
+ * packets (the kernels check the slot's algorithm tag) or, once the slot is reused, the new key. */
 NEB_API int neb_cipher_destroy(neb_cipher* c);
 NEB_API uint32_t neb_cipher_key_id(const neb_cipher* c);
 NEB_API int neb_cipher_alg(const neb_cipher* c);
@@ -172,9 +178,7 @@ NEB_API int neb_open_batch(neb_engine* e, int alg, const neb_desc* d_desc, uint3
  * - any other arena: the range the descriptors touch is streamed through the device in chunks of
  *   8192 packets, H2D -> kernel -> D2H, rotated over three streams; chunks whose arena ranges
  *   overlap are serialised (each copies its whole range back).
- * Environment, read per call: NEB_HOST_MODE=dma (or NEB_HOST_STAGED=1) stages every arena;
- * NEB_HOST_MODE=kcopy stages a mapped, 16-byte aligned arena with copy kernels instead of DMA
- * (slower, for A/B; an unaligned one is DMA-staged). */
+ * Environment, read per call: NEB_HOST_MODE=dma (or NEB_HOST_STAGED=1) stages every arena. */
 NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
                                 size_t arena_len, int32_t* status, uint32_t key_hint);
 NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
@@ -286,6 +290,38 @@ NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnel
                                    const neb_tx_packet* packets, uint32_t npackets, const uint8_t* in, size_t in_len,
                                    uint8_t* out, size_t out_cap, neb_tx_wire* wires, int32_t* wire_status,
                                    uint32_t max_wires, uint32_t* nwires, int32_t* packet_status, uint32_t key_hint);
+/* ---- submission queue: many threads' small flushes -> device-sized batches -------------------- */
+/* Nebula seals <= 128 packets per TX flush (overlay/batch/tx_batch.go:5, flushSendBatch
+ * interface.go:465-487) and opens <= listen.batch = 64 per RX flush (main.go:181, listenOut
+ * interface.go:381-413), from `routines` goroutines at once (interface.go:320-335). A queue
+ * gathers those flushes into one device batch: each submission's packets are copied into pinned
+ * staging, sealed or opened with the other submissions' by one zero-copy kernel launch, and copied
+ * back. A batch goes to the device when it holds max_packets, when the next submission would not
+ * fit its staging, on neb_queue_flush, or max_delay_us after its first submission. */
+typedef struct neb_queue neb_queue;
+typedef struct neb_queue_config {
+    uint32_t max_packets;  /* packets per device batch (0: 16384) */
+    uint32_t max_delay_us; /* a non-empty batch waits at most this long for more (0: 100 us) */
+    uint64_t arena_bytes;  /* pinned staging per batch (0: max_packets x 1536) */
+    uint32_t depth;        /* staging batches in rotation, 2..16 (0: 3) */
+    uint32_t reserved;     /* 0 */
+} neb_queue_config;
+/* A queue for one algorithm and direction (open = 0: seal, 1: open). cfg may be NULL (defaults). */
+NEB_API int neb_queue_create(neb_engine* e, int alg, int open, const neb_queue_config* cfg, neb_queue** out);
+/* Sends out what is queued, waits for it, and frees the queue (no submission may be in progress). */
+NEB_API int neb_queue_destroy(neb_queue* q);
+/* Seal or open n packets of the caller's host arena (any memory) through the queue, blocking until
+ * they are done: the arena bytes and statuses are those of neb_seal_batch_host / neb_open_batch_host
+ * on the same descriptors. Thread-safe, meant to be called by many threads at once. Every
+ * descriptor is checked against arena_len first (NEB_ERR_INVALID: nothing touched). A submission
+ * larger than one batch goes through in pieces. */
+NEB_API int neb_queue_submit(neb_queue* q, const neb_desc* desc, uint32_t n, uint8_t* arena, size_t arena_len,
+                             int32_t* status);
+/* Send the batch being filled to the device now, without waiting for its deadline. */
+NEB_API int neb_queue_flush(neb_queue* q);
+/* stats[0..3]: device batches launched, packets, submissions, staged bytes (since creation). */
+NEB_API int neb_queue_stats(neb_queue* q, uint64_t stats[4]);
+
 /* ---- header (the AAD) --------------------------------------------------------------------- */
 
 NEB_API void neb_header_encode(uint8_t b[16], uint8_t version, uint8_t type, uint8_t subtype, uint32_t remote_index,

@@ -90,7 +90,18 @@ SIGNATURES = {
     "neb_tx_seal_batch": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
     "neb_tx_seal_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _vp, _u32, _vp, _vp,
                                     _u32]),
+    "neb_queue_create": (_i, [_vp, _i, _i, _vp, C.POINTER(_vp)]),
+    "neb_queue_destroy": (_i, [_vp]),
+    "neb_queue_submit": (_i, [_vp, _vp, _u32, _vp, _sz, _vp]),
+    "neb_queue_flush": (_i, [_vp]),
+    "neb_queue_stats": (_i, [_vp, _vp]),
 }
+
+
+class QueueConfig(C.Structure):
+    """neb_queue_config (include/nebula_aead.h)."""
+    _fields_ = [("max_packets", C.c_uint32), ("max_delay_us", C.c_uint32), ("arena_bytes", C.c_uint64),
+                ("depth", C.c_uint32), ("reserved", C.c_uint32)]
 
 _lib = None
 
@@ -134,6 +145,8 @@ def lib():
                                "(nebula_amd has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("NEB_LIB_PATH") and not hasattr(L, name):
+                continue  # an older A/B build (tools/ab.sh) may predate some entry points
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -101,3 +101,49 @@ def host_batch(engine: Engine, alg: int, open_: bool, desc: np.ndarray, arena: n
             arena.nbytes, status.ctypes.data_as(C.c_void_p), key_hint)
     L.check(rc, fn.__name__)
     return status
+
+
+class SubmitQueue:
+    """neb_queue_*: one algorithm and direction's submission queue. Many threads call submit() with
+    their own small flushes (Nebula's 64-128 packet TX / RX flushes, interface.go:381-487); the
+    queue joins them into device batches and returns each caller its own results."""
+
+    def __init__(self, engine: Engine, alg: int, open_: bool, max_packets: int = 0, max_delay_us: int = 0,
+                 arena_bytes: int = 0, depth: int = 0):
+        cfg = L.QueueConfig(max_packets, max_delay_us, arena_bytes, depth, 0)
+        h = C.c_void_p()
+        L.check(L.lib().neb_queue_create(engine.handle, alg, 1 if open_ else 0, C.byref(cfg), C.byref(h)),
+                "neb_queue_create")
+        self.h = h
+        self.alg = alg
+        self.open = open_
+
+    def submit(self, desc: np.ndarray, arena: np.ndarray, status: Optional[np.ndarray] = None) -> np.ndarray:
+        """Seal/open desc over arena (host memory, in place per descriptor), blocking until done."""
+        assert desc.dtype == L.DESC_DTYPE and arena.dtype == np.uint8 and arena.flags["C_CONTIGUOUS"]
+        if status is None:
+            status = np.full(len(desc), -1, np.int32)
+        rc = L.lib().neb_queue_submit(self.h, desc.ctypes.data_as(C.c_void_p), len(desc),
+                                      arena.ctypes.data_as(C.c_void_p), arena.nbytes,
+                                      status.ctypes.data_as(C.c_void_p))
+        L.check(rc, "neb_queue_submit")
+        return status
+
+    def flush(self) -> None:
+        L.check(L.lib().neb_queue_flush(self.h), "neb_queue_flush")
+
+    def stats(self) -> dict:
+        v = (C.c_uint64 * 4)()
+        L.check(L.lib().neb_queue_stats(self.h, v), "neb_queue_stats")
+        return {"batches": v[0], "packets": v[1], "submissions": v[2], "bytes": v[3]}
+
+    def close(self) -> None:
+        if self.h:
+            L.lib().neb_queue_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

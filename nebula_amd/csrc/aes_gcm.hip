@@ -3,27 +3,23 @@
 // Replaces the arithmetic behind noiseutil/aesgcm.go:24-49 (EncryptDanger/DecryptDanger = Go
 // crypto/cipher GCM Seal/Open with nonce 00000000 || BE64(n)) for a whole batch of packets.
 //
-// Work decomposition (DESIGN.md §Kernels):
-//  * One wavefront holds 4 packets at a time, 16 lanes per packet ("packet group").
+// Work decomposition (DESIGN.md §3):
+//  * A "packet group" is 64 / LPP packets of one wave, LPP = 2^lg lanes each (4 in the single-key
+//    kernel and in full mixed-key chunks; 8 or 16 for short tail chunks; 64 in the tail kernel).
 //  * A packet's GHASH input is n = a + m + 1 blocks (a AAD blocks, m ciphertext blocks, 1 length
-//    block), front-padded with zero blocks to n' = 16·R. In round r lane l owns padded block
-//    g' = 16r + l + 1: it runs the AES-CTR keystream for that block (if it is a ciphertext block),
-//    loads / XORs / stores the 16 payload bytes (16 lanes × 16 B contiguous per packet), and folds
-//    the block into its Horner accumulator A_l = A_l·H^16 ⊕ X.
-//  * After R rounds GHASH = Σ_l A_l·H^(16-l): lane l multiplies by H^(NLP - l mod NLP), the
-//    NLP-lane groups XOR-reduce, and a log-tree over the 16/NLP groups with multipliers
-//    H^NLP, H^2NLP, … finishes. The length block always lands on lane 15 of the last round; that
-//    lane also computes E_K(J0) for the tag.
-//  * AES: T-table pairs (T0[x], T2[x]) in LDS, one copy per lane of a 32-lane half (32 copies ×
-//    256 × 8 B = 64 KiB): every ds_read_b64 is bank-conflict-free and its address is one
-//    v_perm_b32; T1/T3 are one rotate of the XOR of two lookups (rotation distributes over XOR).
-//  * GHASH, one tunnel key (SINGLE): the Horner multiply by H^16 uses a "full" 4-bit table over all
-//    32 nibble positions (F_p[v] = v·x^4p·H^16, reduced): 32 conflict-free ds_read_b128 + XORs, no
-//    shifts, no reduction. The final per-lane multiply uses 4-bit Shoup tables M_k[v] = v·H^k with
-//    deferred reduction (NLP = 16). All tables are precomputed at key install and copied into LDS
-//    once per workgroup. Round keys are wave-uniform (scalar registers).
-//  * GHASH, mixed keys: each packet's round keys and Shoup tables for H, H^2, H^4, H^8, H^16
-//    (NLP = 2) are staged in the wave's LDS slice per packet group.
+//    block), front-padded with zero blocks to n' = LPP·R. In round r lane l owns padded block
+//    g' = LPP·r + l + 1: it runs the AES-CTR keystream for that block (if it is a ciphertext block),
+//    loads / XORs / stores the 16 payload bytes, and folds the block into its Horner accumulator
+//    A_l = A_l·H^LPP ⊕ X. The length block always lands on the packet's last lane; that lane also
+//    computes E_K(J0) for the tag.
+//  * After R rounds GHASH = Σ_l A_l·H^(LPP-l): one multiply per lane after a lane permutation
+//    (LPP 4), or a pairwise tree (LPP 8-64).
+//  * AES: T-tables in LDS, 32 swizzled copies so every ds_read_b32 is bank-conflict-free and its
+//    address is one v_perm_b32 (four tables, 128 KiB, in the single-key kernel; two tables, 64 KiB,
+//    T1/T3 by one rotate, elsewhere). Round keys are wave-uniform (scalar registers).
+//  * GHASH tables (precomputed at key install): a reduction-free "full" nibble table of H^4, and
+//    position / Shoup tables of the other powers, staged in LDS per workgroup (one key) or per
+//    wave and chunk (mixed keys).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -33,7 +29,6 @@
 
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
-#include "bs_aes.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
 
@@ -214,6 +209,12 @@ struct TLook4 {
 #ifndef NEB_PRIO
 #define NEB_PRIO 3
 #endif
+#ifndef NEB_RMAX_SHFL
+#define NEB_RMAX_SHFL 0
+#endif
+#ifndef NEB_CHUNK_OPAQUE_LANE
+#define NEB_CHUNK_OPAQUE_LANE 1
+#endif
 
 // AES-256 rounds FIRST..13 (full) and 14 (final) on the state s0..s3 (after round FIRST-1).
 template <int FIRST, class TL, class RK>
@@ -236,17 +237,6 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
         __builtin_amdgcn_s_setprio(0);
 #endif
         // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k; with two tables T1 = rotl8 T0, T3 = rotl8 T2
-#ifdef NEB_DUMMY_VALU
-        {  // experiment: extra VALU work per round that feeds nothing but a final register
-            uint32_t d0 = s0 ^ 0x1234u, d1 = s1 ^ 0x5678u;
-#pragma unroll
-            for (int q = 0; q < NEB_DUMMY_VALU / 2; q++) {
-                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(d0) : "v"(d1), "v"(s2));
-                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(d1) : "v"(d0), "v"(s3));
-            }
-            asm volatile("" ::"v"(d0), "v"(d1));
-        }
-#endif
         if constexpr (TL::kFour) {
             if constexpr (RK::kUniform) {
                 s0 = x3s(x3(a0, a1, a2), a3, k.x);
@@ -417,6 +407,13 @@ __device__ __forceinline__ uint4 gf_mul_xpow(uint4 q, uint32_t i) {
     return gf_reduce(z);
 }
 
+// q·x^b, b < 32 (gf_mul_xpow with no whole-word shift): 128 + 32 bits, the top word reduced.
+__device__ __forceinline__ uint4 gf_mul_xpow32(uint4 q, uint32_t b) {
+    const uint32_t z[8] = {q.x >> b, shr64(q.x, q.y, b), shr64(q.y, q.z, b), shr64(q.z, q.w, b), shr64(q.w, 0u, b),
+                           0u, 0u, 0u};
+    return gf_reduce(z);
+}
+
 // (byte K of w) & 0xF0 in one VALU op (SDWA byte select); hipcc emits a shift + and for most K.
 template <int K>
 __device__ __forceinline__ uint32_t byte_hi_nibble(uint32_t w) {
@@ -449,36 +446,6 @@ __device__ __forceinline__ uint4 gf_mul_full(uint4 x, uint4 acc, const uint4* ft
             const uint4 e2 = lds_at<uint4>(ftab, (uint32_t)(8 * q + 7 - 2 * k) * 256u + al[k]);
             acc = x34(acc, e1, e2);
         }
-    }
-    return acc;
-}
-
-// x · F with a byte-window table (the single-key kernel's GHASH, NEB_GHASH8): 16 lookups of
-// F8_P[b] = b·x^(8P)·H^4 instead of 32 nibble lookups. Entry b of position P sits at byte
-// b*256 + P*16 of f8, so position P owns banks 4P..4P+3. A ds_read_b128 is served in groups of 16
-// lanes whose lane & 15 are all different (MI355X_MICROARCH.md, LDS): lane f reads its byte
-// positions in the rotated order P = (f + j) mod 16, so at every step the 16 lanes of a group read
-// 16 different positions — 16 different bank groups — and no lookup conflicts whatever the data.
-// f = lane & 15; cw[w] byte t = ((f + 4w + t) & 15) << 4 (the bank-group byte of step 4w + t).
-__device__ __forceinline__ uint4 gf_mul_byte(uint4 x, const uint4* f8, uint32_t f, uint4 cw) {
-    // byte j of the little-endian 128-bit z is byte j of the block (GCM order), then rotate right
-    // by 8f bits: byte j of y = byte (f + j) mod 16 of the block
-    const uint32_t z0 = bswap32(x.x), z1 = bswap32(x.y), z2 = bswap32(x.z), z3 = bswap32(x.w);
-    const bool r1 = (f & 4u) != 0u, r2 = (f & 8u) != 0u;
-    const uint32_t a0 = r1 ? z1 : z0, a1 = r1 ? z2 : z1, a2 = r1 ? z3 : z2, a3 = r1 ? z0 : z3;
-    const uint32_t b0 = r2 ? a2 : a0, b1 = r2 ? a3 : a1, b2 = r2 ? a0 : a2, b3 = r2 ? a1 : a3;
-    const uint32_t sh = (f & 3u) << 3;
-    const uint32_t y[4] = {__builtin_amdgcn_alignbit(b1, b0, sh), __builtin_amdgcn_alignbit(b2, b1, sh),
-                           __builtin_amdgcn_alignbit(b3, b2, sh), __builtin_amdgcn_alignbit(b0, b3, sh)};
-    const uint32_t c[4] = {cw.x, cw.y, cw.z, cw.w};
-    uint4 acc = make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 16; j += 2) {
-        // address = (byte t of y) << 8 | (byte t of c): one v_perm
-        const uint32_t t0 = (uint32_t)(j & 3), t1 = (uint32_t)((j + 1) & 3);
-        const uint4 e1 = lds_at<uint4>(f8, perm(y[j >> 2], c[j >> 2], 0x0C0C0000u | ((4u + t0) << 8) | t0));
-        const uint4 e2 = lds_at<uint4>(f8, perm(y[(j + 1) >> 2], c[(j + 1) >> 2], 0x0C0C0000u | ((4u + t1) << 8) | t1));
-        acc = x34(acc, e1, e2);
     }
     return acc;
 }
@@ -611,8 +578,8 @@ struct GcmArgs {
     // TX batches only (tx.hip): a descriptor's first `flags` plaintext bytes are read from its
     // destination (the patched header image), the rest from src (the TUN read itself)
     uint32_t hdr_from_dst;
-    // single-key kernel: the waves of its grid (NEB_SINGLE_TAIL: packets past its full passes are
-    // left to gcm_single_tail_kernel), 0 = it takes every packet itself
+    // single-key kernel: the waves of its grid (packets past its full passes are left to
+    // gcm_single_tail_kernel), 0 = it takes every packet itself
     uint32_t tail_slots;
 };
 
@@ -666,17 +633,11 @@ __device__ __forceinline__ uint4 gcm_lane_load(const neb_desc& d, const LaneBloc
     return in;
 }
 
-// Where the length lane keeps E_K(J0) from its round to the tag finish: a register, or (the
-// mixed-key kernel, whose open would otherwise spill at 128 VGPRs) the lane's LDS slot.
+// Where the length lane keeps E_K(J0) from its round to the tag finish.
 struct Ej0Reg {
     uint4 v = make_uint4(0, 0, 0, 0);
     __device__ __forceinline__ void set(uint4 k) { v = k; }
     __device__ __forceinline__ uint4 get() const { return v; }
-};
-struct Ej0Lds {
-    uint4* p;
-    __device__ __forceinline__ void set(uint4 k) { *p = k; }
-    __device__ __forceinline__ uint4 get() const { return *p; }
 };
 
 // Payload XOR and GHASH input of one block given its input and keystream. Returns X (BE words).
@@ -705,13 +666,9 @@ __device__ __forceinline__ uint4 gcm_lane_io(const neb_desc& d, const LaneBlock&
 template <int CM, class TL, class RK>
 __device__ __forceinline__ uint4 gcm_lane_ks(const LaneBlock& b, uint32_t c1, uint32_t c2, const CtrConst& cc,
                                              const TL& T, const RK& rk) {
-#ifdef NEB_ABLATE_AES
-    return make_uint4(c1 ^ b.ctr, c2, b.ctr * 0x9E3779B9u, cc.k0w);
-#else
     if constexpr (CM == 2) return aes256_ctr8_block(cc, b.ctr, T, rk);
     else if constexpr (CM == 1) return aes256_ctr_block(cc, b.ctr, T, rk);
     else return aes256_block(0u, c1, c2, bswap32(b.ctr), T, rk);
-#endif
 }
 
 // Tag finish on the packet's last lane, which holds E_K(J0) (seal: store; open: compare, zero
@@ -756,15 +713,6 @@ constexpr uint32_t kLpp = 1u << kLg;    // = kFullPow, the full table's power
 constexpr uint32_t kPpw = 64u / kLpp;   // packets per wave
 static_assert(kLpp == kFullPow, "the single-key Horner stride is the full table's power");
 
-// broadcast lane j of each quad (DPP quad_perm)
-template <int J>
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J | (J << 2) | (J << 4) | (J << 6), 0xF, 0xF, false);
-}
-template <int J>
-__device__ __forceinline__ uint4 quad_bcast4(uint4 v) {
-    return make_uint4(quad_bcast<J>(v.x), quad_bcast<J>(v.y), quad_bcast<J>(v.z), quad_bcast<J>(v.w));
-}
 __device__ __forceinline__ uint4 shfl4(uint4 v, uint32_t src) {
     return make_uint4(__shfl(v.x, (int)src), __shfl(v.y, (int)src), __shfl(v.z, (int)src), __shfl(v.w, (int)src));
 }
@@ -774,67 +722,17 @@ __device__ __forceinline__ uint4 shfl_down4(uint4 v, uint32_t d) {
 
 // GHASH tables a packet group multiplies with: horner(A) = A·H^LPP, and final(A) = the packet's
 // Σ_l A_l·H^(LPP-l), valid at least on the packet's last lane (the one holding E_K(J0)).
-// Single-key kernel, experiment (off): part of the CTR keystream from the bitsliced VALU pass
-// (bs_aes.hpp) instead of the LDS T-tables, so the VALU would carry part of the AES while the LDS
-// serves the rest. Mode 1: kBsWaves waves of the workgroup run their packets on it; mode 2: every
-// wave runs an 8-round window of its packets on it, windows staggered by wave phase. Both are
-// bit-exact (GPU parity suite) and both measured ~20% slower on C2 (seal 0.124 -> 0.148-0.152 ms,
-// DESIGN.md §3.4): the pass costs ~1.5 VALU cycles per LDS cycle it saves, and VALU work beside the
-// T-table waves slows their LDS feed.
-#ifndef NEB_BITSLICE
-#define NEB_BITSLICE 0
-#endif
-constexpr bool kBitslice = NEB_BITSLICE != 0;
-#ifndef NEB_BS_WAVES
-#define NEB_BS_WAVES 4  // bitsliced waves per single-key workgroup (one per SIMD)
-#endif
-constexpr int kBsWaves = NEB_BS_WAVES;
-#ifndef NEB_BS_MODE
-#define NEB_BS_MODE 1  // 1: kBsWaves bitsliced waves; 2: every wave, an 8-round window by wave phase
-#endif
-constexpr int kBsMode = NEB_BS_MODE;
-#ifndef NEB_SINGLE_POSH
-#define NEB_SINGLE_POSH 1  // final quad Horner on H's position tables (0: H's Shoup table)
-#endif
-struct GhFull {  // one key per batch, LPP 4: reduction-free full table for H^4 + tables for H
-    static constexpr bool kBitslice = true;  // one key per batch: the bitsliced CTR pass applies
-    const uint4* full;
-    const uint4* shoup_h;  // NEB_SINGLE_POSH: the 8 position tables of H, else its Shoup table
-    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const {
-        return gf_mul_full(a, make_uint4(0, 0, 0, 0), full);
-    }
-    // (((A_0·H ⊕ A_1)·H ⊕ A_2)·H ⊕ A_3)·H, computed identically in the 4 lanes of the quad
-    __device__ __forceinline__ uint4 final(uint4 A, uint32_t, uint32_t) const {
-        uint4 V = quad_bcast4<0>(A);
-#ifndef NEB_ABLATE_FINAL
-#if NEB_SINGLE_POSH
-        V = xor4(gf_mul_pos(V, shoup_h), quad_bcast4<1>(A));
-        V = xor4(gf_mul_pos(V, shoup_h), quad_bcast4<2>(A));
-        V = xor4(gf_mul_pos(V, shoup_h), quad_bcast4<3>(A));
-        V = gf_mul_pos(V, shoup_h);
-#else
-        V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<1>(A));
-        V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<2>(A));
-        V = xor4(gf_mul_shoup(V, 0u, shoup_h), quad_bcast4<3>(A));
-        V = gf_mul_shoup(V, 0u, shoup_h);
-#endif
-#endif
-        return V;
-    }
-};
-// The single-key final as one multiply per lane: lane l of a quad needs A_l·H^(4-l), and the quad
+//
+// The final as one multiply per lane (LPP 4): lane l of a quad needs A_l·H^(4-l), and the quad
 // XOR of those is the packet's Σ_l A_l·H^(4-l). A ds_read_b128 is served in four groups of 16 lanes
 // (MI355X_MICROARCH.md, LDS); lanes of one group reading different tables at the same nibble would
 // conflict, so the accumulators are first permuted (ds_bpermute) so that group g holds role g of
 // all 16 packets and multiplies by H^(4-g) alone — conflict-free, as the Horner step — then pulled
-// back and XORed over the quad. 8 bpermutes + 1 multiply instead of GhFull's 4 multiplies.
-#ifndef NEB_SINGLE_FINAL_PERM
-#define NEB_SINGLE_FINAL_PERM 1
-#endif
+// back and XORed over the quad. 8 bpermutes + 1 multiply instead of a quad Horner's 4 multiplies.
 struct FinalPermLanes {
     uint32_t src1, src2, off;  // pull source (role g of packet idx), pull-back source, table offset
 };
-// tab_off[g]: byte offset from the LDS base of the position tables of H^(4-g)
+// tab_off[g]: byte offset from the LDS base of the tables of H^(4-g)
 __device__ __forceinline__ FinalPermLanes final_perm_lanes(uint32_t lane, const uint32_t tab_off[4]) {
     // b128 lane groups: lanes 32h + 4·c + j with c = quad index mod 8, group 2h + parity(c), index
     // 4·(c >> 1) + j within it (groups {0-3,12-15,20-27}, {4-11,16-19,28-31} and the upper half)
@@ -856,8 +754,18 @@ __device__ __forceinline__ uint4 dpp4(uint4 v) {
                       (uint32_t)__builtin_amdgcn_mov_dpp((int)v.z, CTRL, 0xF, 0xF, false),
                       (uint32_t)__builtin_amdgcn_mov_dpp((int)v.w, CTRL, 0xF, 0xF, false));
 }
-struct GhFullPerm {  // GhFull with the permuted one-multiply final
-    static constexpr bool kBitslice = true;
+// pull role g of every packet into b128 group g, multiply, pull back, XOR over the quad
+template <class MUL>
+__device__ __forceinline__ uint4 final_perm(uint4 A, const FinalPermLanes& fp, MUL&& mul) {
+    const uint4 a = shfl4(A, fp.src1);
+    uint4 v = shfl4(mul(a, fp.off), fp.src2);
+    v = xor4(v, dpp4<0xB1>(v));     // quad_perm [1,0,3,2]
+    return xor4(v, dpp4<0x4E>(v));  // quad_perm [2,3,0,1]
+}
+
+// One key per batch, LPP 4 (gcm_single_kernel): reduction-free full table of H^4 for the Horner
+// step, position tables of H, H^2, H^3, H^4 for the permuted final.
+struct GhFullPerm {
     const uint4* full;
     const void* base;  // the LDS base of FinalPermLanes::off
     FinalPermLanes fp;
@@ -865,87 +773,60 @@ struct GhFullPerm {  // GhFull with the permuted one-multiply final
         return gf_mul_full(a, make_uint4(0, 0, 0, 0), full);
     }
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t, uint32_t) const {
-        const uint4 a = shfl4(A, fp.src1);
-        uint4 v = shfl4(gf_mul_pos_off(a, base, fp.off), fp.src2);
-        v = xor4(v, dpp4<0xB1>(v));  // quad_perm [1,0,3,2]
-        return xor4(v, dpp4<0x4E>(v));  // quad_perm [2,3,0,1]
-    }
-};
-struct GhByte {  // one key per batch, LPP 4: byte-window table for H^4 (gf_mul_byte) + tables for H
-    static constexpr bool kBitslice = true;
-    const uint4* f8;
-    const uint4* shoup_h;  // the 8 position tables of H
-    uint32_t f;            // lane & 15
-    uint4 cw;              // bank-group bytes per step (gf_mul_byte)
-    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_byte(a, f8, f, cw); }
-    __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
-        return GhFull{nullptr, shoup_h}.final(A, lane, lg);
-    }
-};
-constexpr uint32_t kChunkTables = 5;  // Shoup tables H, H^2, H^4, H^8, H^16 (table i = H^(2^i))
-#ifndef NEB_CHUNK_POS
-#define NEB_CHUNK_POS 1  // 4-lane chunks multiply by H^4 with position tables (gf_mul_pos)
-#endif
-struct GhShoup {  // one key per chunk: its Shoup tables (and H^4 position tables) in the wave's LDS slice
-    static constexpr bool kBitslice = false;
-    const uint4* base;
-    const uint4* pos;
-    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t lg) const {
-#if NEB_CHUNK_POS
-        return gf_mul_pos(a, pos);  // the position tables of H^(2^lg)
-#else
-        return gf_mul_shoup(a, lg * 256u, base);
-#endif
-    }
-    // Pairwise tree over the packet's lanes: level i folds V_l·H^(2^i) ⊕ V_(l+2^i) into the lanes
-    // l ≡ 0 mod 2^(i+1); after lg levels lane 0 holds Z with Σ_l A_l·H^(LPP-l) = Z·H.
-    // lg + 1 multiplies instead of a Horner's LPP.
-    __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
-        uint4 V = A;
-        for (uint32_t i = 0; i < lg; i++) V = xor4(gf_mul_shoup(V, i * 256u, base), shfl_down4(V, 1u << i));
-        V = gf_mul_shoup(V, 0u, base);
-        return shfl4(V, lane & ~((1u << lg) - 1u));
+        return final_perm(A, fp, [&](uint4 a, uint32_t off) { return gf_mul_pos_off(a, base, off); });
     }
 };
 
-// Mixed-key chunks (gcm_chunk_kernel): the wave's slice holds the Shoup tables M_1, M_2, M_3, M_4
-// (record tables 0-3) and M_8 (NEB_CHUNK_FINAL_PERM), and the position tables of H^(2^lg). A 4-lane
-// chunk (16 packets, the layout of the single-key kernel) takes the permuted final of GhFullPerm on
-// the Shoup tables: b128 lane group g multiplies role g of every packet by M_(4-g), one multiply per
-// lane instead of the tree's three; 8- and 16-lane tails keep the tree (M_1, M_2, M_4, M_8).
-#ifndef NEB_CHUNK_FINAL_PERM
-#define NEB_CHUNK_FINAL_PERM 1
-#endif
-// (not inlined, its call saves every live register: 208-256 B of scratch per lane instead of 52-64)
-__device__ __forceinline__ uint4 chunk_tree_final(uint4 A, uint32_t lane, uint32_t lg, const uint4* base) {
+// Pairwise tree over the packet's lanes: level i folds V_l·H^(2^i) ⊕ V_(l+2^i) into the lanes
+// l ≡ 0 mod 2^(i+1); after lg levels lane 0 holds Z with Σ_l A_l·H^(LPP-l) = Z·H: lg + 1 multiplies
+// instead of a Horner's LPP. shoup_off(i): LDS byte offset (from base) of the Shoup table of H^(2^i).
+template <class OFF>
+__device__ __forceinline__ uint4 tree_final(uint4 A, uint32_t lane, uint32_t lg, const uint4* base, OFF&& shoup_off) {
     uint4 V = A;
-    for (uint32_t i = 0; i < lg; i++) {
-        const uint32_t off = i == 3u ? 4u * 256u : ((1u << i) - 1u) * 256u;  // M_(2^i)
-        V = xor4(gf_mul_shoup(V, off, base), shfl_down4(V, 1u << i));
-    }
-    V = gf_mul_shoup(V, 0u, base);
+    for (uint32_t i = 0; i < lg; i++) V = xor4(gf_mul_shoup(V, shoup_off(i), base), shfl_down4(V, 1u << i));
+    V = gf_mul_shoup(V, shoup_off(0u), base);
     return shfl4(V, lane & ~((1u << lg) - 1u));
 }
-struct GhChunk {
-    static constexpr bool kBitslice = false;
+
+// The single-key tail kernel (64 lanes per packet): Shoup tables of H^(2^i), i < lg, in order, and
+// the position tables of H^(2^lg) for the Horner step.
+struct GhShoup {
     const uint4* base;
     const uint4* pos;
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
-        if (lg == 2u) {  // wave-uniform
-            const uint32_t tab_off[4] = {3u * 256u, 2u * 256u, 256u, 0u};  // M_4, M_3, M_2, M_1
-            const FinalPermLanes fp = final_perm_lanes(lane, tab_off);
-            const uint4 a = shfl4(A, fp.src1);
-            uint4 v = shfl4(gf_mul_shoup(a, fp.off, base), fp.src2);
-            v = xor4(v, dpp4<0xB1>(v));
-            return xor4(v, dpp4<0x4E>(v));
-        }
-        return chunk_tree_final(A, lane, lg, base);
+        return tree_final(A, lane, lg, base, [](uint32_t i) { return i * 256u; });
     }
 };
-#if NEB_CHUNK_FINAL_PERM
-static_assert(NEB_CHUNK_POS && !NEB_WIDE_CHUNKS, "GhChunk: position-table Horner, chunks of 4-16 lanes per packet");
-#endif
+
+// Mixed-key chunks (gcm_chunk_kernel), tables in the wave's LDS slice, restaged per chunk.
+// Full chunks (16 packets at 4 lanes, the single-key kernel's layout): Horner on the position
+// tables of H^4, the permuted final on the Shoup tables M_1..M_4 (b128 group g multiplies role g of
+// every packet by M_(4-g)).
+struct GhChunk4 {
+    const uint4* shoup;  // M_1, M_2, M_3, M_4 (record Shoup tables 0-3)
+    const uint4* pos;    // position tables of H^4
+    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
+    __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t) const {
+        // the lane permutation is recomputed here rather than held across the chunk loop, where
+        // its registers would be spilled (the compiler would hoist it: the opaque copy of `lane`
+        // keeps it here)
+        const uint32_t ln = lane;
+        const uint32_t tab_off[4] = {3u * 256u, 2u * 256u, 256u, 0u};  // M_4, M_3, M_2, M_1
+        return final_perm(A, final_perm_lanes(ln, tab_off),
+                          [&](uint4 a, uint32_t off) { return gf_mul_shoup(a, off, shoup); });
+    }
+};
+// Tail chunks (1-8 packets at 8 or 16 lanes): Horner on the position tables of H^(2^lg), the tree
+// on M_1, M_2, M_4, M_8.
+struct GhChunkTree {
+    const uint4* shoup;  // M_1, M_2, M_4, M_8
+    const uint4* pos;    // position tables of H^(2^lg)
+    __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
+    __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
+        return tree_final(A, lane, lg, shoup, [](uint32_t i) { return i * 256u; });
+    }
+};
 
 // ---- the TX checksum in the seal (CS; tx.hip kTxCsumFlag) ----------------------------------
 // The TX segment kernel leaves in the L4 checksum field the partial sum of everything but the
@@ -1003,12 +884,10 @@ __device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uin
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
-template <bool OPEN, bool BS, bool CS = false, class GH, class TL, class EJ = Ej0Reg>
+template <bool OPEN, bool CS = false, class GH, class TL>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
-                                                 uint32_t lane, uint32_t lg, EJ ej0 = EJ{},
-                                                 const uint32_t* bs_rec = nullptr, uint32_t bs_phase = 0,
-                                                 const uint4* cs_pow = nullptr) {
+                                                 uint32_t lane, uint32_t lg, const uint4* cs_pow = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
@@ -1028,8 +907,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     sh.n = sh.na + sh.m + 1u;
     sh.R = run ? (sh.n + LPP - 1u) >> lg : 0u;
     sh.pad = (sh.R << lg) - sh.n;
-    uint32_t Rmax = sh.R;
-    for (uint32_t s = LPP; s < 64u; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, (int)s));
+    Ej0Reg ej0;
 
     // nonce 00000000 || BE64(n) as little-endian words; counter block word 3 = BE32(ctr)
     const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32));
@@ -1042,7 +920,6 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
         // round r's payload XOR and GHASH fold, given G = A·H^LPP (the rounds before) and the keystream
         auto io = [&](const LaneBlock& b, uint4 G, uint4 ks) {
-#ifndef NEB_NO_FASTIO
             // the common round: every active lane holds a full payload block with a 16-B aligned
             // destination (the arena base counts too: a caller may pass an arena at any byte
             // address); a source off 16-B alignment (a TX segment inside its TUN read) is read as
@@ -1061,7 +938,6 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 A = xor4(G, bswap4(OPEN ? in : out));
                 return;
             }
-#endif
             const uint4 in = gcm_lane_load(d, b, args.arena, hdr);
             if constexpr (CS) {
                 if (cs_on && b.is_ct) {
@@ -1080,13 +956,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
             }
             A = xor4(G, gcm_lane_io<OPEN>(d, b, in, ks, args.arena, ej0));
         };
-        auto horner = [&](uint32_t r) -> uint4 {
-#ifdef NEB_ABLATE_HORNER
-            return A;
-#else
-            return r == 0 ? make_uint4(0, 0, 0, 0) : gh.horner(A, lg);
-#endif
-        };
+        auto horner = [&](uint32_t r) -> uint4 { return r == 0 ? make_uint4(0, 0, 0, 0) : gh.horner(A, lg); };
         // one round on the LDS: GHASH of the previous rounds first, then this round's T-table AES
         // (one phase's registers at a time)
         auto tround = [&](uint32_t r) {
@@ -1101,66 +971,19 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 io(b, G, ks);
             }
         };
-        if constexpr (BS && CM == 2 && kBsMode == 1) {
-            // Bitsliced waves (gcm_single_kernel): the keystream of every round from the VALU pass
-            // (bs_aes.hpp), 8 rounds per pass; the length lane's slot takes counter 1 (E_K(J0)).
-            for (uint32_t w0 = 0; w0 < Rmax; w0 += 8u) {
-                const uint32_t base = 4u * w0 + 2u - sh.pad - sh.na;  // counter of block 4j + l: round w0 + j
-                const uint32_t jl = sh.R - 1u - w0;                  // the length round in this pass
-                const uint32_t jmask = jl < 8u ? 1u << (4u * jl + 3u) : 0u;
-                uint4 ks[8];
-                bs_ctr_pass(c1, c2, base, jmask, bs_rec, lane, ks);
-                const uint32_t wend = min(w0 + 8u, Rmax);
-                // one copy of the round body; the keystream registers shift down a block per round
-#pragma unroll 1
-                for (uint32_t r = w0; r < wend; r++) {
-                    if (r < sh.R) io(lane_block(sh, r, l, lg), horner(r), ks[0]);
-#pragma unroll
-                    for (int q = 0; q < 7; q++) ks[q] = ks[q + 1];
-                }
-            }
-            return;
-        }
-        uint32_t r0 = 0;
-        if constexpr (BS && CM == 2 && kBsMode == 2) {
-            // Windowed: rounds [s, s+8) of every packet from the VALU pass, s by wave phase so the
-            // waves of one SIMD take their pass at different times; the length block after it.
-            uint32_t Rmin = run ? sh.R : 0u;
-            for (uint32_t sft = LPP; sft < 64u; sft <<= 1) Rmin = min(Rmin, (uint32_t)__shfl_xor((int)Rmin, (int)sft));
-            Rmin = __builtin_amdgcn_readfirstlane(Rmin);
-            if (lg == 2u && Rmin >= 9u) {
-                const uint32_t s = (uint32_t)bs_phase * (Rmin - 9u) / 3u;
-                for (; r0 < s; r0++) tround(r0);
-                uint4 ks[8];
-                bs_ctr_pass(c1, c2, 4u * s + 2u - sh.pad - sh.na, 0u, bs_rec, lane, ks);
-                if (valid) d = args.desc[p];  // re-derived: no registers held across the pass
-                sh.na = (d.aad_len + 15u) >> 4;
-                sh.m = (d.len + 15u) >> 4;
-                sh.n = sh.na + sh.m + 1u;
-                sh.R = run ? (sh.n + LPP - 1u) >> lg : 0u;
-                sh.pad = (sh.R << lg) - sh.n;
-                cc = aes_ctr_prep8(c1, c2, T, rk);
-#pragma unroll 1
-                for (; r0 < s + 8u; r0++) {
-                    io(lane_block(sh, r0, l, lg), horner(r0), ks[0]);
-#pragma unroll
-                    for (int q = 0; q < 7; q++) ks[q] = ks[q + 1];
-                }
-            }
-        }
-        for (uint32_t r = r0; r < Rmax; r++) tround(r);
-    };
-    if constexpr (BS && kBsMode == 1) {
-        rounds(std::integral_constant<int, 2>{});  // the caller checked: every counter below 2^8
-    } else {
-        // counter caching needs every block counter of every packet in the wave below 2^8 / 2^16
-#ifndef NEB_NO_CTR8
-        if (__all(sh.m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
-        else
+#if NEB_RMAX_SHFL
+        uint32_t Rmax = sh.R;
+        for (uint32_t s = LPP; s < 64u; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, (int)s));
+        for (uint32_t r = 0; r < Rmax; r++) tround(r);
+#else
+        // rounds until no packet of the wave has one left (a ballot, no cross-lane reduction)
+        for (uint32_t r = 0; __any(r < sh.R); r++) tround(r);
 #endif
-        if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
-        else rounds(std::integral_constant<int, 0>{});
-    }
+    };
+    // counter caching needs every block counter of every packet in the wave below 2^8 / 2^16
+    if (__all(sh.m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
+    else if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
+    else rounds(std::integral_constant<int, 0>{});
     if constexpr (CS) {
         for (uint32_t sft = 1; sft < LPP; sft <<= 1) {
             cs_acc += (uint32_t)__shfl_xor((int)cs_acc, (int)sft);
@@ -1182,164 +1005,42 @@ __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rk
 
 // ---- one tunnel key for the whole batch -------------------------------------------------------
 
-// Single-key GHASH on the byte-window table (gf_mul_byte: 16 conflict-free lookups per multiply
-// instead of 32); its 64 KiB leave room for the two-table AES only. Bit-exact (GPU parity suite)
-// and it cuts the kernel's LDS-array cycles 6%, but the seal time does not move (0.124 ms both,
-// profiles/r2_micro/ab_ghash8.log): with the LDS less loaded, the waves' own dependency chains at
-// 4 waves per SIMD set the pace. Off: the nibble table is simpler and as fast.
-#ifndef NEB_GHASH8
-#define NEB_GHASH8 0
-#endif
-// The last, partial pass of a batch larger than one pass of the grid's waves (e.g. 65 565 packets
-// = 4098 groups of 16 on 4096 waves) runs with 16 lanes per packet, 4 packets per wave: the groups
-// that would otherwise run alone after everything else take a quarter of the rounds
-// (bench.py --mode tx: 1457 vs 1456 superpackets, 0.243 vs 0.207 ms).
-#ifndef NEB_SINGLE_TAIL
-#define NEB_SINGLE_TAIL 1
-#endif
-
-#ifndef NEB_G8_LAYOUT
-#define NEB_G8_LAYOUT 0
-#endif
-#ifndef NEB_T4
-#if NEB_GHASH8
-#define NEB_T4 0
-#else
-#define NEB_T4 1  // single-key kernel on the four-table AES (TLook4); 0 = the two-table TLook
-#endif
-#endif
-#if NEB_GHASH8 && NEB_T4
-#error "NEB_GHASH8 needs the two-table AES (64 KiB byte-window table + 128 KiB T-tables exceed the LDS)"
-#endif
-#ifndef NEB_SINGLE_WAVES
-#if NEB_T4 || NEB_GHASH8
-#define NEB_SINGLE_WAVES 16  // waves per workgroup (one workgroup per CU: 136-138 KiB of LDS)
-#else
-#define NEB_SINGLE_WAVES 8   // waves per workgroup (2 workgroups per CU, 74 KiB each)
-#endif
-#endif
-static_assert(NEB_SINGLE_WAVES * 64 <= 1024, "workgroup size");
-#ifndef NEB_SINGLE_WPE
-#define NEB_SINGLE_WPE 4    // launch bound: waves per SIMD
-#endif
-constexpr int kSingleWaves = NEB_SINGLE_WAVES;
+// Four-table AES (TLook4, 128 KiB) + the GHASH tables: one 1024-lane workgroup per CU, 4 waves per
+// SIMD, at most 128 VGPRs.
+constexpr int kSingleWaves = 16;
+constexpr int kSingleWpe = 4;  // launch bound: waves per SIMD
 constexpr int kSingleThreads = kSingleWaves * kWave;
 
-#if NEB_GHASH8 && NEB_G8_LAYOUT
-struct SingleLds {  // experiment: T-tables first, the byte table above 64 KiB
-    uint2 ttab[256 * 32];    // 64 KiB  T-table pairs, 32 copies
-    uint4 shoup_h[8 * 16];   // 2 KiB   position tables of H (the final quad Horner)
-    uint4 f8[256 * 16];      // 64 KiB  F8_P[b] for H^4: entry b of position P at b*16 + P
-};
-#elif NEB_GHASH8
-// shoup_h and f8 first: their lookups fold their base into the ds_read offset field; the T-tables
-// sit at byte 66 KiB, reached through bit 16 of the lane bases plus an offset of 2 KiB. f4: the
-// record's nibble table, copied in with coalesced loads to build f8 from (every workgroup reading
-// its entries scattered from global memory put 8 MB of requests on one 8 KiB: +23 µs per launch).
 struct SingleLds {
-    uint4 shoup_h[8 * 16];   // 2 KiB   position tables of H (the final quad Horner)
-    uint4 f8[256 * 16];      // 64 KiB  F8_P[b] for H^4: entry b of position P at b*16 + P
-    uint2 ttab[256 * 32];    // 64 KiB  T-table pairs, 32 copies
-    uint4 f4[32 * 16];       // 8 KiB   F_p[v] for H^4 (prologue only)
-};
-static_assert(NEB_SINGLE_POSH, "NEB_GHASH8 keeps the position-table final");
-#else
-struct SingleLds {
-    uint4 full[32 * 16];     // 8 KiB  F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
-#if NEB_SINGLE_POSH
-    uint4 shoup_h[8 * 16];   // 2 KiB  position tables of H
-#else
-    uint4 shoup_h[16];       // 256 B  M[v] = v·H
-#endif
-#if NEB_T4
+    uint4 full[32 * 16];       // 8 KiB   F_p[v] for H^4 (first: its offsets fit the ds_read offset field)
+    uint4 pos1[8 * 16];        // 2 KiB   position tables of H
     uint2 ttab[2 * 256 * 32];  // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each
-#else
-    uint2 ttab[256 * 32];    // 64 KiB T-table pairs, 32 copies
-#endif
-#if NEB_SINGLE_FINAL_PERM
-    uint4 pos23[2][8 * 16];  // 4 KiB  position tables of H^2 and H^3 (GhFullPerm)
-#endif
+    uint4 pos23[2][8 * 16];    // 4 KiB   position tables of H^2 and H^3 (the permuted final)
 };
-#endif
-#if NEB_SINGLE_FINAL_PERM
-static_assert(NEB_SINGLE_POSH && !NEB_GHASH8, "the permuted final uses the position tables of H, H^2, H^3, H^4");
-#endif
-
 struct SingleLdsCs : SingleLds {
     uint4 pow2[10 * 16];  // 2.5 KiB  Shoup tables of H^(2^j), j < 10 (the TX checksum correction)
 };
 
 // CS: the TX seal with the L4 checksums (gcm_csum_fix)
 template <bool OPEN, bool CS = false>
-__global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_kernel(GcmArgs args) {
+__global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(GcmArgs args) {
     __shared__ std::conditional_t<CS, SingleLdsCs, SingleLds> lds;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
-#if !NEB_GHASH8
     // the record's GHASH tables: loaded before the T-table fill and stored after it, so their
     // latency overlaps the fill's instead of following it
     static_assert(kSingleThreads >= 512, "one full-table entry per thread");
     uint4 r_full = make_uint4(0, 0, 0, 0), r_h = make_uint4(0, 0, 0, 0), r_p = make_uint4(0, 0, 0, 0);
     if (tid < 512u) r_full = ld_rec4(srec, kRecFull + 4u * tid);
-#if NEB_SINGLE_POSH
     if (tid < 128u) r_h = ld_rec4(srec, kRecPos1 + 4u * tid);
-#else
-    if (tid < 16u) r_h = ld_rec4(srec, kRecShoup + 4u * tid);
-#endif
-#if NEB_SINGLE_FINAL_PERM
     if (tid < 256u) r_p = ld_rec4(srec, (tid < 128u ? kRecPos2 : kRecPos3) + 4u * (tid & 127u));
-#endif
-#endif
-#if NEB_GHASH8
-#if NEB_G8_LAYOUT
-    const TLook T{lds.ttab, ttab_lane_base(lane)};
-#else
-    static_assert(offsetof(SingleLds, ttab) == 65536u + 2048u, "T-table base: bit 16 + offset field");
-    const TLook T{reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(&lds) + 2048), ttab_lane_base(lane, 1u << 16)};
-#endif
-    fill_ttab<256u * 32u, kSingleThreads>(lds.ttab, tid, ttab_entry);
-    // F8_P[b] = F4_2P[b >> 4] ^ F4_2P+1[b & 15] from the record's nibble table (layout.hpp)
-#if NEB_G8_LAYOUT
-    for (uint32_t i = tid; i < 256u * 16u; i += kSingleThreads) {
-        const uint32_t b = i >> 4, P = i & 15u;
-        lds.f8[i] = xor4(ld_rec4(srec, kRecFull + 4u * ((2u * P) * 16u + (b >> 4))),
-                         ld_rec4(srec, kRecFull + 4u * ((2u * P + 1u) * 16u + (b & 15u))));
-    }
-#else
-    if (tid < 512u) lds.f4[tid] = ld_rec4(srec, kRecFull + 4u * tid);
-    __syncthreads();
-    for (uint32_t i = tid; i < 256u * 16u; i += kSingleThreads) {
-        const uint32_t b = i >> 4, P = i & 15u;
-        lds.f8[i] = xor4(lds.f4[(2u * P) * 16u + (b >> 4)], lds.f4[(2u * P + 1u) * 16u + (b & 15u)]);
-    }
-#endif
-#elif NEB_T4
     const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
     fill_ttab<2u * 256u * 32u, kSingleThreads>(lds.ttab, tid, ttab4_entry);
-#else
-    const TLook T{lds.ttab, ttab_lane_base(lane)};
-    fill_ttab<256u * 32u, kSingleThreads>(lds.ttab, tid, ttab_entry);
-#endif
-#if !NEB_GHASH8
     if (tid < 512u) lds.full[tid] = r_full;
-#if NEB_SINGLE_POSH
-    if (tid < 128u) lds.shoup_h[tid] = r_h;
-#else
-    if (tid < 16u) lds.shoup_h[tid] = r_h;
-#endif
-#if NEB_SINGLE_FINAL_PERM
+    if (tid < 128u) lds.pos1[tid] = r_h;
     if (tid < 256u) lds.pos23[tid >> 7][tid & 127u] = r_p;
-#endif
-#else
-#if NEB_SINGLE_POSH
-    if (tid < 128u) lds.shoup_h[tid] = ld_rec4(srec, kRecPos1 + 4u * tid);
-#else
-    if (tid < 16u) lds.shoup_h[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
-#endif
-#endif
-
     const uint4* cs_pow = nullptr;
     if constexpr (CS) {
         if (tid < 160u) lds.pow2[tid] = ld_rec4(srec, rec_shoup_pow2(tid >> 4) + 4u * (tid & 15u));
@@ -1349,33 +1050,13 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     load_round_keys(srec, rks);
     __syncthreads();
     const RkRegs rk{rks};
-#if NEB_GHASH8
-    const uint32_t f = lane & 15u;
-    uint4 cw;
-    {
-        uint32_t c[4];
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            c[w] = 0;
-#pragma unroll
-            for (int t = 0; t < 4; t++) c[w] |= ((f + 4u * w + t) & 15u) << (4 + 8 * t);
-        }
-        cw = make_uint4(c[0], c[1], c[2], c[3]);
-    }
-    const GhByte gh{lds.f8, lds.shoup_h, f, cw};
-#elif NEB_SINGLE_FINAL_PERM
     const uint32_t tab_off[4] = {(uint32_t)offsetof(SingleLds, full), (uint32_t)offsetof(SingleLds, pos23[1]),
-                                 (uint32_t)offsetof(SingleLds, pos23[0]), (uint32_t)offsetof(SingleLds, shoup_h)};
+                                 (uint32_t)offsetof(SingleLds, pos23[0]), (uint32_t)offsetof(SingleLds, pos1)};
     const GhFullPerm gh{lds.full, &lds, final_perm_lanes(lane, tab_off)};
-#else
-    const GhFull gh{lds.full, lds.shoup_h};
-#endif
 
     // The slot must still hold an AES-GCM key when the batch runs (a key destroyed, or its slot
     // reused by another algorithm, while the batch was queued): every packet gets BAD_KEY then.
     const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
-    // the last kBsWaves waves (one per SIMD) run the bitsliced keystream (bs_aes.hpp)
-    const bool bs_wave = kBitslice && (kBsMode == 2 || wave >= (uint32_t)(kSingleWaves - kBsWaves));
     uint32_t npkt = args.npkt;
     if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
@@ -1388,44 +1069,30 @@ __global__ __launch_bounds__(kSingleThreads, NEB_SINGLE_WPE) void gcm_single_ker
     // batch on 8 CUs ran as long as a whole 64 Ki pass)
     for (uint32_t grp = blockIdx.x + wave * gridDim.x; grp < main_groups; grp += slots) {
         const uint32_t p = grp * kPpw + lane / kLpp;
-        // a bitsliced wave takes the group if every packet's counters stay below 2^8 (its
-        // counter planes are one byte); otherwise the T-table path
-        bool use_bs = bs_wave;
-        if (use_bs && kBsMode == 1) {
-            const uint32_t len = p < npkt ? args.desc[p].len : 0u;
-            use_bs = __all(((len + 15u) >> 4) + 1u < 256u);
-        }
-        if (use_bs)
-            gcm_packet_group<OPEN, true>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, Ej0Reg{},
-                                         srec, (wave >> 2) & 3u);
-        else
-            gcm_packet_group<OPEN, false, CS>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg,
-                                              Ej0Reg{}, nullptr, 0u, cs_pow);
+        gcm_packet_group<OPEN, CS>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, cs_pow);
     }
 }
 
-// The tail pass (NEB_SINGLE_TAIL): the packets after gcm_single_kernel's full passes over
-// args.tail_slots waves, 2^kTailLg lanes per packet: the two-table AES (64 KiB), Horner stride
+// The tail pass: the packets after gcm_single_kernel's full passes over args.tail_slots waves (the
+// groups that would otherwise run alone after everything else: 65 565 packets = 4098 groups of 16
+// on 4096 waves), 2^kTailLg lanes per packet: the two-table AES (64 KiB), Horner stride
 // H^(2^kTailLg) on its position tables, the final tree on the Shoup tables of H .. H^(2^(kTailLg-1))
 // (GhShoup). A tail is small and runs on few waves, so its time is one packet's latency: at 64
-// lanes a 1300-B packet takes 2 rounds instead of 6 at 16.
-#ifndef NEB_TAIL_LG
-#define NEB_TAIL_LG 6
-#endif
-constexpr uint32_t kTailLg = NEB_TAIL_LG, kTailPpw = kWave >> kTailLg;
+// lanes a 1300-B packet takes 2 rounds instead of 6 at 16 (bench.py --mode tx: 1457 vs 1456
+// superpackets, 0.243 vs 0.207 ms before it).
+constexpr uint32_t kTailLg = 6, kTailPpw = kWave >> kTailLg;
 // GcmArgs::tail_slots value for a batch small enough to run entirely in the tail kernel: one packet
 // per wave over 64 lanes is 2 rounds for 1300 B instead of 21, and a batch under a few thousand
 // packets is bound by one wave's latency, not by throughput
 constexpr uint32_t kTailAll = 0xFFFFFFFFu;
-#ifndef NEB_SMALL_BATCH
-#define NEB_SMALL_BATCH 6144  // packets (host-known count) up to which the tail kernel takes them all (A/B: 6144 55.8 vs 71.3 us per seal, 8192 equal, 12288 101 vs 75)
-#endif
-static_assert(kTailLg == 4 || kTailLg == 6, "tail tables exist for 16 and 64 lanes");
+// packets (host-known count) up to which the tail kernel takes them all (A/B: 6144 55.8 vs 71.3 us
+// per seal, 8192 equal, 12288 101 vs 75)
+constexpr uint32_t kSmallBatch = 6144;
 constexpr int kTailWaves = 8;
 struct TailLds {
-    uint2 ttab[256 * 32];      // 64 KiB T-table pairs, 32 copies
-    uint4 shoup[kTailLg * 16]; // 1-1.5 KiB
-    uint4 pos[8 * 16];         // 2 KiB
+    uint2 ttab[256 * 32];       // 64 KiB T-table pairs, 32 copies
+    uint4 shoup[kTailLg * 16];  // 1.5 KiB
+    uint4 pos[8 * 16];          // 2 KiB
 };
 template <bool OPEN>
 __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(GcmArgs args) {
@@ -1442,81 +1109,83 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     const uint32_t tgroups = (npkt - p0 + kTailPpw - 1u) / kTailPpw;
     if (blockIdx.x * kTailWaves >= tgroups) return;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
-#ifndef NEB_ABLATE_TAIL_STAGE  // (ablation: wrong results, timing only)
     fill_ttab<256u * 32u, kTailWaves * kWave>(lds.ttab, tid, ttab_entry);
-#endif
     if (tid < 16u * kTailLg) {  // M[v] of H^(2^j), j < kTailLg
         const uint32_t j = tid >> 4, v = tid & 15u;
         lds.shoup[tid] = ld_rec4(srec, rec_shoup_pow2(j) + 4u * v);
     }
-    if (tid < 128u) lds.pos[tid] = ld_rec4(srec, (kTailLg == 6u ? kRecPos64 : kRecPos16) + 4u * tid);
+    if (tid < 128u) lds.pos[tid] = ld_rec4(srec, kRecPos64 + 4u * tid);
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
     const TLook T{lds.ttab, ttab_lane_base(lane)};
     const GhShoup gh{lds.shoup, lds.pos};
     const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
-#ifdef NEB_ABLATE_TAIL_WORK  // (ablation: wrong results, timing only)
-    return;
-#endif
     for (uint32_t t = blockIdx.x * kTailWaves + wave; t < tgroups; t += gridDim.x * kTailWaves) {
         const uint32_t p = p0 + kTailPpw * t + (lane >> kTailLg);
-        gcm_packet_group<OPEN, false>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, kTailLg);
+        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, kTailLg);
     }
 }
 
 // ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------
 
-// The mixed-key kernel keeps the two-table AES: with four tables (one 16-wave workgroup per CU)
-// C3 sealed 1-2% faster but IMIX 4% slower (A/B, tools/ablate.sh NEB_CHUNK_T4=1).
-#ifndef NEB_CHUNK_T4
-#define NEB_CHUNK_T4 0
-#endif
-#ifndef NEB_CHUNK_WAVES
-#if NEB_CHUNK_T4 || NEB_CHUNK_POS
-#define NEB_CHUNK_WAVES 16  // one workgroup per CU (116 KiB of LDS; 148 KiB with T4)
-#else
-#define NEB_CHUNK_WAVES 8
-#endif
-#endif
-#ifndef NEB_CHUNK_WPE
-#define NEB_CHUNK_WPE 4  // launch bound: waves per SIMD (4: at most 128 VGPRs)
-#endif
-constexpr int kChunkWaves = NEB_CHUNK_WAVES;
+// One kernel, two code paths, each specialised for its chunk shape (one path with a run-time lanes
+// per packet spilled 52-64 B per lane at 128 VGPRs, inside the chunk loop):
+//  front chunks (chunks[0, F)): groups of 16 packets at 4 lanes each, the layout of the single-key
+//               kernel (GhChunk4), one after another on one staging of the key;
+//  back chunks (chunks[max - 1 - j], j < B): tails of 1-8 packets at 8 or 16 lanes (GhChunkTree).
+// The two-table AES (64 KiB): 16 waves per workgroup, one workgroup per CU.
+constexpr int kChunkWaves = 16;
+constexpr int kChunkWpe = 4;  // launch bound: waves per SIMD (at most 128 VGPRs)
 constexpr int kChunkThreads = kChunkWaves * kWave;
-// E_K(J0) in LDS instead of a register removes the open kernel's in-loop spills (HBM traffic 280 ->
-// 238 MB per C3 launch) but made both chunk kernels 9% slower (171 -> 186 µs, rocprof A/B,
-// tools/ab_ej0.sh): off.
-#ifndef NEB_CHUNK_EJ0_LDS
-#define NEB_CHUNK_EJ0_LDS 0
-#endif
 
 struct ChunkLds {
-    uint4 shoup[kChunkWaves][kChunkTables][16];  // per wave: M[v] for H, H^2, H^4, H^8, H^16 (1.25 KiB)
-#if NEB_CHUNK_POS
-    uint4 pos[kChunkWaves][8 * 16];              // per wave: position tables of H^4 (2 KiB)
-#endif
-#if NEB_CHUNK_EJ0_LDS
-    uint4 ej0[kChunkWaves][kWave];               // per lane: E_K(J0) of its packet (16 KiB)
-#endif
-#if NEB_CHUNK_T4
-    uint2 ttab[2 * 256 * 32];                    // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each
-#else
-    uint2 ttab[256 * 32];                        // 64 KiB T-table pairs, 32 copies
-#endif
+    uint4 shoup[kChunkWaves][4][16];  // per wave: Shoup tables (1 KiB): M_1..M_4 (full), M_1, M_2, M_4, M_8 (tails)
+    uint4 pos[kChunkWaves][8 * 16];   // per wave: position tables of H^(2^lg) (2 KiB)
+    uint2 ttab[256 * 32];             // 64 KiB T-table pairs, 32 copies
 };
 
-// Chunk order (the chunks are sorted longest first):
-//  2 (default): workgroup w owns chunks w, w + G, w + 2G, ... and its waves draw them from an LDS
-//     cursor one chunk ahead, so the next descriptor load overlaps the current chunk. Balance stays
-//     dynamic inside the workgroup and no wave touches a global atomic: C3 step -8%, IMIX -27%
-//     against 0 (A/B, profiles/r2_micro/ab_chunk_order.log).
-//  1: a static stride over all waves, next descriptor loaded ahead (C3 +5%, IMIX -12%).
-//  0: one global work cursor drawn after each chunk (round 1): its returning atomics on one word
-//     serialise across the chip.
-#ifndef NEB_CHUNK_STATIC
-#define NEB_CHUNK_STATIC 2
+// Stage a chunk key's GHASH tables in the wave's LDS slice, computed from the record's raw powers
+// H^1..H^16 (16 B each) rather than copied from its precomputed tables: 128 B of key material per
+// chunk instead of 3 KiB, which for IMIX-sized chunks was a third of the kernel's memory traffic.
+//   shoup[t][v] = v·H^(e_t), t < 4: e = 1, 2, 3, 4 (FULL) or 1, 2, 4, 8 (tails)
+//   pos[r][v]   = v·x^(4r)·P, r < 8, P = H^(2^lg): XOR of the basis P·x^(4r+j) over the set bits
+//                 of v (bit 3 ↔ j = 0), the basis P·x^i (i < 32) one per lane and shuffled
+#ifndef NEB_CHUNK_TABLES_COPY
+#define NEB_CHUNK_TABLES_COPY 0  // A/B: 1 copies the record's precomputed tables instead (3 KiB per chunk)
 #endif
+template <bool FULL>
+__device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t lane, uint32_t lg, uint4* wtab,
+                                                   uint4* wpos) {
+#if NEB_CHUNK_TABLES_COPY
+    if (FULL) {
+        wtab[lane] = ld_rec4(rec, kRecShoup + 4u * lane);
+    } else {
+        const uint32_t t = lane >> 4;  // 0, 1, 3, 7
+        wtab[lane] = ld_rec4(rec, kRecShoup + 64u * ((1u << t) - 1u) + 4u * (lane & 15u));
+    }
+    const uint32_t pt = rec_pos_table(lg);
+    wpos[lane] = ld_rec4(rec, pt + 4u * lane);
+    wpos[64u + lane] = ld_rec4(rec, pt + 4u * (64u + lane));
+    return;
+#endif
+    const uint32_t t = lane >> 4, v = lane & 15u;
+    const uint32_t e = FULL ? t + 1u : 1u << t;
+    const uint4 he = ld_rec4(rec, kRecHPow + 4u * (e - 1u));
+    const uint4 P = ld_rec4(rec, kRecHPow + 4u * ((1u << lg) - 1u));
+    wtab[lane] = gf_tab_entry(he, v);
+    const uint4 B = gf_mul_xpow32(P, lane & 31u);
+    uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; j++) {
+        const uint4 b0 = shfl4(B, 4u * t + j), b1 = shfl4(B, 4u * t + 16u + j);
+        const uint32_t m = (v >> (3u - j)) & 1u ? ~0u : 0u;
+        e0 = xor4(e0, make_uint4(b0.x & m, b0.y & m, b0.z & m, b0.w & m));
+        e1 = xor4(e1, make_uint4(b1.x & m, b1.y & m, b1.z & m, b1.w & m));
+    }
+    wpos[lane] = e0;
+    wpos[64u + lane] = e1;
+}
 
 struct ChunkArgs {
     const uint32_t* sorted;
@@ -1525,129 +1194,91 @@ struct ChunkArgs {
     uint32_t max_chunks;
 };
 
-// Chunks come from a work cursor, full ones first (chunks[0, F)), then the tails stored from the
-// end of the array: waves that drew cheap chunks draw again, and the cheap chunks run last.
+// Chunk order: the chunks of each kind come longest first (size class). Workgroup w owns chunks w,
+// w + G, w + 2G, ... of its kind (G workgroups) and its waves draw them from an LDS cursor, one
+// chunk ahead, so the next chunk's descriptor load overlaps the current chunk. Balance stays
+// dynamic inside the workgroup and no wave touches a global atomic (a global work cursor: returning
+// atomics on one word serialise across the chip; C3 step -8%, IMIX -27% against it, A/B,
+// profiles/r2_micro/ab_chunk_order.log).
 template <bool OPEN>
-__global__ __launch_bounds__(kChunkThreads, NEB_CHUNK_WPE) void gcm_chunk_kernel(GcmArgs args, ChunkArgs ca) {
+__global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(GcmArgs args, ChunkArgs ca) {
     __shared__ ChunkLds lds;
+    __shared__ uint32_t wg_cursor;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-#if NEB_CHUNK_T4
-    const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
-#else
-    const TLook T{lds.ttab, ttab_lane_base(lane)};
-#endif
     const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
     const uint32_t nback = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
-    const uint32_t nch = nfront + nback;
-#if NEB_CHUNK_STATIC == 2
-    if (blockIdx.x >= nch) return;  // owns no chunk (uniform over the workgroup)
-#else
-    if (blockIdx.x * (uint32_t)kChunkWaves >= nch) return;  // uniform over the workgroup
-#endif
-#if NEB_CHUNK_T4
-    fill_ttab<2u * 256u * 32u, kChunkThreads>(lds.ttab, tid, ttab4_entry);
-#else
+    // chunk index space: [0, nfront) the front chunks, then the tails (chunks[max - 1 - j])
+    const uint32_t c0 = 0u, nch = nfront + nback;
+    if (c0 + blockIdx.x >= nch) return;  // owns no chunk (uniform over the workgroup)
     fill_ttab<256u * 32u, kChunkThreads>(lds.ttab, tid, ttab_entry);
-#endif
-    __syncthreads();
-    uint4* wtab = &lds.shoup[wave][0][0];
-#if NEB_CHUNK_POS
-    uint4* wpos = &lds.pos[wave][0];
-#if NEB_CHUNK_FINAL_PERM
-    const GhChunk gh{wtab, wpos};
-#else
-    const GhShoup gh{wtab, wpos};
-#endif
-#else
-    const GhShoup gh{wtab, nullptr};
-#endif
-
-    // First chunk: the wave's own index; later ones from the work cursor once a chunk is done, so
-    // waves that drew short chunks draw again (longest first: front, then back). Every wave
-    // pulling its first chunk off one atomic word at launch would serialise ~4096 dequeues at
-    // ≈88/µs (MI355X_MICROARCH.md, dequeue).
-#if NEB_CHUNK_STATIC != 2
-    const uint32_t nwaves = gridDim.x * kChunkWaves;
-#endif
-#if NEB_CHUNK_STATIC == 2
-    // workgroup w owns chunks w, w + G, w + 2G, ... (G workgroups; longest first); its waves draw
-    // them from an LDS cursor, one chunk ahead, so the next descriptor is in flight meanwhile
-    __shared__ uint32_t wg_cursor;
     if (tid == 0) wg_cursor = kChunkWaves;
     __syncthreads();
-    auto chunk_of = [&](uint32_t k) { return blockIdx.x + k * gridDim.x; };
-    uint32_t c = chunk_of(wave);
-#elif NEB_CHUNK_STATIC == 1
-    uint32_t c = blockIdx.x * kChunkWaves + wave;
-#endif
-#if NEB_CHUNK_STATIC
-    // static stride over the longest-first chunk order, next descriptor loaded one chunk ahead
-    uint4 ch_next = ca.chunks[0];
-    if (c < nch) ch_next = ca.chunks[c < nfront ? c : ca.max_chunks - 1u - (c - nfront)];
+    uint4* wtab = &lds.shoup[wave][0][0];
+    uint4* wpos = &lds.pos[wave][0];
+    auto chunk_at = [&](uint32_t c) { return ca.chunks[c < nfront ? c : ca.max_chunks - 1u - (c - nfront)]; };
+    // Workgroup w owns chunks w, w + G, w + 2G, ... (front chunks first: the longest) and its waves
+    // draw them from an LDS cursor, one chunk ahead. Drawing the last 10-50% from a global cursor
+    // instead (dynamic balance across workgroups) made the C3 kernel 26-50% slower: the returning
+    // atomics on one word serialise across the chip (A/B).
+    auto chunk_of = [&](uint32_t k) -> uint32_t { return c0 + blockIdx.x + k * gridDim.x; };
+    uint32_t c = 0;
+    if (lane == 0u) c = chunk_of(wave);
+    c = __builtin_amdgcn_readfirstlane(c);
+    uint4 ch_next = make_uint4(0, 0, 0, 0);
+    if (c < nch) ch_next = chunk_at(c);
     while (c < nch) {
         const uint4 ch = ch_next;
-#if NEB_CHUNK_STATIC == 2
-        uint32_t k = 0;
-        if (lane == 0u) k = atomicAdd(&wg_cursor, 1u);
-        const uint32_t cn = chunk_of(__builtin_amdgcn_readfirstlane(k));
-#else
-        const uint32_t cn = c + nwaves;
+        const bool full = c < nfront;
+        uint32_t cn = 0;
+        if (lane == 0u) cn = chunk_of(atomicAdd(&wg_cursor, 1u));
+        cn = __builtin_amdgcn_readfirstlane(cn);
+        if (cn < nch) ch_next = chunk_at(cn);
+        // Lane-derived constants (the T-table lane base, shuffle sources, the final's permutation)
+        // are rebuilt per chunk from an opaque copy of the lane index: hoisted out of the chunk loop
+        // they stay live across it and the compiler spills them (36-104 B of scratch per lane).
+        uint32_t ln = lane;
+#if NEB_CHUNK_OPAQUE_LANE
+        asm volatile("" : "+v"(ln));
 #endif
-        if (cn < nch) ch_next = ca.chunks[cn < nfront ? cn : ca.max_chunks - 1u - (cn - nfront)];
-#else
-    for (uint32_t c = blockIdx.x * kChunkWaves + wave; c < nch;) {
-        const uint4 ch = ca.chunks[c < nfront ? c : ca.max_chunks - 1u - (c - nfront)];  // wave-uniform
-#endif
+        const TLook T{lds.ttab, ttab_lane_base(ln)};
         const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
         const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
         const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
-        const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);
         const uint32_t* rec = args.keys + (size_t)(key < args.max_keys ? key : 0u) * kKeyRecDwords;
         const bool key_ok = key < args.max_keys && rec[kRecAlg] == NEB_ALG_AESGCM;
         uint32_t rks[60];
         load_round_keys(rec, rks);
-        // stage the chunk key's Shoup tables H^(2^i), i = 0..4 (record tables 0, 1, 3, 7, 15)
-#if NEB_CHUNK_FINAL_PERM
-        // M_1..M_4 (record tables 0-3, contiguous) and M_8
-        wtab[lane] = ld_rec4(rec, kRecShoup + 4u * lane);
-        if (lane < 16u) wtab[64u + lane] = ld_rec4(rec, kRecShoup + 64u * 7u + 4u * lane);
-#else
-        wtab[lane] = ld_rec4(rec, kRecShoup + 64u * ((1u << (lane >> 4)) - 1u) + 4u * (lane & 15u));
-        if (lane < 16u) wtab[64u + lane] = ld_rec4(rec, kRecShoup + 64u * 15u + 4u * lane);
-#endif
-#if NEB_CHUNK_POS
-        {  // the position tables of H^(2^lg)
-            const uint32_t pt = rec_pos_table(lg);
-            wpos[lane] = ld_rec4(rec, pt + 4u * lane);
-            wpos[64u + lane] = ld_rec4(rec, pt + 4u * (64u + lane));
+        if (full) {
+            stage_chunk_tables<true>(rec, ln, 2u, wtab, wpos);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the chunk's groups of 16 packets at 4 lanes, one after another on the staged tables
+            const GhChunk4 gh{wtab, wpos};
+            for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
+                const uint32_t q = g0 + (ln >> 2);
+                const bool valid = q < count;
+                const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+                gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
+            }
+        } else {
+            const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
+            stage_chunk_tables<false>(rec, ln, lg, wtab, wpos);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t q = ln >> lg;
+            const bool valid = q < count;
+            const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+            const GhChunkTree gh{wtab, wpos};
+            gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg);
         }
-#endif
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t q = lane >> lg;
-        const bool valid = q < count;
-        const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-#if NEB_CHUNK_EJ0_LDS
-        gcm_packet_group<OPEN, false>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg, Ej0Lds{&lds.ej0[wave][lane]});
-#else
-        gcm_packet_group<OPEN, false>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, lane, lg);
-#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#if NEB_CHUNK_STATIC
         c = cn;
-#else
-        uint32_t next = nch;
-        if (nch > nwaves) {
-            if (lane == 0u) next = atomicAdd(&ca.counters[kCntWork], 1u);
-            next = nwaves + __builtin_amdgcn_readfirstlane(next);
-        }
-        c = next;
-#endif
     }
 }
 
@@ -1896,7 +1527,7 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
     const bool cs = !open && hdr_from_dst == 2;  // the TX seal with its checksums (tx.hip)
-    if (NEB_SINGLE_TAIL && !NEB_GHASH8 && !d_n && !cs && n <= (uint32_t)NEB_SMALL_BATCH) {
+    if (!d_n && !cs && n <= neb::kSmallBatch) {
         a.tail_slots = neb::kTailAll;
         const uint32_t tgrid = std::min<uint32_t>(
             ((n + neb::kTailPpw - 1u) / neb::kTailPpw + neb::kTailWaves - 1u) / neb::kTailWaves,
@@ -1910,7 +1541,7 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
     const uint32_t slots = neb_gcm_single_slots(n, cu_count, open, hdr_from_dst);
     // a partial last pass (at most n packets; the real count may be on the device) goes to the
     // tail kernel, 16 lanes per packet
-    const bool tail = NEB_SINGLE_TAIL && !NEB_GHASH8 && groups > slots && (d_n || groups % slots);
+    const bool tail = groups > slots && (d_n || groups % slots);
     if (tail) a.tail_slots = slots;
     const dim3 grid(slots / neb::kSingleWaves);
     if (grid.x == 0) return hipSuccess;
@@ -1939,6 +1570,7 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
 }
 
 // Mixed keys: the batch has been regrouped into chunks by neb_sched_build.
+
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
@@ -1947,8 +1579,8 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
     neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
-    // small batch's chunks spread over the CUs; the chunk count is only known on the device:
-    // workgroups past it exit before filling their tables
+    // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
+    // workgroups past them exit before filling their tables. Full chunks first, then the tails.
     const uint32_t bound = max_chunks * (uint32_t)neb::kChunkWaves;
     return open ? launch_grid(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, a, ca)
                 : launch_grid(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, a, ca);

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -93,82 +94,14 @@ bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len) {
 
 namespace {
 
-// Arena span copy across PCIe for the kernel-staged host path: each wave instruction moves 1 KiB of
-// contiguous bytes (64 lanes x 16 B) and every lane has four loads in flight before its stores, so
-// the link carries full-size requests instead of the 64-byte pieces the zero-copy kernels issue.
-// dst and src are 16-byte aligned; the last nbytes % 16 bytes are copied one per lane.
-__global__ __launch_bounds__(256) void span_copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                                        size_t nbytes) {
-    const size_t n16 = nbytes >> 4;
-    const size_t stride = (size_t)gridDim.x * 256;
-    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = s4[i], b = s4[i + stride], c = s4[i + 2 * stride], d = s4[i + 3 * stride];
-        d4[i] = a;
-        d4[i + stride] = b;
-        d4[i + 2 * stride] = c;
-        d4[i + 3 * stride] = d;
-    }
-    for (; i < n16; i += stride) d4[i] = s4[i];
-    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (t < (nbytes & 15)) dst[(n16 << 4) + t] = src[(n16 << 4) + t];
-}
-
-// Two span copies in one launch, the first blocks0 workgroups on the first: a chunk's copy-in and
-// the previous chunk's copy-back, so both PCIe directions carry traffic at once.
-__global__ __launch_bounds__(256) void span_copy2_kernel(uint8_t* __restrict__ dst0, const uint8_t* __restrict__ src0,
-                                                         size_t n0, uint32_t blocks0, uint8_t* __restrict__ dst1,
-                                                         const uint8_t* __restrict__ src1, size_t n1) {
-    const bool first = blockIdx.x < blocks0;
-    uint8_t* dst = first ? dst0 : dst1;
-    const uint8_t* src = first ? src0 : src1;
-    const size_t nbytes = first ? n0 : n1;
-    const size_t nblk = first ? blocks0 : gridDim.x - blocks0, blk = first ? blockIdx.x : blockIdx.x - blocks0;
-    const size_t n16 = nbytes >> 4, stride = nblk * 256;
-    size_t i = blk * 256 + threadIdx.x;
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = s4[i], b = s4[i + stride], c = s4[i + 2 * stride], d = s4[i + 3 * stride];
-        d4[i] = a;
-        d4[i + stride] = b;
-        d4[i + 2 * stride] = c;
-        d4[i + 3 * stride] = d;
-    }
-    for (; i < n16; i += stride) d4[i] = s4[i];
-    const size_t t = blk * 256 + threadIdx.x;
-    if (t < (nbytes & 15)) dst[(n16 << 4) + t] = src[(n16 << 4) + t];
-}
-
-hipError_t span_copy2(uint8_t* dst0, const uint8_t* src0, size_t n0, uint8_t* dst1, const uint8_t* src1, size_t n1,
-                      hipStream_t s) {
-    const size_t b0 = std::min<size_t>(std::max<size_t>(((n0 >> 4) + 255) / 256, 1), 512);
-    const size_t b1 = std::min<size_t>(std::max<size_t>(((n1 >> 4) + 255) / 256, 1), 512);
-    hipLaunchKernelGGL(span_copy2_kernel, dim3((unsigned)(b0 + b1)), dim3(256), 0, s, dst0, src0, n0, (uint32_t)b0,
-                       dst1, src1, n1);
-    return hipGetLastError();
-}
-
-hipError_t span_copy(uint8_t* dst, const uint8_t* src, size_t nbytes, hipStream_t s) {
-    if (!nbytes) return hipSuccess;
-    const size_t blocks = std::min<size_t>(std::max<size_t>(((nbytes >> 4) + 255) / 256, 1), 1024);
-    hipLaunchKernelGGL(span_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, nbytes);
-    return hipGetLastError();
-}
-
-// Host batch path: NEB_HOST_MODE = "zc" (kernels on the mapped arena), "kcopy" (mapped arena staged
-// by span_copy_kernel), "dma" (hipMemcpyAsync staging); NEB_HOST_STAGED=1 is the older name of "dma".
-enum HostMode { kHostZeroCopy, kHostKernelCopy, kHostDma, kHostSplit };
-// Zero-copy is the default: measured on one MI355X (C2 seal+open, 64 Ki x 1300 B) it runs at 28.4
-// GiB/s against 23.9 for DMA staging and 18.1 for span-copy staging.
+// Host batch path: NEB_HOST_MODE = "zc" (the kernels on the mapped arena, the default) or "dma"
+// (hipMemcpyAsync staging); NEB_HOST_STAGED=1 is the older name of "dma". Measured on one MI355X
+// (C2 seal+open, 64 Ki x 1300 B): zero-copy 28.4 GiB/s against 23.9 for DMA staging.
+enum HostMode { kHostZeroCopy, kHostDma };
 HostMode host_mode() {  // read per batch (a few hundred ns), so a process can switch between batches
     if (std::getenv("NEB_HOST_STAGED")) return kHostDma;
     const char* v = std::getenv("NEB_HOST_MODE");
-    if (v && !std::strcmp(v, "kcopy")) return kHostKernelCopy;
     if (v && !std::strcmp(v, "dma")) return kHostDma;
-    if (v && !std::strcmp(v, "split")) return kHostSplit;
     return kHostZeroCopy;
 }
 
@@ -186,6 +119,18 @@ struct TxSpace {
     std::mutex mu;
 };
 
+// Per-packet staging of one thread on one engine: pinned, mapped host memory the kernel reads and
+// writes in place ([desc 64 B | status 64 B | aad | payload + tag]), and the thread's own stream.
+struct PktSlot {
+    hipStream_t stream = nullptr;
+    uint8_t* h = nullptr;
+    size_t cap = 0;
+};
+struct KeyUse {
+    hipStream_t s;
+    hipEvent_t ev;
+};
+
 struct neb_engine {
     int device = 0;
     int cu_count = 0;
@@ -194,11 +139,19 @@ struct neb_engine {
     uint32_t* d_keys = nullptr;
     std::vector<int> slot_alg;  // 0 = free
     std::mutex key_mu;
+    uint64_t gen = 0;  // unique per engine (a thread's cached packet slot names its engine by it)
 
-    std::mutex io_mu;  // per-packet staging
-    uint8_t* h_stage = nullptr;
-    uint8_t* d_stage = nullptr;
-    size_t stage_cap = 0;
+    // Per-packet CipherState calls: one staging slot and stream per calling thread (PktSlot).
+    std::mutex pkt_mu;
+    std::vector<PktSlot*> pkt_slots;
+
+    // Asynchronous batches still queued when a key is destroyed: per key slot, the last
+    // single-key batch the engine launched on each stream, and the last mixed-key batch per
+    // stream (its keys are only known on the device). neb_cipher_destroy waits for those events
+    // only, not for the device.
+    std::mutex use_mu;
+    std::vector<std::vector<KeyUse>> key_use;
+    std::vector<KeyUse> mixed_use;
 
     std::mutex pipe_mu;
     PipeSlot pipe[kPipeStreams];
@@ -251,18 +204,67 @@ static void set_error(const char* where, hipError_t err) {
         }                                           \
     } while (0)
 
-static int ensure_stage(neb_engine* e, size_t bytes) {
-    if (bytes <= e->stage_cap) return NEB_OK;
-    size_t cap = std::max(kStageMin, align_up(bytes, 1 << 16));
-    if (e->h_stage) hipHostFree(e->h_stage);
-    if (e->d_stage) hipFree(e->d_stage);
-    e->h_stage = nullptr;
-    e->d_stage = nullptr;
-    e->stage_cap = 0;
-    HIP_TRY(hipHostMalloc((void**)&e->h_stage, cap, hipHostMallocDefault));
-    HIP_TRY(hipMalloc((void**)&e->d_stage, cap));
-    e->stage_cap = cap;
-    return NEB_OK;
+// The calling thread's packet slot on engine e, with room for `bytes` (created on first use).
+// A thread caches its slots by engine generation: a destroyed engine's slots are never used again,
+// even if a new engine lands at the same address.
+static std::atomic<uint64_t> g_engine_gen{1};
+static PktSlot* pkt_slot(neb_engine* e, size_t bytes) {
+    struct Cached {
+        uint64_t gen;
+        PktSlot* s;
+    };
+    thread_local Cached cache[8] = {};
+    PktSlot* sl = nullptr;
+    for (auto& c : cache)
+        if (c.gen == e->gen) sl = c.s;
+    if (!sl) {
+        sl = new (std::nothrow) PktSlot;
+        if (!sl) return nullptr;
+        if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) {
+            set_error("hipStreamCreateWithFlags", hipGetLastError());
+            delete sl;
+            return nullptr;
+        }
+        {
+            std::lock_guard<std::mutex> g(e->pkt_mu);
+            e->pkt_slots.push_back(sl);
+        }
+        Cached* victim = &cache[0];
+        for (auto& c : cache)
+            if (c.gen == 0) victim = &c;
+        *victim = {e->gen, sl};
+    }
+    if (bytes > sl->cap) {
+        if (sl->h) hipHostFree(sl->h);
+        sl->h = nullptr;
+        sl->cap = 0;
+        const size_t cap = std::max(kStageMin, align_up(bytes, 1 << 16));
+        hipError_t err = hipHostMalloc((void**)&sl->h, cap, hipHostMallocDefault);
+        if (err != hipSuccess) {
+            set_error("hipHostMalloc", err);
+            sl->h = nullptr;
+            return nullptr;
+        }
+        sl->cap = cap;
+    }
+    return sl;
+}
+
+// After an asynchronous batch is enqueued on stream s: remember it for neb_cipher_destroy (the
+// key_hint's slot, or every slot for a mixed-key batch). Events skip the system-scope cache
+// flush (timing-only markers would carry it for nothing).
+static void note_use(neb_engine* e, uint32_t key_hint, hipStream_t s) {
+    std::lock_guard<std::mutex> g(e->use_mu);
+    std::vector<KeyUse>& v = key_hint == NEB_KEYS_MIXED ? e->mixed_use : e->key_use[key_hint];
+    for (KeyUse& u : v)
+        if (u.s == s) {
+            (void)hipEventRecord(u.ev, s);
+            return;
+        }
+    KeyUse u{s, nullptr};
+    if (hipEventCreateWithFlags(&u.ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return;
+    (void)hipEventRecord(u.ev, s);
+    v.push_back(u);
 }
 
 extern "C" {
@@ -313,7 +315,9 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
     e->device = device;
     e->cu_count = cus;
     e->max_keys = max_keys;
+    e->gen = g_engine_gen.fetch_add(1);
     e->slot_alg.assign(max_keys, 0);
+    e->key_use.resize(max_keys);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess ||
         hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess) {
@@ -364,8 +368,14 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
     if (e->zc_desc) hipFree(e->zc_desc);
     if (e->zc_status) hipFree(e->zc_status);
     if (e->d_keys) hipFree(e->d_keys);
-    if (e->h_stage) hipHostFree(e->h_stage);
-    if (e->d_stage) hipFree(e->d_stage);
+    for (PktSlot* sl : e->pkt_slots) {
+        if (sl->stream) { hipStreamSynchronize(sl->stream); hipStreamDestroy(sl->stream); }
+        if (sl->h) hipHostFree(sl->h);
+        delete sl;
+    }
+    for (auto& v : e->key_use)
+        for (KeyUse& u : v) hipEventDestroy(u.ev);
+    for (KeyUse& u : e->mixed_use) hipEventDestroy(u.ev);
     if (e->stream) hipStreamDestroy(e->stream);
     delete e;
     return NEB_OK;
@@ -396,20 +406,25 @@ NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb
     }
     int rc = NEB_OK;
     {
-        std::lock_guard<std::mutex> g(e->io_mu);
+        // the key goes through the calling thread's pinned slot: the setup kernel reads it there
+        // (mapped host memory) on the thread's stream, then the slot's copy is wiped
         hipSetDevice(e->device);
-        rc = ensure_stage(e, 64);
-        if (rc == NEB_OK) {
-            std::memcpy(e->h_stage, key, 32);
+        PktSlot* sl = pkt_slot(e, 64);
+        if (!sl) {
+            rc = NEB_ERR_HIP;
+        } else {
+            std::memcpy(sl->h, key, 32);
             uint32_t* rec = e->d_keys + (size_t)slot * neb::kKeyRecDwords;
-            hipError_t err = hipMemcpyAsync(e->d_stage, e->h_stage, 32, hipMemcpyHostToDevice, e->stream);
-            if (err == hipSuccess) err = hipMemsetAsync(rec, 0, neb::kKeyRecBytes, e->stream);
+            hipError_t err = hipMemsetAsync(rec, 0, neb::kKeyRecBytes, sl->stream);
             if (err == hipSuccess)
-                err = alg == NEB_ALG_AESGCM ? neb_gcm_key_setup(e->d_stage, rec, e->stream)
-                                            : neb_chacha_key_setup(e->d_stage, rec, e->stream);
-            if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
-            std::memset(e->h_stage, 0, 32);
-            if (err != hipSuccess) rc = NEB_ERR_HIP;
+                err = alg == NEB_ALG_AESGCM ? neb_gcm_key_setup(sl->h, rec, sl->stream)
+                                            : neb_chacha_key_setup(sl->h, rec, sl->stream);
+            if (err == hipSuccess) err = hipStreamSynchronize(sl->stream);
+            std::memset(sl->h, 0, 32);
+            if (err != hipSuccess) {
+                set_error("key setup", err);
+                rc = NEB_ERR_HIP;
+            }
         }
     }
     std::lock_guard<std::mutex> g(e->key_mu);
@@ -430,23 +445,36 @@ NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb
 NEB_API int neb_cipher_destroy(neb_cipher* c) {
     if (!c) return NEB_ERR_INVALID;
     neb_engine* e = c->e;
+    const uint32_t slot = c->key_id;
     hipSetDevice(e->device);
-    // Asynchronous batches (neb_seal_batch / neb_open_batch / neb_tx_seal_batch / neb_rx_open_batch)
-    // still queued on caller streams may read this record: the whole device drains first. A
-    // destroy is rare; an event recorded after every launch instead cost 2-4 µs per kernel
-    // (profiles/r2_micro/ab_inflight_events.log).
-    hipDeviceSynchronize();
+    // Asynchronous batches the engine enqueued that may read this record: the last single-key
+    // batch with this key on each stream, and the last mixed-key batch on each stream (note_use).
+    // Only those are waited for — not the device, so another tunnel's batches in flight elsewhere
+    // do not stall a teardown or rekey. The caller stops enqueuing with a key before destroying it.
+    std::vector<hipEvent_t> wait;
     {
-        std::lock_guard<std::mutex> g(e->io_mu);
-        hipMemsetAsync(e->d_keys + (size_t)c->key_id * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, e->stream);
-        hipStreamSynchronize(e->stream);
+        std::lock_guard<std::mutex> g(e->use_mu);
+        for (KeyUse& u : e->key_use[slot]) wait.push_back(u.ev);
+        for (KeyUse& u : e->mixed_use) wait.push_back(u.ev);
+    }
+    for (hipEvent_t ev : wait) (void)hipEventSynchronize(ev);
+    int rc = NEB_OK;
+    PktSlot* sl = pkt_slot(e, 64);
+    if (!sl || hipMemsetAsync(e->d_keys + (size_t)slot * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, sl->stream) !=
+                   hipSuccess ||
+        hipStreamSynchronize(sl->stream) != hipSuccess)
+        rc = NEB_ERR_HIP;
+    {
+        std::lock_guard<std::mutex> g(e->use_mu);
+        for (KeyUse& u : e->key_use[slot]) hipEventDestroy(u.ev);
+        e->key_use[slot].clear();
     }
     {
         std::lock_guard<std::mutex> g(e->key_mu);
-        e->slot_alg[c->key_id] = 0;
+        e->slot_alg[slot] = 0;
     }
     delete c;
-    return NEB_OK;
+    return rc;
 }
 
 NEB_API uint32_t neb_cipher_key_id(const neb_cipher* c) { return c ? c->key_id : NEB_KEYS_MIXED; }
@@ -529,25 +557,33 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                         sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count, s, hdr_from_dst);
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
-        if (err != hipSuccess) sp.dirty = true;
+        if (err != hipSuccess) {
+            // binning passes of this batch may already be queued on s: let them finish before the
+            // next batch clears the counters (sched_reserve's dirty path waits on sp.done only)
+            (void)hipStreamSynchronize(s);
+            sp.dirty = true;
+        }
         return err;
     }
     return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n, e->cu_count,
                             s, hdr_from_dst);
 }
 
-// One packet through the device: [desc | status | aad | payload (+tag)] in one staging buffer.
+// One packet through the device, on the calling thread's own slot and stream (PktSlot): the packet
+// is copied into the slot's pinned, mapped buffer ([desc | status | aad | payload (+tag)]), the
+// batch kernel seals or opens it there in place (zero-copy: no DMA either way) and the result is
+// copied out. Threads never share a slot, so concurrent calls from Nebula's routines run side by
+// side instead of queueing on one lock.
 static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len, const uint8_t* in, size_t in_len,
                       size_t pay_len, uint64_t n, uint8_t* dst, int32_t* st_out) {
     neb_engine* e = c->e;
     const size_t o_desc = 0, o_status = 64, o_aad = 128;
     const size_t o_pay = align_up(o_aad + ad_len, 16);
     const size_t total = o_pay + pay_len + 16;
-    std::lock_guard<std::mutex> g(e->io_mu);
     hipSetDevice(e->device);
-    int rc = ensure_stage(e, total);
-    if (rc != NEB_OK) return rc;
-    uint8_t* h = e->h_stage;
+    PktSlot* sl = pkt_slot(e, total);
+    if (!sl) return NEB_ERR_HIP;
+    uint8_t* h = sl->h;
     neb_desc d{};
     d.src_off = o_pay - o_aad;
     d.dst_off = o_pay - o_aad;
@@ -557,20 +593,18 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
     d.aad_len = (uint32_t)ad_len;
     d.key_id = c->key_id;
     std::memcpy(h + o_desc, &d, sizeof d);
+    *(int32_t*)(h + o_status) = -1;
     if (ad_len) std::memcpy(h + o_aad, ad, ad_len);
     if (in_len) std::memcpy(h + o_pay, in, in_len);
-    hipError_t err = hipMemcpyAsync(e->d_stage, h, o_pay + in_len, hipMemcpyHostToDevice, e->stream);
-    if (err == hipSuccess)
-        err = launch_batch(e, c->alg, open, (const neb_desc*)(e->d_stage + o_desc), 1, e->d_stage + o_aad,
-                           (int32_t*)(e->d_stage + o_status), c->key_id, e->stream);
-    if (err != hipSuccess) set_error("one_packet", err);
-    const size_t out_len = open ? pay_len : pay_len + 16;
-    if (err == hipSuccess) err = hipMemcpyAsync(h + o_status, e->d_stage + o_status, 4, hipMemcpyDeviceToHost, e->stream);
-    if (err == hipSuccess && out_len)
-        err = hipMemcpyAsync(h + o_pay, e->d_stage + o_pay, out_len, hipMemcpyDeviceToHost, e->stream);
-    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
-    if (err != hipSuccess) return NEB_ERR_HIP;
+    hipError_t err = launch_batch(e, c->alg, open, (const neb_desc*)(h + o_desc), 1, h + o_aad,
+                                  (int32_t*)(h + o_status), c->key_id, sl->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(sl->stream);
+    if (err != hipSuccess) {
+        set_error("one_packet", err);
+        return NEB_ERR_HIP;
+    }
     std::memcpy(st_out, h + o_status, 4);
+    const size_t out_len = open ? pay_len : pay_len + 16;
     if (out_len) std::memcpy(dst, h + o_pay, out_len);
     return NEB_OK;
 }
@@ -634,6 +668,7 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
         set_error("batch launch", err);
         return NEB_ERR_HIP;
     }
+    note_use(e, key_hint, s);
     return NEB_OK;
 }
 
@@ -662,6 +697,33 @@ int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_
         return NEB_ERR_HIP;
     }
     return NEB_OK;
+}
+
+// For the submission queue (queue.cpp): a scheduler workspace of its own, and a launch of one
+// staged batch (zero-copy on pinned memory) on the queue's stream.
+void* neb_sched_space_new() { return new (std::nothrow) SchedSpace; }
+void neb_sched_space_free(void* p) {
+    auto* sp = static_cast<SchedSpace*>(p);
+    if (!sp) return;
+    if (sp->done) { hipEventSynchronize(sp->done); hipEventDestroy(sp->done); }
+    if (sp->mem) hipFree(sp->mem);
+    delete sp;
+}
+int neb_launch_on(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n, uint8_t* arena,
+                  int32_t* status, uint32_t key_hint, hipStream_t s, void* sched) {
+    if (n == 0) return NEB_OK;
+    hipSetDevice(e->device);
+    hipError_t err = launch_batch(e, alg, open, desc, n, arena, status, key_hint, s, nullptr,
+                                  static_cast<SchedSpace*>(sched));
+    if (err != hipSuccess) {
+        set_error("queue batch launch", err);
+        return NEB_ERR_HIP;
+    }
+    return NEB_OK;
+}
+int neb_key_alg(neb_engine* e, uint32_t key) {
+    std::lock_guard<std::mutex> g(e->key_mu);
+    return key < e->max_keys ? e->slot_alg[key] : 0;
 }
 
 // True if p is pinned host memory the device addresses at the same pointer (hipHostMalloc).
@@ -707,10 +769,9 @@ static int batch_host_zero_copy(neb_engine* e, int alg, int open, const neb_desc
 // Host-resident batch. A pinned, mapped arena runs zero-copy (above). Any other arena is staged in
 // chunks of kPipeChunkPkts packets rotated over kPipeStreams streams: each chunk's arena span is
 // copied in (hipMemcpyAsync), sealed/opened on the device and copied back, so one chunk's copy-in
-// overlaps another's kernel and another's copy-back. NEB_HOST_MODE=kcopy stages a mapped arena with
-// span_copy_kernel instead (measured slower, kept for the A/B); =dma forces hipMemcpyAsync staging.
-// Every descriptor is checked before anything is copied or launched, in every mode: an invalid batch
-// returns NEB_ERR_INVALID with the arena and the statuses untouched.
+// overlaps another's kernel and another's copy-back. NEB_HOST_MODE=dma forces the staging for a
+// mapped arena too. Every descriptor is checked before anything is copied or launched: an invalid
+// batch returns NEB_ERR_INVALID with the arena and the statuses untouched.
 static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n, uint8_t* arena,
                       size_t arena_len, int32_t* status, uint32_t key_hint) {
     int rc = check_batch(e, alg, key_hint);
@@ -721,26 +782,15 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
     std::lock_guard<std::mutex> g(e->pipe_mu);
     hipSetDevice(e->device);
-    const HostMode mode = host_mode();
     // The kernels' vector fast path tests the absolute address (arena base + offset), so a mapped
     // arena at any byte address runs zero-copy. A staged arena lands in a device buffer with the
     // same alignment modulo 16, so the kernels take the same paths either way.
-    const bool mapped = mode != kHostDma && host_mapped(arena);
-    if (mapped && mode == kHostZeroCopy)
+    if (host_mode() == kHostZeroCopy && host_mapped(arena))
         return batch_host_zero_copy(e, alg, open, desc, n, arena, arena_len, status, key_hint);
-    // mapped arena: copies by span_copy_kernel, whose 16-byte vector copies need an aligned base
-    // (an unaligned one is DMA-staged)
-    const bool kcopy = mapped && mode == kHostKernelCopy && ((uintptr_t)arena & 15) == 0;
-    // split (mapped arena): each chunk's sources (payload, AAD) are DMA-staged into a device buffer
-    // while the kernel stores its outputs straight into the mapped arena, so the copy engine carries
-    // the H2D direction and the kernel's stores the D2H one, and nothing is copied back.
-    const bool split = mapped && mode == kHostSplit;
     for (auto& s : e->pipe) {
         if (!s.stream) {
             HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-            // system-scope release: a split chunk's kernel stores into the mapped arena, which is
-            // non-coherent (L2-cached) host memory by default; the event must make them visible
-            HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventReleaseToSystem));
+            HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
             HIP_TRY(hipMalloc((void**)&s.d_desc, kPipeChunkPkts * sizeof(neb_desc)));
             HIP_TRY(hipMalloc((void**)&s.d_status, kPipeChunkPkts * sizeof(int32_t)));
             HIP_TRY(hipHostMalloc((void**)&s.h_desc, kPipeChunkPkts * sizeof(neb_desc), hipHostMallocDefault));
@@ -752,11 +802,7 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         }
         s.count = 0;
     }
-    // kcopy: every chunk runs on pipe[0]'s stream and chunk k's copy-in shares one launch with chunk
-    // k-1's copy-back (span_copy2), unless their spans overlap; `pend` is the slot whose copy-back
-    // has not been issued yet. DMA staging: one stream per slot, chunks overlap across streams.
-    hipStream_t ks = e->pipe[0].stream;
-    int slot = 0, pend = -1;
+    int slot = 0;
     auto retire = [](PipeSlot& s) -> hipError_t {
         hipError_t err = hipEventSynchronize(s.done);
         if (err != hipSuccess) return err;
@@ -772,21 +818,14 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         for (uint32_t i = 0; i < cnt; i++) {
             const neb_desc& d = desc[begin + i];
             const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
-            if (split) {  // only what the kernel reads is staged
-                lo = std::min({lo, d.src_off, d.aad_off});
-                hi = std::max({hi, d.src_off + pay, d.aad_off + d.aad_len});
-            } else {
-                lo = std::min({lo, d.src_off, d.dst_off, d.aad_off});
-                hi = std::max({hi, d.src_off + pay, d.dst_off + outl, d.aad_off + d.aad_len});
-            }
+            lo = std::min({lo, d.src_off, d.dst_off, d.aad_off});
+            hi = std::max({hi, d.src_off + pay, d.dst_off + outl, d.aad_off + d.aad_len});
         }
         lo &= ~(uint64_t)15;
         // A chunk copies its whole span back, so spans of chunks in flight must not overlap (the
         // descriptors need not be in arena order): retire any other slot whose span intersects.
-        // (kcopy chunks are ordered by their one stream; only the launch shared with `pend` races.)
-        if (!kcopy && !split)
-            for (auto& o : e->pipe)
-                if (&o != &s && o.count && o.lo < hi && lo < o.hi) HIP_TRY(retire(o));
+        for (auto& o : e->pipe)
+            if (&o != &s && o.count && o.lo < hi && lo < o.hi) HIP_TRY(retire(o));
         s.lo = lo;
         s.hi = hi;
         const size_t span = (size_t)(hi - lo);
@@ -800,49 +839,18 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
             neb_desc d = desc[begin + i];
             d.src_off -= lo;
             d.aad_off -= lo;
-            // split: the kernel's d_buf + dst_off must land on the mapped arena (64-bit wrap-around)
-            d.dst_off = split ? (uint64_t)(uintptr_t)(arena + d.dst_off) - (uint64_t)(uintptr_t)s.d_buf : d.dst_off - lo;
+            d.dst_off -= lo;
             s.h_desc[i] = d;
         }
         s.user_status = status;
         s.user_begin = begin;
         s.count = cnt;
-        if (kcopy) {
-            HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, cnt * sizeof(neb_desc), hipMemcpyHostToDevice, ks));
-            if (pend >= 0) {
-                PipeSlot& p = e->pipe[pend];
-                const size_t pspan = (size_t)(p.hi - p.lo);
-                if (p.lo < hi && lo < p.hi) {  // overlapping spans: copy back first, then copy in
-                    HIP_TRY(span_copy(arena + p.lo, p.d_buf, pspan, ks));
-                    HIP_TRY(span_copy(s.d_buf, arena + lo, span, ks));
-                } else {
-                    HIP_TRY(span_copy2(s.d_buf, arena + lo, span, arena + p.lo, p.d_buf, pspan, ks));
-                }
-                HIP_TRY(hipEventRecord(p.done, ks));
-            } else {
-                HIP_TRY(span_copy(s.d_buf, arena + lo, span, ks));
-            }
-            HIP_TRY(launch_batch(e, alg, open, s.d_desc, cnt, s.d_buf, s.d_status, key_hint, ks, nullptr, s.sched));
-            HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, ks));
-            pend = slot;
-            continue;
-        }
         HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s.stream));
         HIP_TRY(hipMemcpyAsync(s.d_buf, arena + lo, span, hipMemcpyHostToDevice, s.stream));
         HIP_TRY(launch_batch(e, alg, open, s.d_desc, cnt, s.d_buf, s.d_status, key_hint, s.stream, nullptr, s.sched));
-        if (split) {
-            HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
-            HIP_TRY(hipEventRecord(s.done, s.stream));
-            continue;
-        }
         HIP_TRY(hipMemcpyAsync(arena + lo, s.d_buf, span, hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipEventRecord(s.done, s.stream));
-    }
-    if (pend >= 0) {
-        PipeSlot& p = e->pipe[pend];
-        HIP_TRY(span_copy(arena + p.lo, p.d_buf, (size_t)(p.hi - p.lo), ks));
-        HIP_TRY(hipEventRecord(p.done, ks));
     }
     for (auto& s : e->pipe)
         if (s.count) HIP_TRY(retire(s));
@@ -1006,6 +1014,7 @@ NEB_API int neb_tx_seal_batch(neb_engine* e, int alg, neb_tx_tunnel* d_tunnels, 
     std::lock_guard<std::mutex> g(e->tx.mu);
     rc = tx_run(e, alg, d_tunnels, ntunnels, d_packets, npackets, d_in, d_out, out_cap, d_wires, d_wire_status,
                 max_wires, d_nwires, d_packet_status, key_hint, s);
+    if (rc == NEB_OK) note_use(e, key_hint, s);
     return rc;
 }
 

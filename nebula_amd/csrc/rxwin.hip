@@ -430,6 +430,14 @@ __global__ void rx_gather_desc_kernel(const neb_desc* __restrict__ desc, RxDevWs
     if (j < *ws.nsub) ws.sub_desc[j] = desc[ws.sub_map[j]];
 }
 
+__global__ __launch_bounds__(256) void rx_span_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                      const neb_span* __restrict__ spans, uint32_t n) {
+    const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (j >= n) return;
+    const neb_span sp = spans[j];
+    for (uint32_t k = lane; k < sp.len; k += 64u) dst[sp.dst + k] = src ? src[sp.src + k] : (uint8_t)0;
+}
+
 __device__ __forceinline__ bool rx_fast(uint32_t fl) { return (fl & kRxTouched) && !(fl & (kRxRisky | kRxSlow)); }
 
 // Per admitted packet (compacted order): its tag verdict into its status (a failure sends the
@@ -625,6 +633,13 @@ extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const
 
 // Phase 3: verdicts and the admitted counters' bits, then the parallel finish of every window
 // whose admitted packets all verified.
+extern "C" hipError_t neb_rxdev_spans(const uint8_t* src, uint8_t* dst, const neb_span* d_spans, uint32_t n,
+                                      hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(neb::rx_span_kernel, dim3((n + 3u) / 4u), dim3(256), 0, s, src, dst, d_spans, n);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const RxDevWin* win, const RxDevWs* ws, int32_t* d_status,
                                        hipStream_t s) {
     hipLaunchKernelGGL(neb::rx_settle_kernel, rx_grid(n), dim3(256), 0, s, *win, *ws, d_status);

@@ -128,5 +128,15 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const neb::RxDevWin* win,
                                      const neb::RxDevWs* ws, int32_t* d_status, hipStream_t s);
 extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
+// Byte spans between two device buffers, one wave per span (the exact receive pass's speculative
+// opens: packets copied out of the arena into a scratch buffer, plaintext copied back for the ones
+// the windows accept, zeros for the ones that pass their window but fail their tag). src == NULL
+// writes zeros.
+struct neb_span {
+    uint64_t src, dst;
+    uint32_t len, pad;
+};
+extern "C" hipError_t neb_rxdev_spans(const uint8_t* src, uint8_t* dst, const neb_span* d_spans, uint32_t n,
+                                      hipStream_t s);
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const neb::RxDevWin* win, const neb::RxDevWs* ws,
                                        int32_t* d_status, hipStream_t s);

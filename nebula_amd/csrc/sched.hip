@@ -46,15 +46,16 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t c = b < nb ? ws.hist[b] : 0u;
     if (c) ws.hist[b] = 0;  // clear for the next batch
     const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
-    const uint32_t nwide = NEB_WIDE_CHUNKS ? c / kWidePkts : 0u;
-    const uint32_t rest = c - nwide * kWidePkts;
-    const uint32_t nfull = rest / kChunkPkts, tail = rest % kChunkPkts;
+    const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
     const uint32_t lg = tail ? sched_tail_lg(tail, cls) : 2u;
-    // chunks at 4 lanes per packet (the long ones) go to the front, the short tails to the back:
-    // the crypto kernel takes them in that order. Front <= n/16 + bins, back <= bins and
-    // front + back <= n/16 + min(n, bins): the ranges never meet inside max_chunks
-    // (sched_max_chunks).
-    const uint32_t nfront = nwide + nfull + (tail && lg == 2u ? 1u : 0u), nback = tail && lg != 2u ? 1u : 0u;
+    // the bin's first `fpk` packets run in groups at 4 lanes per packet (a 9-15 packet tail is a
+    // partial group), packed sched_groups(cls) groups to a front chunk; a tail at 8 or 16 lanes is
+    // one back chunk. The crypto kernels take the front chunks, then the back ones. Front <= n/16 +
+    // bins, back <= bins and front + back <= n/16 + min(n, bins): the ranges never meet inside
+    // max_chunks (sched_max_chunks).
+    const uint32_t fpk = nfull * kChunkPkts + (tail && lg == 2u ? tail : 0u);
+    const uint32_t cpk = sched_groups(cls) * kChunkPkts;  // packets per front chunk
+    const uint32_t nfront = (fpk + cpk - 1u) / cpk, nback = tail && lg != 2u ? 1u : 0u;
     uint32_t off_p, off_f, off_b, tot_p, tot_f, tot_b;
     Scan(tmp).ExclusiveSum(c, off_p, tot_p);
     __syncthreads();
@@ -70,20 +71,13 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     if (c == 0u) return;
     const uint32_t base = wg_base[0] + off_p;
     ws.base[b] = base;
-    const uint32_t cw = wg_base[1] + off_f;
-    for (uint32_t j = 0; j < nwide && cw + j < ws.max_chunks; j++)
-        ws.chunks[cw + j] = make_uint4(base + j * kWidePkts, kWidePkts, key, cls);  // lg 0
-    const uint32_t cf = cw + nwide, pbase = base + nwide * kWidePkts;
-    for (uint32_t j = 0; j < nfull && cf + j < ws.max_chunks; j++)
-        ws.chunks[cf + j] = make_uint4(pbase + j * kChunkPkts, kChunkPkts, key, cls | (2u << kChunkLgShift));
-    if (tail) {
-        const uint4 ch = make_uint4(pbase + nfull * kChunkPkts, tail, key, cls | (lg << kChunkLgShift));
-        if (lg == 2u) {
-            if (cf + nfull < ws.max_chunks) ws.chunks[cf + nfull] = ch;
-        } else {
-            const uint32_t t = wg_base[2] + off_b;
-            if (t < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - t] = ch;
-        }
+    const uint32_t cf = wg_base[1] + off_f;
+    for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
+        ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));
+    if (nback) {
+        const uint32_t t = wg_base[2] + off_b;
+        if (t < ws.max_chunks)
+            ws.chunks[ws.max_chunks - 1u - t] = make_uint4(base + fpk, tail, key, cls | (lg << kChunkLgShift));
     }
 }
 

@@ -15,37 +15,31 @@
 
 namespace neb {
 
-constexpr uint32_t kChunkPkts = 16;   // packets per full chunk (4 lanes each)
+constexpr uint32_t kChunkPkts = 16;   // packets per packet group at 4 lanes per packet
 constexpr uint32_t kSizeClasses = 8;  // round-count classes at 4 lanes per packet: 1, 2, 3-4, 5-8, 9-16, 17-32, 33-64, 65+
 
-// A bin of c packets becomes c / 16 full chunks of 16 packets at 4 lanes per packet, and one tail
-// chunk of the c mod 16 others at 2^lg lanes per packet: lg 4 (16 lanes) for up to 4 packets, 3
-// for up to 8, else 2 — capped for short packets so that no lane idles on a block that does not
-// exist (size class 0: <= 4 blocks, lg 2; class 1: <= 8 blocks, lg 3). A wave then runs a tail of
-// 1-4 packets in a quarter of the rounds instead of leaving 48-60 of its lanes idle.
+// A bin of c packets becomes c / 16 full groups of 16 packets at 4 lanes per packet, and one tail
+// of the c mod 16 others at 2^lg lanes per packet: lg 4 (16 lanes) for up to 4 packets, 3 for up
+// to 8, else 2 — capped for short packets so that no lane idles on a block that does not exist
+// (size class 0: <= 4 blocks, lg 2; class 1: <= 8 blocks, lg 3). A wave then runs a tail of 1-4
+// packets in a quarter of the rounds instead of leaving 48-60 of its lanes idle.
+// Groups at 4 lanes (the full ones, and a tail of 9-15 packets) are packed into "front" chunks of
+// up to sched_groups(cls) groups: one wave runs a chunk's groups one after another on one staging
+// of the key's tables and round keys, so short packets (IMIX 90 B: 2 rounds per group) do not pay
+// the staging per 16 packets. Tails at 8 or 16 lanes are "back" chunks of their own.
 constexpr uint32_t kChunkLgShift = 8;  // chunk.w = size class | lg << kChunkLgShift
-// Wide chunks: a bin's first c / 64 x 64 packets run at one lane per packet (lg 0, Horner stride H,
-// position tables of H). Its GHASH final is one multiply per packet instead of the 4-lane tree's
-// 3 per lane, and a chunk carries 4x the packets for one staging of the key's tables: for a
-// 90-B packet 9 multiplies instead of 20. Off: C5 step 1.67 -> 1.71 ms with it (A/B,
-// profiles/r2_micro/ab_wide_chunks.log) — at one lane per packet every payload load instruction
-// touches 64 different cache lines.
-#ifndef NEB_WIDE_CHUNKS
-#define NEB_WIDE_CHUNKS 0
-#endif
-constexpr uint32_t kWidePkts = 64;
 __host__ __device__ inline uint32_t sched_tail_lg(uint32_t count, uint32_t cls) {
     const uint32_t fit = count <= 4u ? 4u : (count <= 8u ? 3u : 2u);
     const uint32_t size = cls == 0u ? 2u : (cls == 1u ? 3u : 4u);
-#ifdef NEB_TAIL_LG_MAX  // ablation: cap the tail chunks' lanes per packet
-    if (fit > NEB_TAIL_LG_MAX) return NEB_TAIL_LG_MAX;
-#endif
     return fit < size ? fit : size;
 }
+// groups of 16 packets per front chunk: about 8 rounds of work per chunk for the short classes
+__host__ __device__ inline uint32_t sched_groups(uint32_t cls) { return cls >= 3u ? 1u : 8u >> cls; }
+constexpr uint32_t kMaxChunkPkts = 8u * kChunkPkts;
 
 // counters[] slots
 constexpr uint32_t kCntPackets = 0;      // cursor into sorted[]
-constexpr uint32_t kCntFrontChunks = 1;  // chunks at 4 lanes per packet (full or 9-15 packets), chunks[0, F)
+constexpr uint32_t kCntFrontChunks = 1;  // chunks of groups at 4 lanes per packet, chunks[0, F)
 constexpr uint32_t kCntBackChunks = 2;   // tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
 constexpr uint32_t kCntWork = 3;         // the crypto kernel's chunk cursor (front chunks first)
 constexpr uint32_t kSchedCounters = 4;
@@ -58,7 +52,7 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
     uint32_t* binof;      // [n] bin of each packet
     uint32_t* binpos;     // [n] rank of each packet within its bin (the histogram atomic's return)
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
-    uint4* chunks;        // [max_chunks] {start in sorted, count, key_id, size class | lg << 8}
+    uint4* chunks;        // [max_chunks] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
     uint32_t max_chunks;
 };
 

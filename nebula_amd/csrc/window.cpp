@@ -227,18 +227,28 @@ struct WindowCore {
 // The exact receive order for some windows' packet runs: Check → tag verdict → Update, packet
 // after packet in arrival order (connection_state.go:99-119). A packet not opened yet that its
 // window now accepts — an earlier copy of it failed its tag, or a forged counter further ahead held
-// it back in the simulation — stops its window there: the rest of that window's run is simulated
-// again from the real state (every tag assumed to verify), and all stopped windows' admitted
-// packets are opened in one batch (open_fn). A forged packet then costs one more round, never one
-// open per packet behind it. Rounds release the windows' locks; a packet the simulation admits is
-// never refused by the real pass (the simulation applies a superset of the real updates), barring
-// another thread moving the window meanwhile.
+// it back in the simulation — stops its window there, and the stopped windows' remaining packets
+// are opened in one more batch:
+//   * first extra round: the rest of each stopped window's run is simulated again from the real
+//     state (tags already known to fail skipped, unknown ones assumed to verify) and what the
+//     simulation admits is opened in place (the simulation applies a superset of the real
+//     updates, so the real pass never refuses such a packet, barring another thread moving the
+//     window meanwhile);
+//   * any later round: every packet still unopened in the stopped runs is verified speculatively,
+//     out of place (spec_fn: plaintext into a scratch copy, the arena untouched); the real pass
+//     then knows every verdict and finishes without stopping. The packets it accepts get their
+//     plaintext copied into the arena (*commit), those that pass their window but fail their tag
+//     get their payload zeroed (*zero), as an in-place open would, and refused ones stay untouched.
+// Interleaved forgeries (F1, P1, F2, P2, ...: each forged far-ahead counter holds back the genuine
+// packets after it) therefore cost at most two extra batches, not one per forgery.
+// opened[i]: 0 = not yet, 1 = opened in place, 2 = verified speculatively.
 struct ExactRun {
     uint32_t w, k0, k1;  // window, run positions [k0, k1)
 };
-template <class Ctr, class Pkt, class WithWin, class OpenFn, class Par>
+template <class Ctr, class Pkt, class WithWin, class OpenFn, class SpecFn, class Par>
 int exact_rounds(const std::vector<ExactRun>& runs, uint32_t max_groups, Ctr&& ctr, Pkt&& pkt, uint8_t* opened,
-                 const int32_t* verd, int32_t* status, WithWin&& with_window, OpenFn&& open_fn, Par&& par) {
+                 int32_t* verd, int32_t* status, WithWin&& with_window, OpenFn&& open_fn, SpecFn&& spec_fn,
+                 Par&& par, std::vector<uint32_t>* commit, std::vector<uint32_t>* zero) {
     const bool stats = std::getenv("NEB_RX_STATS") != nullptr;  // rounds and opens to stderr (per call)
     uint32_t rounds = 0, extra_opens = 0, extra_pkts = 0;
     std::vector<uint32_t> pos(runs.size());
@@ -247,11 +257,14 @@ int exact_rounds(const std::vector<ExactRun>& runs, uint32_t max_groups, Ctr&& c
         pos[r] = runs[r].k0;
         active[r] = (uint32_t)r;
     }
+    const uint32_t ng = std::max(1u, std::min(max_groups, (uint32_t)runs.size()));
+    std::vector<std::vector<uint32_t>> cm(ng), zr(ng);  // per group: packets to commit / zero
     while (!active.empty()) {
-        const uint32_t ng = std::max(1u, std::min(max_groups, (uint32_t)active.size()));
-        std::vector<std::vector<uint32_t>> want(ng);
-        par(ng, [&](uint32_t gi) {
-            const size_t a0 = active.size() * gi / ng, a1 = active.size() * (gi + 1) / ng;
+        const uint32_t na = std::max(1u, std::min(ng, (uint32_t)active.size()));
+        const bool speculative = extra_opens >= 1;  // the second extra round verifies everything left
+        std::vector<std::vector<uint32_t>> want(na);
+        par(na, [&](uint32_t gi) {
+            const size_t a0 = active.size() * gi / na, a1 = active.size() * (gi + 1) / na;
             for (size_t a = a0; a < a1; a++) {
                 const uint32_t r = active[a];
                 const ExactRun& R = runs[r];
@@ -265,19 +278,30 @@ int exact_rounds(const std::vector<ExactRun>& runs, uint32_t max_groups, Ctr&& c
                             continue;
                         }
                         if (!opened[i]) {
+                            if (speculative) {
+                                for (uint32_t k2 = k; k2 < R.k1; k2++)
+                                    if (!opened[pkt(k2)]) want[gi].push_back(pkt(k2));
+                                break;
+                            }
                             WindowCore sim = core;
-                            for (uint32_t k2 = k; k2 < R.k1; k2++)
+                            for (uint32_t k2 = k; k2 < R.k1; k2++) {
+                                const uint32_t i2 = pkt(k2);
+                                if (opened[i2] && verd[i2] != NEB_STATUS_OK) continue;  // known to fail
                                 if (sim.check(ctr(k2))) {
                                     sim.update(ctr(k2));
-                                    if (!opened[pkt(k2)]) want[gi].push_back(pkt(k2));
+                                    if (!opened[i2]) want[gi].push_back(i2);
                                 }
+                            }
                             break;
                         }
                         if (verd[i] != NEB_STATUS_OK) {
                             status[i] = verd[i];
+                            if (opened[i] == 2 && verd[i] == NEB_STATUS_AUTH_FAILED) zr[gi].push_back(i);
                             continue;
                         }
-                        status[i] = core.update(c) ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
+                        const bool ok = core.update(c);
+                        status[i] = ok ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
+                        if (ok && opened[i] == 2) cm[gi].push_back(i);
                     }
                     pos[r] = k;
                 });
@@ -288,13 +312,18 @@ int exact_rounds(const std::vector<ExactRun>& runs, uint32_t max_groups, Ctr&& c
         for (uint32_t r : active)
             if (pos[r] < runs[r].k1) next.push_back(r);
         if (!all.empty()) {
-            const int rc = open_fn(all);  // sets opened[] and the verdicts of these packets
+            // sets opened[] (1 in place, 2 speculative) and the verdicts of these packets
+            const int rc = speculative ? spec_fn(all) : open_fn(all);
             if (rc != NEB_OK) return rc;
             extra_opens++;
             extra_pkts += (uint32_t)all.size();
         }
         active.swap(next);
         rounds++;
+    }
+    for (uint32_t g = 0; g < ng; g++) {
+        commit->insert(commit->end(), cm[g].begin(), cm[g].end());
+        zero->insert(zero->end(), zr[g].begin(), zr[g].end());
     }
     if (stats)
         std::fprintf(stderr, "rx exact: %zu windows, %u rounds, %u extra opens of %u packets\n", runs.size(), rounds,
@@ -513,6 +542,17 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
         }
     }
     const auto td = now();
+    // The verdicts are copied out of the staging statuses before the pipeline is released: gst is
+    // the engine's shared pinned buffer, which the next receive call on this engine (another
+    // thread) overwrites, or frees and reallocates for a larger batch, as soon as it holds rx.mu.
+    std::vector<uint8_t> opened(n, 0);
+    std::vector<int32_t> verd(n, NEB_STATUS_BAD_KEY);
+    if (rc == NEB_OK)
+        for (uint32_t i = 0; i < n; i++)
+            if (plan[i] == kToGpu) {
+                opened[i] = 1;
+                verd[i] = gst[sub_of[i]];
+            }
     if (piped) neb_rx_pipe_end(e);
     if (rc != NEB_OK) return rc;
     const auto t2 = now();
@@ -520,16 +560,14 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
     // 3. the real windows, each in arrival order: Check → tag verdict → Update (exact_rounds: a
     //    packet held back that its window accepts is opened with the rest of its window's run)
     for (uint32_t k = start[nwindows]; k < start[nwindows + 1]; k++) status[order[k]] = NEB_STATUS_BAD_KEY;
-    std::vector<uint8_t> opened(n, 0);
-    std::vector<int32_t> verd(n, NEB_STATUS_BAD_KEY);
-    for (uint32_t i = 0; i < n; i++)
-        if (plan[i] == kToGpu) {
-            opened[i] = 1;
-            verd[i] = gst[sub_of[i]];
-        }
     std::vector<ExactRun> runs;
     for (uint32_t g = 0; g < nwindows; g++)
         if (start[g] != start[g + 1]) runs.push_back({g, start[g], start[g + 1]});
+    // speculative verifications (exact_rounds' later rounds): each packet's AAD and ciphertext+tag
+    // copied into a private arena and opened there; pt_at[i] = its plaintext's offset in it
+    std::vector<uint8_t> spec;
+    std::vector<uint64_t> pt_at;
+    std::vector<uint32_t> commit, zero;
     rc = exact_rounds(
         runs, nwg, [&](uint32_t k) { return desc[order[k]].counter; }, [&](uint32_t k) { return order[k]; },
         opened.data(), verd.data(), status,
@@ -550,7 +588,39 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
             }
             return NEB_OK;
         },
-        [&](uint32_t cnt, auto&& fn) { pool.run(cnt, fn); });
+        [&](const std::vector<uint32_t>& pk) -> int {
+            std::vector<neb_desc> ds(pk.size());
+            size_t total = 0;
+            for (uint32_t i : pk) total += (((size_t)desc[i].aad_len + 15) & ~(size_t)15) + desc[i].len + 16 + 16;
+            spec.assign(total, 0);
+            pt_at.assign(n, 0);
+            size_t off = 0;
+            for (size_t j = 0; j < pk.size(); j++) {
+                const neb_desc& d = desc[pk[j]];
+                neb_desc s2 = d;
+                s2.aad_off = off;
+                std::memcpy(spec.data() + off, arena + d.aad_off, d.aad_len);
+                off += ((size_t)d.aad_len + 15) & ~(size_t)15;
+                s2.src_off = s2.dst_off = off;
+                std::memcpy(spec.data() + off, arena + d.src_off, (size_t)d.len + 16);
+                pt_at[pk[j]] = off;
+                off += (((size_t)d.len + 16) + 15) & ~(size_t)15;
+                ds[j] = s2;
+            }
+            std::vector<int32_t> st(pk.size(), NEB_STATUS_BAD_KEY);
+            const int r = neb_open_batch_host(e, alg, ds.data(), (uint32_t)ds.size(), spec.data(), spec.size(),
+                                              st.data(), key_hint);
+            if (r != NEB_OK) return r;
+            for (size_t j = 0; j < pk.size(); j++) {
+                opened[pk[j]] = 2;
+                verd[pk[j]] = st[j];
+            }
+            return NEB_OK;
+        },
+        [&](uint32_t cnt, auto&& fn) { pool.run(cnt, fn); }, &commit, &zero);
+    if (rc != NEB_OK) return rc;
+    for (uint32_t i : commit) std::memcpy(arena + desc[i].dst_off, spec.data() + pt_at[i], desc[i].len);
+    for (uint32_t i : zero) std::memset(arena + desc[i].dst_off, 0, desc[i].len);
     if (rc != NEB_OK) return rc;
     if (prof)
         std::fprintf(stderr,
@@ -667,8 +737,9 @@ NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
     if (!d) return NEB_ERR_INVALID;
     hipSetDevice(neb_engine_device_of(d->e));
     {
+        // neb_rx_open_batch returns only once its stream has run the batch, and holds d->mu
+        // throughout: with the lock taken, nothing of this window set is in flight
         std::lock_guard<std::mutex> g(d->mu);
-        hipDeviceSynchronize();
         if (d->ws_mem) hipFree(d->ws_mem);
         if (d->mem) hipFree(d->mem);
         if (d->h_host) hipHostFree(d->h_host);
@@ -807,10 +878,27 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
         return dw_read(d, w, cores[core_of[w]]);
     });
     if (rc != NEB_OK) return rc;
+    // speculative verifications: packets copied into a device scratch arena and opened there
+    uint8_t* d_spec = nullptr;
+    std::vector<neb_desc> h_desc(n);
+    std::vector<uint64_t> pt_at;
+    std::vector<uint32_t> commit, zero;
+    RX_HIP(hipMemcpyAsync(h_desc.data(), d_desc, (size_t)n * sizeof(neb_desc), hipMemcpyDeviceToHost, s));
+    RX_HIP(hipStreamSynchronize(s));
+    auto run_spans = [&](const uint8_t* src, uint8_t* dst, const std::vector<neb_span>& sp) -> int {
+        if (sp.empty()) return NEB_OK;
+        neb_span* d_sp = nullptr;
+        RX_HIP(hipMalloc((void**)&d_sp, sp.size() * sizeof(neb_span)));
+        hipError_t err = hipMemcpyAsync(d_sp, sp.data(), sp.size() * sizeof(neb_span), hipMemcpyHostToDevice, s);
+        if (err == hipSuccess) err = neb_rxdev_spans(src, dst, d_sp, (uint32_t)sp.size(), s);
+        if (err == hipSuccess) err = hipStreamSynchronize(s);
+        hipFree(d_sp);
+        return err == hipSuccess ? NEB_OK : NEB_ERR_HIP;
+    };
     rc = exact_rounds(
         runs, 1, [&](uint32_t k) { return run_c[k]; }, [&](uint32_t k) { return run_i[k]; }, adm.data(),
         verdict.data(), status.data(), [&](uint32_t w, auto&& fn) { fn(cores[core_of[w]]); },
-        [&](const std::vector<uint32_t>& pk) -> int {  // one device open of these packets
+        [&](const std::vector<uint32_t>& pk) -> int {  // one device open of these packets, in place
             const uint32_t cnt = (uint32_t)pk.size();
             RX_HIP(hipMemcpyAsync(ws.sub_map, pk.data(), (size_t)cnt * 4, hipMemcpyHostToDevice, s));
             RX_HIP(hipMemcpyAsync(ws.nsub, &cnt, 4, hipMemcpyHostToDevice, s));
@@ -826,9 +914,64 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
             }
             return NEB_OK;
         },
+        [&](const std::vector<uint32_t>& pk) -> int {  // out of place, into a scratch arena
+            const uint32_t cnt = (uint32_t)pk.size();
+            std::vector<neb_span> sp;
+            std::vector<neb_desc> ds(cnt);
+            pt_at.assign(n, 0);
+            uint64_t off = 0;
+            for (uint32_t j = 0; j < cnt; j++) {
+                const neb_desc& dd = h_desc[pk[j]];
+                neb_desc s2 = dd;
+                s2.aad_off = off;
+                sp.push_back({dd.aad_off, off, dd.aad_len, 0});
+                off += ((uint64_t)dd.aad_len + 15) & ~15ull;
+                s2.src_off = s2.dst_off = off;
+                sp.push_back({dd.src_off, off, dd.len + 16u, 0});
+                pt_at[pk[j]] = off;
+                off += ((uint64_t)dd.len + 16 + 15) & ~15ull;
+                ds[j] = s2;
+            }
+            if (d_spec) hipFree(d_spec);
+            d_spec = nullptr;
+            RX_HIP(hipMalloc((void**)&d_spec, off + 16));
+            int r = run_spans(d_arena, d_spec, sp);
+            if (r != NEB_OK) return r;
+            neb_desc* d_ds = nullptr;
+            int32_t* d_st = nullptr;
+            RX_HIP(hipMalloc((void**)&d_ds, (size_t)cnt * sizeof(neb_desc)));
+            if (hipMalloc((void**)&d_st, (size_t)cnt * 4) != hipSuccess) {
+                hipFree(d_ds);
+                return NEB_ERR_HIP;
+            }
+            std::vector<int32_t> st(cnt, NEB_STATUS_BAD_KEY);
+            hipError_t err = hipMemcpyAsync(d_ds, ds.data(), (size_t)cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s);
+            r = err == hipSuccess ? neb_open_batch_count(e, alg, d_ds, cnt, nullptr, d_spec, d_st, key_hint, s)
+                                  : NEB_ERR_HIP;
+            if (r == NEB_OK && (hipMemcpyAsync(st.data(), d_st, (size_t)cnt * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                                hipStreamSynchronize(s) != hipSuccess))
+                r = NEB_ERR_HIP;
+            hipFree(d_ds);
+            hipFree(d_st);
+            if (r != NEB_OK) return r;
+            for (uint32_t j = 0; j < cnt; j++) {
+                adm[pk[j]] = 2;
+                verdict[pk[j]] = st[j];
+            }
+            return NEB_OK;
+        },
         [](uint32_t cnt, auto&& fn) {
             for (uint32_t j = 0; j < cnt; j++) fn(j);
-        });
+        },
+        &commit, &zero);
+    if (rc == NEB_OK && (!commit.empty() || !zero.empty())) {
+        std::vector<neb_span> back, zsp;
+        for (uint32_t i : commit) back.push_back({pt_at[i], h_desc[i].dst_off, h_desc[i].len, 0});
+        for (uint32_t i : zero) zsp.push_back({0, h_desc[i].dst_off, h_desc[i].len, 0});
+        rc = run_spans(d_spec, d_arena, back);
+        if (rc == NEB_OK) rc = run_spans(nullptr, d_arena, zsp);
+    }
+    if (d_spec) hipFree(d_spec);
     if (rc != NEB_OK) return rc;
     for (size_t r = 0; r < runs.size(); r++)
         if ((rc = dw_write(d, runs[r].w, cores[r])) != NEB_OK) return rc;

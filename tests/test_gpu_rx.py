@@ -284,6 +284,38 @@ def test_rx_forged_far_counter_costs_one_round(engine, oracle_mod, capfd, device
     assert rounds <= 3 and opens <= 2, lines[-1]
 
 
+@pytest.mark.parametrize("order", ["increasing", "decreasing"])
+@pytest.mark.parametrize("device", [False, True])
+def test_rx_interleaved_forgeries_bounded_rounds(engine, oracle_mod, capfd, device, order):
+    """Forged packets with counters far ahead, each followed by a run of genuine ones (F1, P.., F2,
+    P.., ...): every forgery holds back the genuine packets after it in the simulation. The exact
+    pass must still finish in at most two extra batches (the second verifies everything left out of
+    place), with results identical to the sequential loop: refused packets untouched, accepted ones
+    decrypted, forged ones that pass their window zeroed."""
+    arr, nxt = [], 3
+    for m in range(40):
+        far = 10**6 + (m if order == "increasing" else 40 - m) * 10**5
+        arr.append((0, far, True))
+        for _ in range(8):
+            arr.append((0, nxt, False))
+            nxt += 1
+        if m % 7 == 3:
+            arr.append((0, nxt - 2, False))  # an in-batch replay too
+    arr.append((1, 3, False))
+    os.environ["NEB_RX_STATS"] = "1"
+    try:
+        _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=2, window_len=8192, seed=8, lens=[0, 16, 100],
+             device=device)
+    finally:
+        os.environ.pop("NEB_RX_STATS", None)
+    err = capfd.readouterr().err
+    lines = [ln for ln in err.splitlines() if ln.startswith("rx exact:")]
+    assert lines, err
+    import re
+    rounds, opens = map(int, re.search(r"(\d+) rounds, (\d+) extra opens", lines[-1]).groups())
+    assert rounds <= 3 and opens <= 2, lines[-1]
+
+
 def test_rx_batch_invalid_descriptor_touches_nothing(engine, oracle_mod):
     """A receive batch with a descriptor whose offset wraps around 2^64 is refused before any
     window moves or any packet is opened."""
@@ -430,3 +462,63 @@ def test_rx_device_batches_one_and_many_windows(engine, oracle_mod, strict):
             dw.destroy()
         for c in ciphers.values():
             c.destroy()
+
+
+def test_rx_concurrent_receives_on_one_engine(engine, oracle_mod):
+    """Two threads receive on one engine at once (Nebula's `routines` listenOut loops share one
+    engine): pinned arenas, so both take the piped zero-copy path through the engine's shared
+    staging buffers, and the second batch is larger, so its call reallocates them. Every call's
+    statuses, arena bytes and windows equal the sequential oracle's (the verdicts are copied out of
+    the shared staging before it is released)."""
+    import threading
+
+    import replay_oracle as R
+    from nebula_amd.batch import PinnedBuffer
+    from nebula_amd.connection_state import Bits, rx_open_batch
+    from nebula_amd.noiseutil import CipherAESGCM
+
+    rng = random.Random(21)
+    jobs = []
+    for j, n in enumerate([1500, 6000, 2500, 9000]):
+        keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(2)]
+        arr = _random_arrivals(random.Random(100 + j), n, 2, 0.03)
+        arena, desc, pts = _build(oracle_mod, L.ALG_AESGCM, keys, arr, 30 + j, lens=[0, 16, 100, 576])
+        st, exp, owins = _expected(oracle_mod, R, L.ALG_AESGCM, keys, arr, arena, pts, 1024, {0: 2, 1: 2}, {0, 1})
+        ciphers = [CipherAESGCM.Cipher(engine, k) for k in keys]
+        buf = PinnedBuffer(arena.nbytes)
+        buf.array[:] = arena
+        wins = [None] * engine.max_keys
+        ew = []
+        for t, c in enumerate(ciphers):
+            w = Bits(1024)
+            w.Update(1)
+            w.Update(2)
+            wins[c.key_id] = w
+            ew.append(w)
+        d = desc.copy()
+        d["key_id"] = [ciphers[int(t)].key_id for t in desc["key_id"]]
+        jobs.append(dict(d=d, buf=buf, wins=wins, ew=ew, st=st, exp=exp, owins=owins, ciphers=ciphers))
+    results = [None] * len(jobs)
+
+    def work(j):
+        jb = jobs[j]
+        results[j] = rx_open_batch(engine, L.ALG_AESGCM, jb["wins"], jb["d"], jb["buf"].array)
+
+    try:
+        for rep in range(2):
+            ths = [threading.Thread(target=work, args=(j,)) for j in (2 * rep, 2 * rep + 1)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+        for j, jb in enumerate(jobs):
+            assert results[j].tolist() == jb["st"], j
+            assert np.array_equal(jb["buf"].array, jb["exp"]), j
+            for t, w in enumerate(jb["ew"]):
+                o = jb["owins"][t]
+                assert (w.current, w.lost, w.dupe, w.out_of_window) == (o.current, o.lost, o.dupe, o.out_of_window)
+    finally:
+        for jb in jobs:
+            jb["buf"].free()
+            for c in jb["ciphers"]:
+                c.destroy()

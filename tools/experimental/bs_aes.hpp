@@ -22,7 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "layout.hpp"
+#include "../../nebula_amd/csrc/layout.hpp"
 
 namespace neb {
 

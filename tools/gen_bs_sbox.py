@@ -1,4 +1,4 @@
-"""Generate nebula_amd/csrc/bs_sbox.inc: the AES S-box as a bitsliced Boolean circuit for gfx950.
+"""Generate tools/experimental/bs_sbox.inc: the AES S-box as a bitsliced Boolean circuit for gfx950.
 
 The circuit is the 115-gate (83 XOR/XNOR + 32 AND) Boyar-Peralta S-box network (published in
 "A new combinational logic minimization technique with applications to cryptology", SEA 2010).
@@ -192,7 +192,7 @@ def main():
         if sum(env[f"s{i}"] << (7 - i) for i in range(8)) != SBOX[x]:
             sys.exit(f"emitted bitop3 codes: mismatch at {x:#04x}")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = os.path.join(root, "nebula_amd", "csrc", "bs_sbox.inc")
+    out = os.path.join(root, "tools", "experimental", "bs_sbox.inc")
     with open(out, "w") as f:
         f.write("// GENERATED by tools/gen_bs_sbox.py — do not edit. The Boyar-Peralta AES S-box circuit\n")
         f.write(f"// ({n0} gates) folded to {n_ops} ops of at most 3 inputs (v_bitop3_b32), checked on all\n")

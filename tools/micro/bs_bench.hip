@@ -3,7 +3,7 @@
 // VALU instructions per pass from the code object (counted separately). Not part of the engine.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
-#include "../../nebula_amd/csrc/bs_aes.hpp"
+#include "../experimental/bs_aes.hpp"
 
 __global__ __launch_bounds__(1024, 4) void bs_kernel(const uint32_t* rec, uint4* out, int npass) {
     const uint32_t lane = threadIdx.x & 63u;

@@ -1,0 +1,62 @@
+"""Record one bench config's counter passes in profiles/pmc_configs.json, keyed by config (not by
+kernel name: C3 and C5 run the same mixed-key kernel, with different traffic).
+
+From a profiles/<tag> directory written by tools/pmc_summary.py (pmc_fetch.json, pmc_write.json,
+pmc_lds.json, trace_kernel_stats.csv) it takes, for the config's dominant kernel (the seal launch):
+  hbm_bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes; MI355X_MICROARCH.md §HBM: on
+                         gfx950 FETCH_SIZE reports half the bytes of 16 B/lane streaming reads)
+  lds_busy  = SQ_LDS_IDX_ACTIVE / SQ_BUSY_CU_CYCLES
+  valu_busy = SQ_INSTS_VALU x 2 cycles per wave64 op / 4 SIMDs per CU, over the CU-busy cycles
+  mean_ns   = the kernel's rocprof mean duration (the same passes' kernel trace)
+usage: python tools/pmc_config.py CONFIG KERNEL_SUBSTRING profiles/<tag>
+   e.g. python tools/pmc_config.py C3 "gcm_chunk_kernel<false>" profiles/r3_c3
+"""
+import csv
+import json
+import os
+import sys
+
+CUS, SIMDS_PER_CU, VALU_CYCLES = 256, 4, 2
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+
+
+def pick(d, sub):
+    hits = [k for k in d if sub in k]
+    if not hits:
+        raise SystemExit(f"no kernel matching {sub!r} in {sorted(d)}")
+    return d[sorted(hits, key=len)[0]]
+
+
+def main():
+    cfg, sub, tag = sys.argv[1:4]
+    load = lambda n: json.load(open(os.path.join(tag, f"pmc_{n}.json")))  # noqa: E731
+    f, w = pick(load("fetch"), sub), pick(load("write"), sub)
+    ent = {
+        "kernel": sub,
+        "fetch_size_kib": round(f["FETCH_SIZE"], 1),
+        "write_size_kib": round(w["WRITE_SIZE"], 1),
+        "hbm_bytes_per_launch": int(2 * f["FETCH_SIZE"] * 1024 + w["WRITE_SIZE"] * 1024),
+        "source": os.path.relpath(tag, ROOT),
+    }
+    try:
+        lds = pick(load("lds"), sub)
+        busy = lds["SQ_BUSY_CU_CYCLES"]
+        ent["lds_busy"] = round(lds["SQ_LDS_IDX_ACTIVE"] / busy, 3)
+        ent["valu_busy"] = round(lds["SQ_INSTS_VALU"] / (CUS * SIMDS_PER_CU) * VALU_CYCLES / (busy / CUS), 3)
+    except (OSError, KeyError, SystemExit):
+        pass
+    stats = os.path.join(tag, "trace_kernel_stats.csv")
+    if os.path.exists(stats):
+        for r in csv.DictReader(open(stats)):
+            if sub in r["Name"]:
+                ent["mean_ns"] = round(float(r["AverageNs"]), 1)
+                break
+    path = os.path.join(ROOT, "profiles", "pmc_configs.json")
+    allc = json.load(open(path)) if os.path.exists(path) else {}
+    allc[cfg] = ent
+    json.dump(allc, open(path, "w"), indent=1, sort_keys=True)
+    print(cfg, json.dumps(ent))
+
+
+if __name__ == "__main__":
+    main()
