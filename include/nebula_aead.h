@@ -226,6 +226,33 @@ NEB_API int neb_dwindows_store(neb_dwindows* d, uint32_t idx, neb_window* w);
  * sequential finish: those where a tag failed, or counters within 2^62 of wrapping). */
 NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb_desc* d_desc, uint32_t n,
                               uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream);
+/* ---- receive from the wire: readOutsidePackets' gate in front of Decrypt / VerifyRelay ---------- */
+/* One received UDP datagram (or GRO segment) of a receive batch, as readOutsidePackets gets it
+ * (outside.go:30): the wire packet header(16) || ct || tag(16) at off of the arena, len bytes, and
+ * the tunnel (window / key slot) the caller's hostmap lookup resolved from the header's remote
+ * index (outside.go:94-100), NEB_KEYS_MIXED when it found none. */
+typedef struct neb_rx_packet {
+    uint64_t off;
+    uint32_t len;
+    uint32_t key_id;
+} neb_rx_packet;
+#define NEB_STATUS_NOT_MESSAGE 7 /* a valid header of an unencrypted type (handshake, recv error,
+                                    outside.go:83-89): left to the control plane, untouched */
+/* Per packet, readOutsidePackets up to the decrypt, then Decrypt or VerifyRelay: h.Parse (len < 16:
+ * NEB_STATUS_INVALID, header.go:143-146); version 1 and IsValidSubType (header.go:192-205), else
+ * NEB_STATUS_INVALID (outside.go:49-64); Handshake / RecvError types -> NEB_STATUS_NOT_MESSAGE; no
+ * tunnel -> NEB_STATUS_BAD_KEY (outside.go:100-106); len < 16 + 16 -> NEB_STATUS_INVALID
+ * (outside.go:108-114); the nonce is the header's counter (bytes 8:16, big-endian). Message/Relay
+ * packets are verified GMAC-only over packet[:len-16] (VerifyRelay, connection_state.go:121-148),
+ * every other type is opened in place with the header as AAD (Decrypt, connection_state.go:99-119),
+ * both through the replay window of their tunnel: statuses, arena bytes and windows as
+ * neb_rx_open_batch_host / neb_rx_open_batch give for the descriptors the gate builds. Packets the
+ * gate refuses are not touched. The host form checks every packet against arena_len first. */
+NEB_API int neb_rx_open_wire_batch_host(neb_engine* e, int alg, neb_window* const* windows, uint32_t nwindows,
+                                        const neb_rx_packet* pk, uint32_t n, uint8_t* arena, size_t arena_len,
+                                        int32_t* status, uint32_t key_hint);
+NEB_API int neb_rx_open_wire_batch(neb_engine* e, int alg, neb_dwindows* d, const neb_rx_packet* d_pk, uint32_t n,
+                                   uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream);
 /* ---- transmit: TUN reads (IP packets, TSO/USO superpackets) -> sealed wire packets ------------ */
 /* virtio_net_hdr values (linux/virtio_net.h), as the TUN hands them over (overlay/tio/virtio/header_linux.go) */
 #define NEB_VNET_F_NEEDS_CSUM 1

@@ -35,6 +35,7 @@ STATUS_BAD_KEY = 3
 STATUS_REPLAY = 4
 STATUS_INVALID = 5
 STATUS_NO_SPACE = 6
+STATUS_NOT_MESSAGE = 7
 
 OVERHEAD = 16
 HEADER_LEN = 16
@@ -48,6 +49,9 @@ DESC_DTYPE = np.dtype(
      ("len", "<u4"), ("aad_len", "<u4"), ("key_id", "<u4"), ("flags", "<u4")]
 )
 assert DESC_DTYPE.itemsize == 48
+# neb_rx_packet (include/nebula_aead.h): one received wire packet and its tunnel
+RX_PACKET_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("key_id", "<u4")])
+assert RX_PACKET_DTYPE.itemsize == 16
 
 # Every symbol include/nebula_aead.h declares, with (restype, argtypes).
 _vp, _u8p, _sz, _u32, _u64, _i = C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
@@ -90,6 +94,8 @@ SIGNATURES = {
     "neb_tx_seal_batch": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
     "neb_tx_seal_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _vp, _u32, _vp, _vp,
                                     _u32]),
+    "neb_rx_open_wire_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _u32]),
+    "neb_rx_open_wire_batch": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
     "neb_queue_create": (_i, [_vp, _i, _i, _vp, C.POINTER(_vp)]),
     "neb_queue_destroy": (_i, [_vp]),
     "neb_queue_submit": (_i, [_vp, _vp, _u32, _vp, _sz, _vp]),

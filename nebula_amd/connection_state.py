@@ -167,6 +167,24 @@ def rx_open_batch(engine, alg: int, windows: Sequence[Optional[Bits]], desc: np.
     return status
 
 
+def rx_open_wire_batch(engine, alg: int, windows: Sequence[Optional[Bits]], packets: np.ndarray,
+                       arena: np.ndarray, key_hint: int = L.KEYS_MIXED) -> np.ndarray:
+    """readOutsidePackets over a receive batch of wire packets (outside.go:30-133): the header
+    parse, version / subtype / size checks and the counter from the header on the engine's side,
+    then Decrypt or VerifyRelay through the windows. packets: RX_PACKET_DTYPE (off, len, key_id =
+    the tunnel the caller's hostmap lookup resolved, KEYS_MIXED for none). Returns the statuses."""
+    lib = L.lib()
+    n = len(packets)
+    status = np.full(n, -1, dtype=np.int32)
+    arr = (C.c_void_p * max(len(windows), 1))(*[(w.handle.value if w is not None else None) for w in windows])
+    pk = np.ascontiguousarray(packets, dtype=L.RX_PACKET_DTYPE)
+    rc = lib.neb_rx_open_wire_batch_host(engine.handle, alg, arr, len(windows), pk.ctypes.data_as(C.c_void_p), n,
+                                         arena.ctypes.data_as(C.c_void_p), arena.nbytes,
+                                         status.ctypes.data_as(C.c_void_p), key_hint)
+    L.check(rc, "neb_rx_open_wire_batch_host")
+    return status
+
+
 class DeviceWindows:
     """A set of replay windows in device memory (neb_dwindows_*), slot = the tunnel's key_id, for
     receive batches that stay on the device (rx_open_batch_device). load/store copy one window's
@@ -213,3 +231,17 @@ def rx_open_batch_device(engine, alg: int, windows: DeviceWindows, d_desc, d_are
 
 __all__ = ["Bits", "NewBits", "ConnectionState", "ReplayWindow", "ErrAlreadySeen", "ErrOpen", "rx_open_batch",
            "DeviceWindows", "rx_open_batch_device"]
+
+
+def rx_open_wire_batch_device(engine, alg: int, windows: DeviceWindows, d_packets, d_arena, d_status,
+                              key_hint: int = L.KEYS_MIXED, stream=None) -> None:
+    """rx_open_wire_batch with the wire packets, the arena, the statuses and the windows in device
+    memory (torch tensors: d_packets uint8 of RX_PACKET_DTYPE records)."""
+    import torch
+
+    s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+    n = d_packets.numel() // L.RX_PACKET_DTYPE.itemsize
+    rc = L.lib().neb_rx_open_wire_batch(engine.handle, alg, windows.handle, C.c_void_p(d_packets.data_ptr()), n,
+                                        C.c_void_p(d_arena.data_ptr()), C.c_void_p(d_status.data_ptr()), key_hint,
+                                        C.c_void_p(s))
+    L.check(rc, "neb_rx_open_wire_batch")

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/nebula_aead.h"
+#include "host_common.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
 #include "tx.hpp"
@@ -78,19 +79,9 @@ struct PipeSlot {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// [off, off + len) lies inside [0, cap), written so that no sum can wrap around 2^64.
-inline bool span_in(uint64_t off, uint64_t len, uint64_t cap) { return off <= cap && len <= cap - off; }
 
 }  // namespace
 
-// Every region a descriptor touches lies inside a host arena of arena_len bytes: the AAD, the
-// source (payload, plus the tag when opening) and the destination (payload, plus the tag when
-// sealing). Shared with window.cpp, which validates a receive batch before touching anything.
-bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len) {
-    const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
-    return span_in(d.src_off, pay, arena_len) && span_in(d.dst_off, outl, arena_len) &&
-           span_in(d.aad_off, d.aad_len, arena_len);
-}
 
 namespace {
 

@@ -1,30 +1,12 @@
-// queue.cpp — the submission queue (include/nebula_aead.h, "submission queue"): many threads'
-// small seal/open flushes gathered into device-sized batches.
-//
-// Nebula seals at most 128 packets per TX flush (overlay/batch/tx_batch.go:5, interface.go:465-469)
-// and opens at most listen.batch = 64 per RX flush (main.go:181, interface.go:395-400), from
-// `routines` goroutines at once (interface.go:320-335). A device batch only pays for itself at
-// thousands of packets, so neb_queue_submit lets every routine hand over its flush as is: the
-// packets are copied into pinned staging, joined with the other routines' flushes into one batch,
-// sealed or opened by one kernel launch running zero-copy on the staging, and copied back; the call
-// returns when its own packets are done, with the same arena bytes and statuses as
-// neb_seal_batch_host / neb_open_batch_host.
-//
-// A batch goes to the device when it reaches max_packets, when the next submission would not fit
-// its staging, when neb_queue_flush asks, or max_delay_us after its first submission. `depth`
-// staging batches rotate: one filling, the others on the device or being copied out.
+// queue.cpp — the C ABI of the submission queue (include/nebula_aead.h): queue_core.hpp's state
+// machine over the engine. Staging is pinned, mapped host memory, each batch is one zero-copy
+// kernel launch on the queue's stream (its own mixed-key scheduler workspace), and a HIP event with
+// a system-scope release marks it done.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <chrono>
-#include <condition_variable>
-#include <cstring>
-#include <mutex>
 #include <new>
-#include <thread>
-#include <vector>
 
-#include "../../include/nebula_aead.h"
+#include "queue_core.hpp"
 
 extern "C" {  // engine.cpp, internal
 void* neb_sched_space_new();
@@ -34,124 +16,27 @@ int neb_launch_on(neb_engine* e, int alg, int open, const neb_desc* desc, uint32
 int neb_key_alg(neb_engine* e, uint32_t key);
 int neb_engine_device_of(const neb_engine* e);
 }
-bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len);
 
 namespace {
 
-using Clock = std::chrono::steady_clock;
-
-enum class BState { kFree, kFilling, kSealed, kLaunched, kDone };
-
-struct QBatch {
-    // pinned, mapped staging: the kernels read and write it in place
-    uint8_t* arena = nullptr;
-    neb_desc* desc = nullptr;
-    int32_t* status = nullptr;
-    hipEvent_t ev = nullptr;
-    BState state = BState::kFree;
-    uint32_t npk = 0, subs = 0, writers = 0, readers = 0;
-    size_t used = 0;
-    uint32_t key0 = NEB_KEYS_MIXED;  // the one key every packet uses so far, or NEB_KEYS_MIXED
-    bool one_key = true;
-    Clock::time_point first{};
-    int rc = NEB_OK;
+struct HipDev {
+    using Token = hipEvent_t;
+    neb_engine* e = nullptr;
+    int alg = 0, open = 0;
+    hipStream_t stream = nullptr;
+    void* sched = nullptr;
+    int launch(neb_desc* desc, uint32_t n, uint8_t* arena, int32_t* status, uint32_t hint, Token& ev) {
+        int rc = neb_launch_on(e, alg, open, desc, n, arena, status, hint, stream, sched);
+        if (rc == NEB_OK && hipEventRecord(ev, stream) != hipSuccess) rc = NEB_ERR_HIP;
+        return rc;
+    }
+    int wait(Token& ev) { return hipEventSynchronize(ev) == hipSuccess ? NEB_OK : NEB_ERR_HIP; }
+    bool key_ok(uint32_t key) { return neb_key_alg(e, key) == alg; }
 };
-
-size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
-
-// staging bytes one packet takes: AAD, the source (payload, + tag when opening), and a separate
-// destination when the descriptor is not in place
-size_t staged_bytes(const neb_desc& d, int open) {
-    const size_t src = (size_t)d.len + (open ? 16u : 0u), dst = (size_t)d.len + (open ? 0u : 16u);
-    const size_t in_place = d.src_off == d.dst_off ? 0 : up16(dst);
-    return up16(d.aad_len) + up16(std::max(src, dst)) + in_place;
-}
 
 }  // namespace
 
-struct neb_queue {
-    neb_engine* e = nullptr;
-    int alg = 0, open = 0;
-    neb_queue_config cfg{};
-    hipStream_t stream = nullptr;
-    void* sched = nullptr;
-    std::vector<QBatch> b;
-    uint32_t cur = 0;          // the batch accepting submissions
-    uint32_t next_launch = 0;  // batches launch and complete in ring order
-    std::mutex mu;
-    std::condition_variable cv;   // submitters: a batch became free or done
-    std::condition_variable fcv;  // the flusher: a batch has work / was sealed / writers finished
-    bool flush_req = false, quit = false;
-    std::thread flusher, completer;
-    uint64_t n_batches = 0, n_packets = 0, n_subs = 0, n_bytes = 0;
-
-    // seal the filling batch and move `cur` to the next one (caller holds mu)
-    void seal_current() {
-        QBatch& x = b[cur];
-        if (x.state != BState::kFilling) return;
-        x.state = BState::kSealed;
-        cur = (cur + 1) % (uint32_t)b.size();
-        fcv.notify_all();
-    }
-
-    void flush_loop() {
-        std::unique_lock<std::mutex> lk(mu);
-        for (;;) {
-            QBatch& x = b[next_launch];
-            if (quit && x.state != BState::kSealed && (x.state != BState::kFilling || x.subs == 0)) return;
-            if (x.state == BState::kFilling && x.subs > 0) {
-                const auto due = x.first + std::chrono::microseconds(cfg.max_delay_us);
-                if (flush_req || quit || Clock::now() >= due) {
-                    flush_req = false;
-                    if (cur == next_launch) seal_current();
-                    continue;
-                }
-                fcv.wait_until(lk, due);
-                continue;
-            }
-            if (x.state != BState::kSealed || x.writers > 0) {
-                fcv.wait(lk);
-                continue;
-            }
-            // sealed and every submitter's copy-in is done: launch it
-            const uint32_t n = x.npk;
-            uint32_t hint = x.one_key ? x.key0 : NEB_KEYS_MIXED;
-            lk.unlock();
-            // one tunnel's packets run the single-key kernel, if that key is installed for this
-            // algorithm (otherwise the mixed path reports NEB_STATUS_BAD_KEY per packet)
-            if (hint != NEB_KEYS_MIXED && neb_key_alg(e, hint) != alg) hint = NEB_KEYS_MIXED;
-            int rc = neb_launch_on(e, alg, open, x.desc, n, x.arena, x.status, hint, stream, sched);
-            if (rc == NEB_OK && hipEventRecord(x.ev, stream) != hipSuccess) rc = NEB_ERR_HIP;
-            lk.lock();
-            x.rc = rc;
-            x.state = BState::kLaunched;
-            n_batches++;
-            n_packets += n;
-            next_launch = (next_launch + 1) % (uint32_t)b.size();
-            fcv.notify_all();  // the completer
-        }
-    }
-
-    void complete_loop() {
-        uint32_t i = 0;
-        std::unique_lock<std::mutex> lk(mu);
-        for (;;) {
-            QBatch& x = b[i];
-            if (x.state != BState::kLaunched) {
-                if (quit && x.state != BState::kSealed && x.state != BState::kFilling) return;
-                fcv.wait(lk);
-                continue;
-            }
-            lk.unlock();
-            hipError_t err = x.rc == NEB_OK ? hipEventSynchronize(x.ev) : hipSuccess;
-            lk.lock();
-            if (err != hipSuccess && x.rc == NEB_OK) x.rc = NEB_ERR_HIP;
-            x.state = BState::kDone;
-            cv.notify_all();
-            i = (i + 1) % (uint32_t)b.size();
-        }
-    }
-};
+struct neb_queue : neb_q::Queue<HipDev> {};
 
 extern "C" {
 
@@ -160,213 +45,65 @@ NEB_API int neb_queue_create(neb_engine* e, int alg, int open, const neb_queue_c
         return NEB_ERR_INVALID;
     *out = nullptr;
     neb_queue_config c = cfg ? *cfg : neb_queue_config{};
-    if (c.max_packets == 0) c.max_packets = 16384;
-    if (c.max_delay_us == 0) c.max_delay_us = 100;
-    if (c.arena_bytes == 0) c.arena_bytes = (uint64_t)c.max_packets * 1536;
-    if (c.depth == 0) c.depth = 3;
-    if (c.depth < 2 || c.depth > 16 || c.max_packets > (1u << 22) || c.arena_bytes > (1ull << 36)) return NEB_ERR_INVALID;
+    if (!neb_q::normalize(c)) return NEB_ERR_INVALID;
     neb_queue* q = new (std::nothrow) neb_queue;
     if (!q) return NEB_ERR_INVALID;
-    q->e = e;
-    q->alg = alg;
+    q->dev.e = e;
+    q->dev.alg = alg;
+    q->dev.open = open;
     q->open = open;
     q->cfg = c;
     hipSetDevice(neb_engine_device_of(e));
     q->b.resize(c.depth);
-    bool ok = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) == hipSuccess;
-    q->sched = ok ? neb_sched_space_new() : nullptr;
-    ok = ok && q->sched;
-    for (QBatch& x : q->b) {
-        // release-to-system: the kernel's stores into the mapped staging are visible to the host
-        // once the event completes
+    bool ok = hipStreamCreateWithFlags(&q->dev.stream, hipStreamNonBlocking) == hipSuccess;
+    q->dev.sched = ok ? neb_sched_space_new() : nullptr;
+    ok = ok && q->dev.sched;
+    for (auto& x : q->b) {
         ok = ok && hipHostMalloc((void**)&x.arena, c.arena_bytes, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipHostMalloc((void**)&x.desc, (size_t)c.max_packets * sizeof(neb_desc), hipHostMallocDefault) ==
                        hipSuccess;
         ok = ok && hipHostMalloc((void**)&x.status, (size_t)c.max_packets * 4, hipHostMallocDefault) == hipSuccess;
-        ok = ok && hipEventCreateWithFlags(&x.ev, hipEventDisableTiming | hipEventReleaseToSystem) == hipSuccess;
+        // release-to-system: the kernel's stores into the mapped staging are visible to the host
+        // once the event completes
+        ok = ok && hipEventCreateWithFlags(&x.tok, hipEventDisableTiming | hipEventReleaseToSystem) == hipSuccess;
     }
     if (!ok) {
         neb_queue_destroy(q);
         return NEB_ERR_HIP;
     }
-    q->flusher = std::thread([q] { q->flush_loop(); });
-    q->completer = std::thread([q] { q->complete_loop(); });
+    q->start();
     *out = q;
     return NEB_OK;
 }
 
 NEB_API int neb_queue_destroy(neb_queue* q) {
     if (!q) return NEB_ERR_INVALID;
-    {
-        std::lock_guard<std::mutex> g(q->mu);
-        q->quit = true;
-        q->fcv.notify_all();
-        q->cv.notify_all();
-    }
-    if (q->flusher.joinable()) q->flusher.join();
-    {
-        std::lock_guard<std::mutex> g(q->mu);
-        q->fcv.notify_all();
-    }
-    if (q->completer.joinable()) q->completer.join();
-    {
-        // wait for every submitter to have copied its results out
-        std::unique_lock<std::mutex> lk(q->mu);
-        q->cv.wait(lk, [q] {
-            for (QBatch& x : q->b)
-                if (x.readers > 0) return false;
-            return true;
-        });
-    }
-    hipSetDevice(neb_engine_device_of(q->e));
-    if (q->stream) hipStreamSynchronize(q->stream);
-    for (QBatch& x : q->b) {
+    q->shutdown();
+    hipSetDevice(neb_engine_device_of(q->dev.e));
+    if (q->dev.stream) hipStreamSynchronize(q->dev.stream);
+    for (auto& x : q->b) {
         if (x.arena) hipHostFree(x.arena);
         if (x.desc) hipHostFree(x.desc);
         if (x.status) hipHostFree(x.status);
-        if (x.ev) hipEventDestroy(x.ev);
+        if (x.tok) hipEventDestroy(x.tok);
     }
-    neb_sched_space_free(q->sched);
-    if (q->stream) hipStreamDestroy(q->stream);
+    neb_sched_space_free(q->dev.sched);
+    if (q->dev.stream) hipStreamDestroy(q->dev.stream);
     delete q;
     return NEB_OK;
 }
 
-NEB_API int neb_queue_flush(neb_queue* q) {
-    if (!q) return NEB_ERR_INVALID;
-    std::lock_guard<std::mutex> g(q->mu);
-    q->flush_req = true;
-    q->fcv.notify_all();
-    return NEB_OK;
-}
+NEB_API int neb_queue_flush(neb_queue* q) { return q ? q->flush() : NEB_ERR_INVALID; }
 
 NEB_API int neb_queue_stats(neb_queue* q, uint64_t stats[4]) {
     if (!q || !stats) return NEB_ERR_INVALID;
-    std::lock_guard<std::mutex> g(q->mu);
-    stats[0] = q->n_batches;
-    stats[1] = q->n_packets;
-    stats[2] = q->n_subs;
-    stats[3] = q->n_bytes;
+    q->stats(stats);
     return NEB_OK;
 }
 
 NEB_API int neb_queue_submit(neb_queue* q, const neb_desc* desc, uint32_t n, uint8_t* arena, size_t arena_len,
                              int32_t* status) {
-    if (!q || (n && (!desc || !arena || !status))) return NEB_ERR_INVALID;
-    if (n == 0) return NEB_OK;
-    const int open = q->open;
-    // validated before anything is staged: a bad batch leaves the arena and statuses untouched
-    for (uint32_t i = 0; i < n; i++)
-        if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
-    // the submission in pieces that each fit one batch
-    uint32_t p0 = 0;
-    while (p0 < n) {
-        uint32_t cnt = 0;
-        size_t bytes = 0;
-        while (p0 + cnt < n && cnt < q->cfg.max_packets) {
-            const size_t sb = staged_bytes(desc[p0 + cnt], open);
-            if (bytes + sb > q->cfg.arena_bytes) break;
-            bytes += sb;
-            cnt++;
-        }
-        if (cnt == 0) return NEB_ERR_INVALID;  // one packet larger than the whole staging
-        // reserve room in the filling batch
-        QBatch* x = nullptr;
-        uint32_t pk0 = 0;
-        size_t off0 = 0;
-        {
-            std::unique_lock<std::mutex> lk(q->mu);
-            for (;;) {
-                if (q->quit) return NEB_ERR_INVALID;
-                QBatch& c = q->b[q->cur];
-                if (c.state == BState::kFree) {
-                    c.state = BState::kFilling;
-                    c.npk = c.subs = c.writers = c.readers = 0;
-                    c.used = 0;
-                    c.one_key = true;
-                    c.key0 = NEB_KEYS_MIXED;
-                    c.rc = NEB_OK;
-                }
-                if (c.state == BState::kFilling) {
-                    if (c.npk + cnt <= q->cfg.max_packets && c.used + bytes <= q->cfg.arena_bytes) break;
-                    q->seal_current();  // full for this submission: it goes out, the next one fills
-                    continue;
-                }
-                q->cv.wait(lk);  // every staging batch is busy
-            }
-            QBatch& c = q->b[q->cur];
-            x = &c;
-            pk0 = c.npk;
-            off0 = c.used;
-            c.npk += cnt;
-            c.used += bytes;
-            if (c.subs++ == 0) {
-                c.first = Clock::now();
-                q->fcv.notify_all();  // the flusher starts this batch's deadline
-            }
-            c.writers++;
-            c.readers++;
-            q->n_subs++;
-            q->n_bytes += bytes;
-            for (uint32_t i = 0; i < cnt; i++) {
-                const uint32_t k = desc[p0 + i].key_id;
-                if (c.key0 == NEB_KEYS_MIXED && c.one_key) c.key0 = k;
-                else if (c.key0 != k) c.one_key = false;
-            }
-            if (c.npk == q->cfg.max_packets) q->seal_current();
-        }
-        // copy the packets into the staging (outside the lock: submitters copy in parallel)
-        size_t off = off0;
-        for (uint32_t i = 0; i < cnt; i++) {
-            const neb_desc& d = desc[p0 + i];
-            neb_desc s = d;
-            const size_t src = (size_t)d.len + (open ? 16u : 0u), dst = (size_t)d.len + (open ? 0u : 16u);
-            s.aad_off = off;
-            if (d.aad_len) std::memcpy(x->arena + off, arena + d.aad_off, d.aad_len);
-            off += up16(d.aad_len);
-            s.src_off = off;
-            std::memcpy(x->arena + off, arena + d.src_off, src);
-            if (d.src_off == d.dst_off) {
-                s.dst_off = off;
-                off += up16(std::max(src, dst));
-            } else {
-                off += up16(std::max(src, dst));
-                s.dst_off = off;
-                off += up16(dst);
-            }
-            s.flags = 0;
-            x->desc[pk0 + i] = s;
-            x->status[pk0 + i] = -1;
-        }
-        {
-            std::unique_lock<std::mutex> lk(q->mu);
-            if (--x->writers == 0) q->fcv.notify_all();
-            q->cv.wait(lk, [x] { return x->state == BState::kDone; });
-        }
-        const int rc = x->rc;
-        if (rc == NEB_OK) {
-            for (uint32_t i = 0; i < cnt; i++) {
-                const neb_desc& d = desc[p0 + i];
-                const neb_desc& s = x->desc[pk0 + i];
-                const int32_t st = x->status[pk0 + i];
-                status[p0 + i] = st;
-                // what the in-place batch writes: the sealed payload + tag, or the opened (or, on a
-                // failed tag, zeroed) payload; nothing for a refused key or an exhausted counter
-                if (st == NEB_STATUS_OK || (open && st == NEB_STATUS_AUTH_FAILED))
-                    std::memcpy(arena + d.dst_off, x->arena + s.dst_off, (size_t)d.len + (open ? 0u : 16u));
-            }
-        }
-        {
-            std::lock_guard<std::mutex> g(q->mu);
-            if (--x->readers == 0) {
-                x->state = BState::kFree;
-                q->cv.notify_all();
-            }
-        }
-        if (rc != NEB_OK) return rc;
-        p0 += cnt;
-    }
-    return NEB_OK;
+    return q ? q->submit(desc, n, arena, arena_len, status) : NEB_ERR_INVALID;
 }
 
 }  // extern "C"

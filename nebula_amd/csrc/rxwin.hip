@@ -438,6 +438,28 @@ __global__ __launch_bounds__(256) void rx_span_kernel(const uint8_t* __restrict_
     for (uint32_t k = lane; k < sp.len; k += 64u) dst[sp.dst + k] = src ? src[sp.src + k] : (uint8_t)0;
 }
 
+__global__ __launch_bounds__(256) void rx_wire_kernel(const neb_rx_packet* __restrict__ pk, uint32_t n,
+                                                      const uint8_t* __restrict__ arena, neb_desc* __restrict__ desc,
+                                                      int32_t* __restrict__ gate) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const neb_rx_packet p = pk[i];
+    uint8_t h[16];
+    if (p.len >= 16u)
+        for (int k = 0; k < 16; k++) h[k] = arena[p.off + k];
+    neb_desc d{p.off, p.off, p.off, 0, 0, 0, NEB_KEYS_MIXED, 0};
+    const int32_t g = neb_rx_wire_gate(h, p, &d);
+    if (g != NEB_STATUS_OK) d = neb_desc{p.off, p.off, p.off, 0, 0, 0, NEB_KEYS_MIXED, 0};
+    desc[i] = d;
+    gate[i] = g;
+}
+
+__global__ __launch_bounds__(256) void rx_wire_fix_kernel(const int32_t* __restrict__ gate, int32_t* __restrict__ status,
+                                                          uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n && gate[i] != NEB_STATUS_OK) status[i] = gate[i];
+}
+
 __device__ __forceinline__ bool rx_fast(uint32_t fl) { return (fl & kRxTouched) && !(fl & (kRxRisky | kRxSlow)); }
 
 // Per admitted packet (compacted order): its tag verdict into its status (a failure sends the
@@ -637,6 +659,19 @@ extern "C" hipError_t neb_rxdev_spans(const uint8_t* src, uint8_t* dst, const ne
                                       hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(neb::rx_span_kernel, dim3((n + 3u) / 4u), dim3(256), 0, s, src, dst, d_spans, n);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t neb_rxdev_wire(const neb_rx_packet* d_pk, uint32_t n, const uint8_t* d_arena, neb_desc* d_desc,
+                                     int32_t* d_gate, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(neb::rx_wire_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, d_pk, n, d_arena, d_desc, d_gate);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t neb_rxdev_wire_fix(const int32_t* d_gate, int32_t* d_status, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(neb::rx_wire_fix_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, d_gate, d_status, n);
     return hipGetLastError();
 }
 

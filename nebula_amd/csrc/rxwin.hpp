@@ -128,6 +128,39 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const neb::RxDevWin* win,
                                      const neb::RxDevWs* ws, int32_t* d_status, hipStream_t s);
 extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
+// readOutsidePackets (outside.go:30-114) for one wire packet, up to the decrypt: returns
+// NEB_STATUS_OK with *d describing the Decrypt (header as AAD, in place) or the VerifyRelay (GMAC
+// over packet[:len-16]), or the status the packet ends with. h: the first 16 bytes (read only when
+// len >= 16). Shared by the host (window.cpp) and the device (rx_wire_kernel) forms.
+__host__ __device__ inline int32_t neb_rx_wire_gate(const uint8_t* h, const neb_rx_packet& p, neb_desc* d) {
+    if (p.len < 16u) return NEB_STATUS_INVALID;  // h.Parse: ErrHeaderTooShort (header.go:144-146)
+    const uint32_t ver = h[0] >> 4, type = h[0] & 15u, sub = h[1];
+    if (ver != 1u) return NEB_STATUS_INVALID;  // header.Version (outside.go:49-55)
+    // IsValidSubType (header.go:192-205): Message 0/1, Handshake 0 (IXPSK0), Test 0/1, RecvError,
+    // LightHouse, CloseTunnel, Control 0
+    const bool valid = (type == 1u || type == 4u) ? sub <= 1u : (type == 0u || (type >= 2u && type <= 6u)) && sub == 0u;
+    if (!valid) return NEB_STATUS_INVALID;
+    if (type == 0u || type == 2u) return NEB_STATUS_NOT_MESSAGE;  // handshake, recv error (outside.go:83-89)
+    if (p.key_id == NEB_KEYS_MIXED) return NEB_STATUS_BAD_KEY;    // no hostinfo (outside.go:100-106)
+    if (p.len < 32u) return NEB_STATUS_INVALID;                   // header.Len + Overhead (outside.go:108-114)
+    uint64_t c = 0;
+    for (int i = 8; i < 16; i++) c = c << 8 | h[i];
+    d->counter = c;
+    d->key_id = p.key_id;
+    d->flags = 0;
+    d->aad_off = p.off;
+    if (type == 1u && sub == 1u) {  // VerifyRelay: AD = everything but the trailing tag
+        d->aad_len = p.len - 16u;
+        d->src_off = d->dst_off = p.off + p.len - 16u;
+        d->len = 0;
+    } else {  // Decrypt: in place after the header
+        d->aad_len = 16u;
+        d->src_off = d->dst_off = p.off + 16u;
+        d->len = p.len - 32u;
+    }
+    return NEB_STATUS_OK;
+}
+
 // Byte spans between two device buffers, one wave per span (the exact receive pass's speculative
 // opens: packets copied out of the arena into a scratch buffer, plaintext copied back for the ones
 // the windows accept, zeros for the ones that pass their window but fail their tag). src == NULL
@@ -138,5 +171,11 @@ struct neb_span {
 };
 extern "C" hipError_t neb_rxdev_spans(const uint8_t* src, uint8_t* dst, const neb_span* d_spans, uint32_t n,
                                       hipStream_t s);
+// the gate over a device batch of wire packets: descriptors (refused packets: a harmless empty
+// descriptor with key NEB_KEYS_MIXED, so the receive leaves them alone) and the gate's statuses
+extern "C" hipError_t neb_rxdev_wire(const neb_rx_packet* d_pk, uint32_t n, const uint8_t* d_arena, neb_desc* d_desc,
+                                     int32_t* d_gate, hipStream_t s);
+// status[i] = gate[i] wherever the gate refused the packet
+extern "C" hipError_t neb_rxdev_wire_fix(const int32_t* d_gate, int32_t* d_status, uint32_t n, hipStream_t s);
 extern "C" hipError_t neb_rxdev_finish(uint32_t n, const neb::RxDevWin* win, const neb::RxDevWs* ws,
                                        int32_t* d_status, hipStream_t s);

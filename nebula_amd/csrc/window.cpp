@@ -34,10 +34,11 @@
 #include <vector>
 
 #include "../../include/nebula_aead.h"
+#include "host_common.hpp"
 #include "rxwin.hpp"
+#include "window_core.hpp"
 
 // engine.cpp
-bool neb_desc_in_arena(const neb_desc& d, int open, size_t arena_len);
 extern "C" {  // internal (hidden), defined inside engine.cpp's extern "C" block
 bool neb_rx_pipe_begin(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena, uint32_t n, uint32_t nchunks,
                        neb_desc** h_desc, int32_t** h_status, int* rc);
@@ -51,287 +52,8 @@ int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_
                          uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s);
 }
 
-namespace {
+using namespace neb_rx;
 
-// The batched receive's window simulation and real window pass run on a small persistent pool
-// when a batch touches at least kRxMinWindows windows: windows are independent, and each window's
-// packets stay on one thread, in arrival order. NEB_RX_THREADS sets the pool size (1 = this
-// thread only). Groups under kRxMinPerThread packets are not split.
-constexpr uint32_t kRxMinPerThread = 2048, kRxMinWindows = 64, kRxMaxThreads = 8;
-
-class RxPool {
-  public:
-    explicit RxPool(uint32_t nthreads) {
-        for (uint32_t t = 1; t < nthreads; t++) th_.emplace_back([this] { loop(); });
-    }
-    ~RxPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            quit_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    uint32_t size() const { return (uint32_t)th_.size() + 1; }
-    // fn(j) for j in [0, n), on the pool and this thread; returns when every call has returned.
-    // Calls from several threads at once run one after another.
-    void run(uint32_t n, const std::function<void(uint32_t)>& fn) {
-        if (n <= 1 || th_.empty()) {
-            for (uint32_t j = 0; j < n; j++) fn(j);
-            return;
-        }
-        std::lock_guard<std::mutex> serial(run_mu_);
-        {
-            std::lock_guard<std::mutex> g(m_);
-            job_ = &fn;
-            njobs_ = n;
-            next_.store(0);
-            left_ = n;
-            gen_++;
-        }
-        cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> g(m_);
-        done_cv_.wait(g, [&] { return left_ == 0 && active_ == 0; });
-        job_ = nullptr;
-    }
-
-  private:
-    void work() {
-        for (;;) {
-            const uint32_t j = next_.fetch_add(1);
-            if (j >= njobs_) return;
-            (*job_)(j);
-            std::lock_guard<std::mutex> g(m_);
-            if (--left_ == 0) done_cv_.notify_all();
-        }
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            {
-                std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return quit_ || (gen_ != seen && job_); });
-                if (quit_) return;
-                seen = gen_;
-                active_++;
-            }
-            work();
-            std::lock_guard<std::mutex> g(m_);
-            if (--active_ == 0 && left_ == 0) done_cv_.notify_all();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex m_, run_mu_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(uint32_t)>* job_ = nullptr;
-    uint32_t njobs_ = 0, left_ = 0, active_ = 0;
-    std::atomic<uint32_t> next_{0};
-    uint64_t gen_ = 0;
-    bool quit_ = false;
-};
-
-RxPool& rx_pool() {
-    static RxPool pool([] {
-        const char* v = std::getenv("NEB_RX_THREADS");
-        int t = v ? std::atoi(v) : (int)std::min(kRxMaxThreads, std::max(1u, std::thread::hardware_concurrency()));
-        return (uint32_t)std::max(1, std::min(t, 64));
-    }());
-    return pool;
-}
-
-struct WindowCore {
-    uint64_t length = 0, mask = 0, current = 0;
-    std::vector<uint64_t> words;
-    int64_t lost = 0, dupe = 0, out_of_window = 0;
-
-    bool get(uint64_t i) const {
-        const uint64_t p = i & mask;
-        return (words[p >> 6] >> (p & 63)) & 1u;
-    }
-    void set(uint64_t i) {
-        const uint64_t p = i & mask;
-        words[p >> 6] |= 1ull << (p & 63);
-    }
-    // clear `count` circular slots from slot `start`; returns how many were set (bits.go:63-118)
-    uint64_t clear_range(uint64_t start, uint64_t count) {
-        uint64_t was = 0;
-        if (count >= length) {
-            for (uint64_t& w : words) {
-                was += (uint64_t)__builtin_popcountll(w);
-                w = 0;
-            }
-            return was;
-        }
-        uint64_t pos = start, rem = count;
-        while (rem) {
-            const uint64_t b = pos & 63;
-            const uint64_t take = std::min({64 - b, rem, length - pos});
-            const uint64_t m = take == 64 ? ~0ull : ((1ull << take) - 1) << b;
-            uint64_t& w = words[pos >> 6];
-            was += (uint64_t)__builtin_popcountll(w & m);
-            w &= ~m;
-            rem -= take;
-            pos = (pos + take) & mask;
-        }
-        return was;
-    }
-    bool strictly_within(uint64_t i) const {  // bits.go:120-132
-        if (i < length && current < length) return true;
-        return i > current - length;
-    }
-    bool check(uint64_t i) const {  // bits.go:134-150
-        if (i > current) return true;
-        if (strictly_within(i)) return !get(i);
-        return false;
-    }
-    bool update(uint64_t i) {  // bits.go:168-262
-        if (i == current + 1) {
-            if (i > length && !get(i)) lost++;
-            set(i);
-            current = i;
-            return true;
-        }
-        if (i > current) {
-            const uint64_t top = current + length;
-            const uint64_t end = i > top ? top : i;
-            const uint64_t count = end - current;
-            const uint64_t start = (current + 1) & mask;
-            int64_t l = 0;
-            if (current >= length) {
-                l = (int64_t)count - (int64_t)clear_range(start, count);
-            } else {  // warmup: the first window, taken at most once per connection
-                for (uint64_t n = current + 1; n <= end; n++)
-                    if (!get(n) && n > length) l++;
-                clear_range(start, count);
-            }
-            if (i > top) l += (int64_t)(i - current - length);
-            lost += l;
-            set(i);
-            current = i;
-            return true;
-        }
-        if (strictly_within(i)) {
-            if (current == i || get(i)) {
-                dupe++;
-                return false;
-            }
-            set(i);
-            return true;
-        }
-        out_of_window++;
-        return false;
-    }
-};
-
-// The exact receive order for some windows' packet runs: Check → tag verdict → Update, packet
-// after packet in arrival order (connection_state.go:99-119). A packet not opened yet that its
-// window now accepts — an earlier copy of it failed its tag, or a forged counter further ahead held
-// it back in the simulation — stops its window there, and the stopped windows' remaining packets
-// are opened in one more batch:
-//   * first extra round: the rest of each stopped window's run is simulated again from the real
-//     state (tags already known to fail skipped, unknown ones assumed to verify) and what the
-//     simulation admits is opened in place (the simulation applies a superset of the real
-//     updates, so the real pass never refuses such a packet, barring another thread moving the
-//     window meanwhile);
-//   * any later round: every packet still unopened in the stopped runs is verified speculatively,
-//     out of place (spec_fn: plaintext into a scratch copy, the arena untouched); the real pass
-//     then knows every verdict and finishes without stopping. The packets it accepts get their
-//     plaintext copied into the arena (*commit), those that pass their window but fail their tag
-//     get their payload zeroed (*zero), as an in-place open would, and refused ones stay untouched.
-// Interleaved forgeries (F1, P1, F2, P2, ...: each forged far-ahead counter holds back the genuine
-// packets after it) therefore cost at most two extra batches, not one per forgery.
-// opened[i]: 0 = not yet, 1 = opened in place, 2 = verified speculatively.
-struct ExactRun {
-    uint32_t w, k0, k1;  // window, run positions [k0, k1)
-};
-template <class Ctr, class Pkt, class WithWin, class OpenFn, class SpecFn, class Par>
-int exact_rounds(const std::vector<ExactRun>& runs, uint32_t max_groups, Ctr&& ctr, Pkt&& pkt, uint8_t* opened,
-                 int32_t* verd, int32_t* status, WithWin&& with_window, OpenFn&& open_fn, SpecFn&& spec_fn,
-                 Par&& par, std::vector<uint32_t>* commit, std::vector<uint32_t>* zero) {
-    const bool stats = std::getenv("NEB_RX_STATS") != nullptr;  // rounds and opens to stderr (per call)
-    uint32_t rounds = 0, extra_opens = 0, extra_pkts = 0;
-    std::vector<uint32_t> pos(runs.size());
-    std::vector<uint32_t> active(runs.size());
-    for (size_t r = 0; r < runs.size(); r++) {
-        pos[r] = runs[r].k0;
-        active[r] = (uint32_t)r;
-    }
-    const uint32_t ng = std::max(1u, std::min(max_groups, (uint32_t)runs.size()));
-    std::vector<std::vector<uint32_t>> cm(ng), zr(ng);  // per group: packets to commit / zero
-    while (!active.empty()) {
-        const uint32_t na = std::max(1u, std::min(ng, (uint32_t)active.size()));
-        const bool speculative = extra_opens >= 1;  // the second extra round verifies everything left
-        std::vector<std::vector<uint32_t>> want(na);
-        par(na, [&](uint32_t gi) {
-            const size_t a0 = active.size() * gi / na, a1 = active.size() * (gi + 1) / na;
-            for (size_t a = a0; a < a1; a++) {
-                const uint32_t r = active[a];
-                const ExactRun& R = runs[r];
-                with_window(R.w, [&](WindowCore& core) {
-                    uint32_t k = pos[r];
-                    for (; k < R.k1; k++) {
-                        const uint32_t i = pkt(k);
-                        const uint64_t c = ctr(k);
-                        if (!core.check(c)) {
-                            status[i] = NEB_STATUS_REPLAY;
-                            continue;
-                        }
-                        if (!opened[i]) {
-                            if (speculative) {
-                                for (uint32_t k2 = k; k2 < R.k1; k2++)
-                                    if (!opened[pkt(k2)]) want[gi].push_back(pkt(k2));
-                                break;
-                            }
-                            WindowCore sim = core;
-                            for (uint32_t k2 = k; k2 < R.k1; k2++) {
-                                const uint32_t i2 = pkt(k2);
-                                if (opened[i2] && verd[i2] != NEB_STATUS_OK) continue;  // known to fail
-                                if (sim.check(ctr(k2))) {
-                                    sim.update(ctr(k2));
-                                    if (!opened[i2]) want[gi].push_back(i2);
-                                }
-                            }
-                            break;
-                        }
-                        if (verd[i] != NEB_STATUS_OK) {
-                            status[i] = verd[i];
-                            if (opened[i] == 2 && verd[i] == NEB_STATUS_AUTH_FAILED) zr[gi].push_back(i);
-                            continue;
-                        }
-                        const bool ok = core.update(c);
-                        status[i] = ok ? NEB_STATUS_OK : NEB_STATUS_REPLAY;
-                        if (ok && opened[i] == 2) cm[gi].push_back(i);
-                    }
-                    pos[r] = k;
-                });
-            }
-        });
-        std::vector<uint32_t> all, next;
-        for (auto& v : want) all.insert(all.end(), v.begin(), v.end());
-        for (uint32_t r : active)
-            if (pos[r] < runs[r].k1) next.push_back(r);
-        if (!all.empty()) {
-            // sets opened[] (1 in place, 2 speculative) and the verdicts of these packets
-            const int rc = speculative ? spec_fn(all) : open_fn(all);
-            if (rc != NEB_OK) return rc;
-            extra_opens++;
-            extra_pkts += (uint32_t)all.size();
-        }
-        active.swap(next);
-        rounds++;
-    }
-    for (uint32_t g = 0; g < ng; g++) {
-        commit->insert(commit->end(), cm[g].begin(), cm[g].end());
-        zero->insert(zero->end(), zr[g].begin(), zr[g].end());
-    }
-    if (stats)
-        std::fprintf(stderr, "rx exact: %zu windows, %u rounds, %u extra opens of %u packets\n", runs.size(), rounds,
-                     extra_opens, extra_pkts);
-    return NEB_OK;
-}
-
-}  // namespace
 
 struct neb_window {
     WindowCore core;
@@ -645,6 +367,8 @@ struct neb_dwindows {
     neb::RxDevWs ws{};
     uint32_t ws_n = 0;
     uint32_t* h_host = nullptr;  // pinned, mapped: the finish sets it when a window needs the host
+    uint8_t* wire_mem = nullptr;  // neb_rx_open_wire_batch: descriptors + gate statuses
+    uint32_t wire_n = 0;
 };
 
 namespace {
@@ -741,6 +465,7 @@ NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
         // throughout: with the lock taken, nothing of this window set is in flight
         std::lock_guard<std::mutex> g(d->mu);
         if (d->ws_mem) hipFree(d->ws_mem);
+        if (d->wire_mem) hipFree(d->wire_mem);
         if (d->mem) hipFree(d->mem);
         if (d->h_host) hipHostFree(d->h_host);
     }
@@ -782,13 +507,12 @@ NEB_API int neb_dwindows_store(neb_dwindows* d, uint32_t idx, neb_window* w) {
     return NEB_OK;
 }
 
-NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb_desc* d_desc, uint32_t n,
-                              uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream) {
-    if (!e || !d || d->e != e || (n && (!d_desc || !d_arena || !d_status))) return NEB_ERR_INVALID;
-    int rc = neb_check_batch_args(e, alg, key_hint);
-    if (rc != NEB_OK) return rc;
-    if (n == 0) return NEB_OK;
-    std::lock_guard<std::mutex> g(d->mu);
+}  // extern "C"
+
+// neb_rx_open_batch with d->mu held (the wire form builds its descriptors under the same lock)
+static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const neb_desc* d_desc, uint32_t n,
+                                uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream) {
+    int rc = NEB_OK;
     hipSetDevice(neb_engine_device_of(e));
     hipStream_t s = (hipStream_t)stream;
     auto& v = d->win;
@@ -977,6 +701,70 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
         if ((rc = dw_write(d, runs[r].w, cores[r])) != NEB_OK) return rc;
     if (rc != NEB_OK) return rc;
     RX_HIP(hipMemcpyAsync(d_status, status.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+    RX_HIP(hipStreamSynchronize(s));
+    return NEB_OK;
+}
+
+extern "C" {
+
+NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb_desc* d_desc, uint32_t n,
+                              uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream) {
+    if (!e || !d || d->e != e || (n && (!d_desc || !d_arena || !d_status))) return NEB_ERR_INVALID;
+    int rc = neb_check_batch_args(e, alg, key_hint);
+    if (rc != NEB_OK) return rc;
+    if (n == 0) return NEB_OK;
+    std::lock_guard<std::mutex> g(d->mu);
+    return rx_open_batch_locked(e, alg, d, d_desc, n, d_arena, d_status, key_hint, stream);
+}
+
+// readOutsidePackets' gate (neb_rx_wire_gate) on the host, then the batched receive over the
+// descriptors it builds; refused packets carry an empty descriptor with no key (untouched by the
+// receive) and get the gate's status.
+NEB_API int neb_rx_open_wire_batch_host(neb_engine* e, int alg, neb_window* const* windows, uint32_t nwindows,
+                                        const neb_rx_packet* pk, uint32_t n, uint8_t* arena, size_t arena_len,
+                                        int32_t* status, uint32_t key_hint) {
+    if (!e || (n && (!pk || !arena || !status || !windows))) return NEB_ERR_INVALID;
+    if (n == 0) return NEB_OK;
+    for (uint32_t i = 0; i < n; i++)  // every wire packet inside the arena (sums cannot wrap)
+        if (pk[i].off > arena_len || pk[i].len > arena_len - pk[i].off) return NEB_ERR_INVALID;
+    std::vector<neb_desc> desc(n);
+    std::vector<int32_t> gate(n);
+    for (uint32_t i = 0; i < n; i++) {
+        neb_desc dd{pk[i].off, pk[i].off, pk[i].off, 0, 0, 0, NEB_KEYS_MIXED, 0};
+        gate[i] = neb_rx_wire_gate(arena + pk[i].off, pk[i], &dd);
+        if (gate[i] != NEB_STATUS_OK) dd = neb_desc{pk[i].off, pk[i].off, pk[i].off, 0, 0, 0, NEB_KEYS_MIXED, 0};
+        desc[i] = dd;
+    }
+    const int rc = neb_rx_open_batch_host(e, alg, windows, nwindows, desc.data(), n, arena, arena_len, status, key_hint);
+    if (rc != NEB_OK) return rc;
+    for (uint32_t i = 0; i < n; i++)
+        if (gate[i] != NEB_STATUS_OK) status[i] = gate[i];
+    return NEB_OK;
+}
+
+NEB_API int neb_rx_open_wire_batch(neb_engine* e, int alg, neb_dwindows* d, const neb_rx_packet* d_pk, uint32_t n,
+                                   uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, void* stream) {
+    if (!e || !d || d->e != e || (n && (!d_pk || !d_arena || !d_status))) return NEB_ERR_INVALID;
+    int rc = neb_check_batch_args(e, alg, key_hint);
+    if (rc != NEB_OK) return rc;
+    if (n == 0) return NEB_OK;
+    std::lock_guard<std::mutex> g(d->mu);
+    hipSetDevice(neb_engine_device_of(e));
+    hipStream_t s = (hipStream_t)stream;
+    if (n > d->wire_n) {
+        RX_HIP(hipStreamSynchronize(s));
+        if (d->wire_mem) hipFree(d->wire_mem);
+        d->wire_mem = nullptr;
+        d->wire_n = 0;
+        RX_HIP(hipMalloc((void**)&d->wire_mem, (size_t)n * (sizeof(neb_desc) + 4)));
+        d->wire_n = n;
+    }
+    neb_desc* wd = (neb_desc*)d->wire_mem;
+    int32_t* gate = (int32_t*)(d->wire_mem + (size_t)d->wire_n * sizeof(neb_desc));
+    RX_HIP(neb_rxdev_wire(d_pk, n, d_arena, wd, gate, s));
+    rc = rx_open_batch_locked(e, alg, d, wd, n, d_arena, d_status, key_hint, stream);
+    if (rc != NEB_OK) return rc;
+    RX_HIP(neb_rxdev_wire_fix(gate, d_status, n, s));
     RX_HIP(hipStreamSynchronize(s));
     return NEB_OK;
 }

@@ -29,7 +29,7 @@ def _i64(x: int) -> int:
     return x - (1 << 64) if x >> 63 else x
 
 # status codes of the batched RX open (include/nebula_aead.h)
-OK, AUTH_FAILED, EXHAUSTED, BAD_KEY, REPLAY = 0, 1, 2, 3, 4
+OK, AUTH_FAILED, EXHAUSTED, BAD_KEY, REPLAY, INVALID, NOT_MESSAGE = 0, 1, 2, 3, 4, 5, 7
 
 
 class Bits:
@@ -136,3 +136,33 @@ def rx_sequential(windows, keys, counters, verdicts):
             continue
         status.append(OK if w.update(c) else REPLAY)
     return status, decrypted
+
+
+def read_outside_gate(packet: bytes, has_tunnel: bool):
+    """readOutsidePackets (outside.go:30-114) up to the decrypt, restated: h.Parse
+    (header.go:143-156), the version and IsValidSubType checks (header.go:192-205), the unencrypted
+    types handed elsewhere (outside.go:83-89), the hostinfo lookup (outside.go:94-106) and the size
+    check (outside.go:108-114). Returns (status, None) for a packet that stops here, or
+    (None, (kind, counter)) with kind "decrypt" (Decrypt, header as AD, in place) or "relay"
+    (VerifyRelay: AD = packet[:len-16], tag = the last 16 bytes)."""
+    if len(packet) < 16:
+        return INVALID, None
+    ver, typ, sub = packet[0] >> 4, packet[0] & 15, packet[1]
+    if ver != 1:
+        return INVALID, None
+    if typ in (1, 4):
+        valid = sub in (0, 1)
+    elif typ in (0, 2, 3, 5, 6):
+        valid = sub == 0
+    else:
+        valid = False
+    if not valid:
+        return INVALID, None
+    if typ in (0, 2):
+        return NOT_MESSAGE, None
+    if not has_tunnel:
+        return BAD_KEY, None
+    if len(packet) < 32:
+        return INVALID, None
+    counter = int.from_bytes(packet[8:16], "big")
+    return None, ("relay" if (typ == 1 and sub == 1) else "decrypt", counter)

@@ -9,7 +9,10 @@ Sources, in order of authority:
        RFC 8439 §2.8.2 ChaCha20-Poly1305 AEAD vector (x/crypto v0.54.0 chacha20poly1305)
   3. Batch digests for the BASELINE.json configs, produced by the plain-C oracle
      (oracle/aead_oracle.c) and independently re-derived with OpenSSL EVP
-     (oracle/evp_baseline.c); the script refuses to write if the two disagree.
+     (oracle/evp_baseline.c); the script refuses to write if the two disagree. Scaled batches
+     (tags committed) in batches.json, and the full C2-C5 batches (64 Ki x 1300 B; 1 Mi IMIX)
+     as SHA-256 digests of the whole sealed and opened arenas in full_digests.json
+     (`--no-full` skips them: about a minute on 8 cores).
 
 The Go reference itself cannot run here (no Go toolchain), so (3) is pinned by (1)+(2) through
 the oracle, not by Go output.
@@ -66,6 +69,54 @@ BATCHES = {
 }
 
 
+# the BASELINE.json configs at full size: only digests are committed. The script
+# refuses to write unless the plain-C oracle (multithreaded over disjoint packet ranges) and the
+# OpenSSL EVP port produce the same sealed arena byte for byte.
+FULL = {
+    "c2_full": lambda: W.config(1),
+    "c3_full": lambda: W.config(2),
+    "c4_full": lambda: W.config(3),
+    "c5_full": lambda: W.config(4),
+}
+
+
+def oracle_threaded(alg, open_flag, keys, desc, arena, threads=8):
+    """oracle.batch over `threads` disjoint descriptor ranges at once (ctypes drops the GIL)."""
+    import threading
+
+    st = np.zeros(len(desc), np.int32)
+    bounds = [len(desc) * t // threads for t in range(threads + 1)]
+
+    def run(t):
+        st[bounds[t]:bounds[t + 1]] = oracle.batch(alg, open_flag, keys, desc[bounds[t]:bounds[t + 1]], arena)
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    return st
+
+
+def full_digests(b):
+    sealed = b.arena.copy()
+    assert (oracle_threaded(b.alg, 0, b.keys, b.desc, sealed) == 0).all()
+    evp = b.arena.copy()
+    _, st = oracle.evp_batch(b.alg, 0, b.keys, b.desc, evp, threads=8)
+    assert (st == 0).all()
+    if not np.array_equal(sealed, evp):
+        raise SystemExit("oracle and OpenSSL EVP disagree on a full batch — refusing to write fixtures")
+    del evp
+    opened = sealed.copy()
+    assert (oracle_threaded(b.alg, 1, b.keys, b.desc, opened) == 0).all()
+    return {
+        "n": b.n, "nkeys": b.nkeys, "alg": b.alg, "stride": b.stride, "name": b.name,
+        "plain_sha256": hashlib.sha256(b.arena.tobytes()).hexdigest(),
+        "sealed_sha256": hashlib.sha256(sealed.tobytes()).hexdigest(),
+        "opened_sha256": hashlib.sha256(opened.tobytes()).hexdigest(),
+    }
+
+
 def sealed_digest(b):
     arena = b.arena.copy()
     st = oracle.batch(b.alg, 0, b.keys, b.desc, arena)
@@ -105,6 +156,15 @@ def main():
         print(name, meta[name]["sealed_sha256"][:16])
     with open(os.path.join(OUT, "batches.json"), "w") as f:
         json.dump(meta, f, indent=1)
+    if "--no-full" not in sys.argv:
+        full = {}
+        for name, mk in FULL.items():
+            b = mk()
+            full[name] = full_digests(b)
+            print(name, full[name]["sealed_sha256"][:16])
+            del b
+        with open(os.path.join(OUT, "full_digests.json"), "w") as f:
+            json.dump(full, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -3,6 +3,7 @@ noiseutil/fips140_test.go case by case (through nebula_amd.noiseutil -> C ABI ->
 import json
 import os
 
+import numpy as np
 import pytest
 
 from nebula_amd import noiseutil as N
@@ -137,3 +138,90 @@ def test_append_semantics(engine, cf):
     with pytest.raises(N.ErrOpen):  # ciphertext shorter than the tag
         cs.DecryptDanger(None, b"", b"0123456789", 9)
     cs.destroy()
+
+
+def test_concurrent_encrypt_decrypt_danger(engine, oracle_mod):
+    """EncryptDanger / DecryptDanger from 16 threads at once on shared CipherStates (Nebula calls
+    them from every routine, lock-free: noiseutil/notboring.go:12): each thread has its own slot
+    and stream in the engine, and every output equals the oracle's."""
+    import threading
+
+    from nebula_amd import _lib as L
+    from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
+
+    rng = np.random.default_rng(11)
+    states = []
+    for i in range(4):
+        cf = CipherAESGCM if i % 2 == 0 else CipherChaChaPoly
+        k = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        states.append((cf.Cipher(engine, k), k, L.ALG_AESGCM if i % 2 == 0 else L.ALG_CHACHAPOLY))
+    errors = []
+
+    def worker(t):
+        try:
+            r = np.random.default_rng(100 + t)
+            for j in range(150):
+                cs, k, alg = states[(t + j) % 4]
+                n = (t << 32) | j
+                pt = bytes(r.integers(0, 256, int(r.choice([0, 1, 100, 1300])), dtype=np.uint8))
+                ad = bytes(r.integers(0, 256, 16, dtype=np.uint8))
+                ct = cs.EncryptDanger(None, ad, pt, n).bytes()
+                ref = oracle_mod.seal(alg, k, oracle_mod.nonce(alg, n), ad, pt)
+                if ct != ref:
+                    raise AssertionError(f"seal mismatch t={t} j={j}")
+                if cs.DecryptDanger(None, ad, ct, n).bytes() != pt:
+                    raise AssertionError(f"open mismatch t={t} j={j}")
+        except Exception as ex:
+            errors.append(ex)
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    try:
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errors, errors[:3]
+    finally:
+        for cs, _, _ in states:
+            cs.destroy()
+
+
+def test_destroy_does_not_wait_for_another_tunnels_batch(engine, oracle_mod):
+    """neb_cipher_destroy waits only for batches that may read the destroyed key: with another
+    tunnel's long single-key batch still running on another stream, destroying a key whose batches
+    are done returns before that batch finishes (the old device-wide drain waited for it)."""
+    import time
+
+    import torch
+
+    from nebula_amd import workload as W
+    from nebula_amd.batch import DeviceBatch, install_keys
+    from nebula_amd.noiseutil import CipherAESGCM
+
+    b = W.make_batch(1, 65536, 1, name="long")
+    ciphers = install_keys(engine, b)
+    other = CipherAESGCM.Cipher(engine, bytes(range(32)))
+    try:
+        db = DeviceBatch(engine, b, ciphers)
+        s = torch.cuda.Stream()
+        db.seal(stream=s.cuda_stream)  # warm
+        s.synchronize()
+        ev_end = torch.cuda.Event()
+        with torch.cuda.stream(s):
+            x = torch.randn(4096, 4096, device="cuda")
+            for _ in range(8):  # a few ms ahead of the batch on its stream
+                x = x @ x
+            for _ in range(20):
+                db.seal(stream=s.cuda_stream)
+            ev_end.record(s)
+        t0 = time.perf_counter()
+        other.destroy()
+        dt = time.perf_counter() - t0
+        still_running = not ev_end.query()
+        s.synchronize()
+        assert still_running, "the other tunnel's batch finished before the destroy returned"
+        assert (db.status_host() == 0).all()
+        assert dt < 0.05, dt
+    finally:
+        for c in ciphers:
+            c.destroy()

@@ -570,3 +570,38 @@ def test_relay_gmac_batches(engine, oracle_mod, alg, nkeys):
     got, st = run_device(engine, mb, seal=True)
     assert (st == 0).all()
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name", ["c2_full", "c3_full", "c4_full", "c5_full"])
+def test_full_size_batches_match_oracle_digests(engine, name):
+    """Every BASELINE.json GPU config at full size (C2/C3/C4: 64 Ki x 1300 B, 1 and 4096 keys, both
+    ciphers; C5: 1 Mi IMIX packets over 4096 keys on one GPU): the whole sealed arena and the whole
+    opened arena hash to the digests the plain-C oracle and OpenSSL EVP agreed on
+    (tests/golden/full_digests.json, make_golden.py). Seal and open through the device batch path."""
+    import hashlib
+    import time
+
+    import torch
+    from nebula_amd.batch import DeviceBatch, install_keys
+    import make_golden
+
+    meta = json.load(open(os.path.join(GOLD, "full_digests.json")))[name]
+    t0 = time.time()
+    b = make_golden.FULL[name]()
+    assert (b.n, b.nkeys, b.alg, b.stride) == (meta["n"], meta["nkeys"], meta["alg"], meta["stride"])
+    assert hashlib.sha256(b.arena.tobytes()).hexdigest() == meta["plain_sha256"]
+    ciphers = install_keys(engine, b)
+    try:
+        db = DeviceBatch(engine, b, ciphers)
+        db.seal()
+        torch.cuda.synchronize()
+        assert (db.status_host() == 0).all()
+        assert hashlib.sha256(db.arena_host().tobytes()).hexdigest() == meta["sealed_sha256"]
+        db.open()
+        torch.cuda.synchronize()
+        assert (db.status_host() == 0).all()
+        assert hashlib.sha256(db.arena_host().tobytes()).hexdigest() == meta["opened_sha256"]
+    finally:
+        for c in ciphers:
+            c.destroy()
+    print(f"{name}: {b.n} packets, {time.time() - t0:.1f} s")

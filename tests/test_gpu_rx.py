@@ -522,3 +522,161 @@ def test_rx_concurrent_receives_on_one_engine(engine, oracle_mod):
             jb["buf"].free()
             for c in jb["ciphers"]:
                 c.destroy()
+
+
+def _wire_batch(oracle_mod, alg, keys, seed=3, n_rand=600):
+    """Wire packets of every kind readOutsidePackets meets (outside.go:30-133): messages, relayed
+    messages (GMAC over the AD), encrypted control types, unencrypted types, bad versions and
+    subtypes, runts, packets with no tunnel, forgeries, replays, a header whose counter was edited.
+    Returns (arena, packets [(off, len, tunnel or None)], plaintexts)."""
+    rng = random.Random(seed)
+    SL = 1600
+    items = []
+    ctr = {t: 2 for t in range(len(keys))}
+
+    def sealed(t, typ, sub, c, pt, relay=False):
+        hdr = bytes([(1 << 4) | typ, sub, 0, 0]) + (0x1000 + t).to_bytes(4, "big") + c.to_bytes(8, "big")
+        nb = oracle_mod.nonce(alg, c)
+        if relay:
+            ad = hdr + pt
+            return ad + oracle_mod.seal(alg, keys[t], nb, ad, b"")
+        return hdr + oracle_mod.seal(alg, keys[t], nb, hdr, pt)
+
+    fixed = []
+    for t in range(len(keys)):
+        for typ, sub in ((1, 0), (1, 1), (4, 0), (4, 1), (6, 0), (3, 0), (5, 0)):
+            ctr[t] += 1
+            pt = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 16, 100, 1300])))
+            fixed.append((sealed(t, typ, sub, ctr[t], pt, relay=(typ, sub) == (1, 1)), t))
+    hs = bytes([0x10, 0, 0, 0]) + bytes(60)           # handshake IXPSK0: left to the control plane
+    fixed += [(hs, 0), (bytes([0x12, 0]) + bytes(40), 1)]  # recv error
+    fixed += [(bytes([0x21, 0]) + bytes(40), 0)]        # version 2
+    fixed += [(bytes([0x11, 2]) + bytes(40), 0), (bytes([0x10, 1]) + bytes(40), 0), (bytes([0x17, 0]) + bytes(40), 0)]
+    fixed += [(b"", 0), (b"\x11", 0), (bytes([0x11, 0]) + bytes(13), 0)]  # runts (< 16: no header)
+    ctr[0] += 1
+    short = sealed(0, 1, 0, ctr[0], b"")[:31]             # a header and 15 bytes: under 16 + 16
+    fixed += [(short, 0)]
+    ctr[1] += 1
+    fixed += [(sealed(1, 1, 0, ctr[1], b"no tunnel"), None)]
+    ctr[2] += 1
+    edited = bytearray(sealed(2, 1, 0, ctr[2], b"x" * 200))
+    edited[15] ^= 1                                        # counter edited in flight: wrong nonce, wrong AD
+    fixed += [(bytes(edited), 2)]
+    # random traffic: messages, forgeries, replays of earlier packets
+    sent = []
+    for _ in range(n_rand):
+        t = rng.randrange(len(keys))
+        r = rng.random()
+        if r < 0.15 and sent:
+            fixed.append(rng.choice(sent))
+            continue
+        ctr[t] += 1 + (rng.random() < 0.1) * rng.randrange(1, 30)
+        relay = rng.random() < 0.1
+        pkt = bytearray(sealed(t, 1, 1 if relay else 0, ctr[t], bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 20, 576]))),
+                               relay=relay))
+        if rng.random() < 0.05:
+            pkt[rng.randrange(16, len(pkt))] ^= 1 << rng.randrange(8)
+        fixed.append((bytes(pkt), t))
+        sent.append((bytes(pkt), t))
+    rng.shuffle(fixed)
+    arena = np.zeros(len(fixed) * SL, np.uint8)
+    packets = []
+    for i, (pkt, t) in enumerate(fixed):
+        arena[i * SL:i * SL + len(pkt)] = np.frombuffer(pkt, np.uint8)
+        packets.append((i * SL, len(pkt), t))
+    return arena, packets
+
+
+def _wire_expected(oracle_mod, R, alg, keys, arena, packets, window_len):
+    wins = {t: R.Bits(window_len) for t in range(len(keys))}
+    for w in wins.values():
+        w.update(1)
+        w.update(2)
+    exp = arena.copy()
+    status = []
+    for off, ln, t in packets:
+        pkt = bytes(arena[off:off + ln])
+        st, go = R.read_outside_gate(pkt, t is not None)
+        if st is not None:
+            status.append(st)
+            continue
+        kind, c = go
+        w = wins[t]
+        if not w.check(c):
+            status.append(R.REPLAY)
+            continue
+        nb = oracle_mod.nonce(alg, c)
+        if kind == "relay":
+            ok = oracle_mod.open_(alg, keys[t], nb, pkt[:ln - 16], pkt[ln - 16:]) is not None
+        else:
+            pt = oracle_mod.open_(alg, keys[t], nb, pkt[:16], pkt[16:])
+            ok = pt is not None
+            exp[off + 16:off + ln - 16] = np.frombuffer(pt, np.uint8) if ok else 0
+        if not ok:
+            status.append(R.AUTH_FAILED)
+            continue
+        status.append(R.OK if w.update(c) else R.REPLAY)
+    return status, exp, wins
+
+
+@pytest.mark.parametrize("device", [False, True])
+@pytest.mark.parametrize("alg", [L.ALG_AESGCM, L.ALG_CHACHAPOLY])
+def test_rx_wire_gate_matches_read_outside_packets(engine, oracle_mod, alg, device):
+    """neb_rx_open_wire_batch[_host]: the header parse, version / subtype / size checks and the
+    header's counter as nonce on the engine's side, then Decrypt or VerifyRelay — statuses, every
+    arena byte and the windows equal the oracle's readOutsidePackets loop (oracle/replay_oracle.py
+    read_outside_gate + the sequential receive)."""
+    import replay_oracle as R
+    from nebula_amd.connection_state import (Bits, DeviceWindows, rx_open_wire_batch,
+                                             rx_open_wire_batch_device)
+    from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
+
+    rng = random.Random(alg * 5 + device)
+    keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(3)]
+    arena, packets = _wire_batch(oracle_mod, alg, keys, seed=alg + 2 * device)
+    exp_status, exp_arena, owins = _wire_expected(oracle_mod, R, alg, keys, arena, packets, 256)
+    cf = CipherAESGCM if alg == L.ALG_AESGCM else CipherChaChaPoly
+    ciphers = [cf.Cipher(engine, k) for k in keys]
+    try:
+        pk = np.zeros(len(packets), L.RX_PACKET_DTYPE)
+        for i, (off, ln, t) in enumerate(packets):
+            pk[i] = (off, ln, ciphers[t].key_id if t is not None else L.KEYS_MIXED)
+        ewins = []
+        for c in ciphers:
+            w = Bits(256)
+            w.Update(1)
+            w.Update(2)
+            ewins.append(w)
+        if device:
+            import torch
+            dev = torch.device("cuda", engine.device)
+            dw = DeviceWindows(engine, engine.max_keys, 256)
+            try:
+                for c, w in zip(ciphers, ewins):
+                    dw.load(c.key_id, w)
+                d_pk = torch.from_numpy(pk.view(np.uint8).copy()).to(dev)
+                d_arena = torch.from_numpy(arena).to(dev)
+                d_status = torch.full((len(pk),), -1, dtype=torch.int32, device=dev)
+                rx_open_wire_batch_device(engine, alg, dw, d_pk, d_arena, d_status)
+                torch.cuda.synchronize()
+                got = d_status.cpu().numpy()
+                arena = d_arena.cpu().numpy()
+                for c, w in zip(ciphers, ewins):
+                    dw.store(c.key_id, w)
+            finally:
+                dw.destroy()
+        else:
+            windows = [None] * engine.max_keys
+            for c, w in zip(ciphers, ewins):
+                windows[c.key_id] = w
+            got = rx_open_wire_batch(engine, alg, windows, pk, arena)
+        assert got.tolist() == exp_status
+        assert np.array_equal(arena, exp_arena)
+        for t, w in enumerate(ewins):
+            o = owins[t]
+            assert (w.current, w.lost, w.dupe, w.out_of_window) == (o.current, o.lost, o.dupe, o.out_of_window)
+        kinds = set(exp_status)
+        assert {R.OK, R.INVALID, R.NOT_MESSAGE, R.BAD_KEY, R.REPLAY, R.AUTH_FAILED} <= kinds, kinds
+    finally:
+        for c in ciphers:
+            c.destroy()

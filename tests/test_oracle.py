@@ -122,3 +122,22 @@ def test_oracle_matches_golden_batches(oracle_mod, name):
     assert hashlib.sha256(arena.tobytes()).hexdigest() == meta["sealed_sha256"]
     tags = np.load(os.path.join(GOLD, f"{name}_tags.npy"))
     assert hashlib.sha256(tags.tobytes()).hexdigest() == meta["tags_sha256"]
+
+
+def test_full_digest_inputs_are_reproducible():
+    """The full-size fixtures (tests/golden/full_digests.json) name their inputs by digest: the
+    deterministic generator must still produce exactly those plaintext arenas (C2-C4; C5's 1.4 GB
+    arena is checked on the GPU box, test_full_size_batches_match_oracle_digests)."""
+    import hashlib
+    import json
+    import os
+
+    from nebula_amd import workload as W
+
+    meta = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "full_digests.json")))
+    assert set(meta) == {"c2_full", "c3_full", "c4_full", "c5_full"}
+    for name, idx in (("c2_full", 1), ("c3_full", 2), ("c4_full", 3)):
+        b = W.config(idx)
+        assert b.n == meta[name]["n"] == 65536
+        assert hashlib.sha256(b.arena.tobytes()).hexdigest() == meta[name]["plain_sha256"], name
+    assert meta["c5_full"]["n"] == 1 << 20 and meta["c5_full"]["nkeys"] == 4096
