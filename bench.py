@@ -179,6 +179,10 @@ def main():
                          "rx-device: the same with the batch and the windows in device memory; relay: GMAC-only "
                          "seal+verify of 1348-B relayed packets (VerifyRelay), device-resident")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inproc", action="store_true",
+                    help="device mode, --gpus N engines in ONE process (Nebula is one process): each engine its "
+                         "own batch of the config's shape on its GPU (round-robin over the visible devices), "
+                         "all enqueued by one neb_*_batch_sharded call per step (SURVEY.md §8e)")
     ap.add_argument("--tx-superpackets", type=int, default=1457,
                     help="tx mode: 64 KiB TSO superpackets per batch (45 segments each; 1457 -> 65 565 wires, "
                          "1456 -> 65 520: within one pass of the 4096 waves of 16 packets)")
@@ -186,6 +190,8 @@ def main():
 
     from nebula_amd.shard import Control, dist_env
 
+    if args.inproc:
+        return bench_inproc(args)
     rank, world, local = dist_env()
     import torch
 
@@ -357,6 +363,73 @@ def main():
             log(f"cpu_baseline failed: {e!r}")
             out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
+
+
+def bench_inproc(args):
+    """--inproc: args.gpus engines in this one process, one per visible GPU (round-robin), each with
+    its own batch of the config's shape (weak scaling, as the one-process-per-GPU mode); each step
+    seals then opens every engine's batch through one neb_seal_batch_sharded / neb_open_batch_sharded
+    call (every shard enqueued on its engine's stream before any is waited for)."""
+    import ctypes as C
+
+    import torch
+
+    from nebula_amd import _lib as L
+    from nebula_amd import workload as W
+    from nebula_amd.batch import DeviceBatch, install_keys
+    from nebula_amd.noiseutil import Engine
+
+    cfg, m = args.config, args.gpus
+    ndev = max(1, torch.cuda.device_count())
+    spec = {1: (L.ALG_AESGCM, 65536, 1), 2: (L.ALG_AESGCM, 65536, 4096), 3: (L.ALG_CHACHAPOLY, 65536, 4096)}
+    engines, batches, ciphers, dbs = [], [], [], []
+    for k in range(m):
+        dev = k % ndev
+        torch.cuda.set_device(dev)
+        b = W.make_batch(*spec[cfg], seed=W.SEED ^ k, name=f"C{cfg + 1}") if cfg in spec else W.config(4)
+        e = Engine(dev, max_keys=4096)
+        cs = install_keys(e, b)
+        engines.append(e)
+        batches.append(b)
+        ciphers.append(cs)
+        dbs.append(DeviceBatch(e, b, cs))
+    streams = [torch.cuda.Stream(device=db.dev) for db in dbs]
+    arr = (L.Shard * m)()
+    for k, (e, db) in enumerate(zip(engines, dbs)):
+        arr[k] = L.Shard(e.handle.value, db.desc.data_ptr(), db.n, db.arena.data_ptr(), db.status.data_ptr(),
+                         streams[k].cuda_stream)
+    hint = dbs[0].key_hint
+    if any(db.key_hint != hint for db in dbs):
+        hint = L.KEYS_MIXED
+    alg = batches[0].alg
+
+    def step():
+        L.check(L.lib().neb_seal_batch_sharded(alg, arr, m, hint), "seal_sharded")
+        L.check(L.lib().neb_open_batch_sharded(alg, arr, m, hint), "open_sharded")
+
+    step()
+    assert all((db.status_host() == 0).all() for db in dbs)
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    dt = time.perf_counter() - t0
+    assert all((db.status_host() == 0).all() for db in dbs), "open failed inside the timed region"
+    payload = sum(float(b.payload_bytes) for b in batches)
+    print(json.dumps({
+        "metric": f"GiB/s device-resident seal+open, {m} engine(s) in one process (config {cfg + 1})",
+        "value": round(2 * payload * args.steps / dt / GIB, 3), "unit": "GiB/s", "n_gpus": min(m, ndev),
+        "engines": m, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"C{cfg + 1} per engine, {m} engine(s) over {ndev} visible device(s), one process, "
+                               "neb_*_batch_sharded (no collective)"},
+    }), flush=True)
+    for cs in ciphers:
+        for c in cs:
+            c.destroy()
+    for e in engines:
+        e.close()
 
 
 def bench_relay(args, ctrl, rank, world, device):

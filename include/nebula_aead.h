@@ -184,6 +184,34 @@ NEB_API int neb_seal_batch_host(neb_engine* e, int alg, const neb_desc* desc, ui
 NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, uint32_t n, uint8_t* arena,
                                 size_t arena_len, int32_t* status, uint32_t key_hint);
 
+/* ---- several GPUs in one process: contiguous shards, no collective ------------ */
+/* Packets are independent, so a batch shards by contiguous packet range over engines (one per GPU,
+ * or several on one GPU): shard k takes packets [n*k/m, n*(k+1)/m) of m engines. Every engine must
+ * hold the batch's keys at the same key_ids (install each tunnel key on every engine in the same
+ * order: neb_cipher_create hands out the lowest free slot). */
+/* Host-resident batch (the arena in host memory, pinned or not): one host thread per engine runs
+ * neb_seal_batch_host / neb_open_batch_host on its shard; returns when every shard is done, with
+ * the first failing shard's return code (the other shards still complete). */
+NEB_API int neb_seal_batch_host_multi(neb_engine* const* engines, uint32_t nengines, int alg, const neb_desc* desc,
+                                      uint32_t n, uint8_t* arena, size_t arena_len, int32_t* status,
+                                      uint32_t key_hint);
+NEB_API int neb_open_batch_host_multi(neb_engine* const* engines, uint32_t nengines, int alg, const neb_desc* desc,
+                                      uint32_t n, uint8_t* arena, size_t arena_len, int32_t* status,
+                                      uint32_t key_hint);
+/* Device-resident shards: shard k's descriptors, arena and statuses live on engine k's device
+ * (each shard's descriptors index its own arena); each is enqueued on its stream (NULL: the
+ * device's default stream) and the call returns once every shard is done. */
+typedef struct neb_shard {
+    neb_engine* e;
+    const neb_desc* d_desc;
+    uint32_t n;
+    uint8_t* d_arena;
+    int32_t* d_status;
+    void* stream;
+} neb_shard;
+NEB_API int neb_seal_batch_sharded(int alg, const neb_shard* shards, uint32_t nshards, uint32_t key_hint);
+NEB_API int neb_open_batch_sharded(int alg, const neb_shard* shards, uint32_t nshards, uint32_t key_hint);
+
 /* Pinned host memory (hipHostMalloc) for arenas that back the reference's batch.Arena
  * (overlay/batch/coalesce_core.go:142-169) so the batch path needs no bounce copy. */
 NEB_API int neb_host_alloc(size_t bytes, void** out);

@@ -96,12 +96,22 @@ SIGNATURES = {
                                     _u32]),
     "neb_rx_open_wire_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _u32]),
     "neb_rx_open_wire_batch": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
+    "neb_seal_batch_host_multi": (_i, [_vp, _u32, _i, _vp, _u32, _vp, _sz, _vp, _u32]),
+    "neb_open_batch_host_multi": (_i, [_vp, _u32, _i, _vp, _u32, _vp, _sz, _vp, _u32]),
+    "neb_seal_batch_sharded": (_i, [_i, _vp, _u32, _u32]),
+    "neb_open_batch_sharded": (_i, [_i, _vp, _u32, _u32]),
     "neb_queue_create": (_i, [_vp, _i, _i, _vp, C.POINTER(_vp)]),
     "neb_queue_destroy": (_i, [_vp]),
     "neb_queue_submit": (_i, [_vp, _vp, _u32, _vp, _sz, _vp]),
     "neb_queue_flush": (_i, [_vp]),
     "neb_queue_stats": (_i, [_vp, _vp]),
 }
+
+
+class Shard(C.Structure):
+    """neb_shard (include/nebula_aead.h): one engine's device-resident part of a sharded batch."""
+    _fields_ = [("e", C.c_void_p), ("d_desc", C.c_void_p), ("n", C.c_uint32), ("d_arena", C.c_void_p),
+                ("d_status", C.c_void_p), ("stream", C.c_void_p)]
 
 
 class QueueConfig(C.Structure):

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/nebula_aead.h"
@@ -1079,6 +1080,70 @@ NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnel
     }
     *nwires = nw;
     return NEB_OK;
+}
+
+// ---- several engines --------------------------------------------------------------
+
+static int batch_host_multi(neb_engine* const* engines, uint32_t m, int alg, int open, const neb_desc* desc,
+                            uint32_t n, uint8_t* arena, size_t arena_len, int32_t* status, uint32_t key_hint) {
+    if (!engines || m == 0 || (n && (!desc || !arena || !status))) return NEB_ERR_INVALID;
+    for (uint32_t k = 0; k < m; k++)
+        if (!engines[k]) return NEB_ERR_INVALID;
+    // every descriptor checked before any shard starts: an invalid batch touches nothing
+    for (uint32_t i = 0; i < n; i++)
+        if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
+    std::vector<int> rc(m, NEB_OK);
+    std::vector<std::thread> th;
+    for (uint32_t k = 1; k < m; k++) {
+        const uint32_t b = (uint32_t)((uint64_t)n * k / m), c = (uint32_t)((uint64_t)n * (k + 1) / m) - b;
+        th.emplace_back([&, k, b, c] {
+            rc[k] = batch_host(engines[k], alg, open, desc + b, c, arena, arena_len, status + b, key_hint);
+        });
+    }
+    rc[0] = batch_host(engines[0], alg, open, desc, (uint32_t)((uint64_t)n / m), arena, arena_len, status, key_hint);
+    for (auto& t : th) t.join();
+    for (int r : rc)
+        if (r != NEB_OK) return r;
+    return NEB_OK;
+}
+
+NEB_API int neb_seal_batch_host_multi(neb_engine* const* engines, uint32_t nengines, int alg, const neb_desc* desc,
+                                      uint32_t n, uint8_t* arena, size_t arena_len, int32_t* status,
+                                      uint32_t key_hint) {
+    return batch_host_multi(engines, nengines, alg, 0, desc, n, arena, arena_len, status, key_hint);
+}
+
+NEB_API int neb_open_batch_host_multi(neb_engine* const* engines, uint32_t nengines, int alg, const neb_desc* desc,
+                                      uint32_t n, uint8_t* arena, size_t arena_len, int32_t* status,
+                                      uint32_t key_hint) {
+    return batch_host_multi(engines, nengines, alg, 1, desc, n, arena, arena_len, status, key_hint);
+}
+
+static int batch_sharded(int alg, int open, const neb_shard* sh, uint32_t m, uint32_t key_hint) {
+    if (!sh || m == 0) return NEB_ERR_INVALID;
+    int rc = NEB_OK;
+    uint32_t launched = 0;
+    for (; launched < m && rc == NEB_OK; launched++)  // every shard queued first, then all waited for
+        rc = batch_device(sh[launched].e, alg, open, sh[launched].d_desc, sh[launched].n, sh[launched].d_arena,
+                          sh[launched].d_status, key_hint, sh[launched].stream);
+    for (uint32_t k = 0; k < launched; k++) {
+        if (!sh[k].e) continue;
+        hipSetDevice(sh[k].e->device);
+        const hipError_t err = hipStreamSynchronize((hipStream_t)sh[k].stream);
+        if (err != hipSuccess && rc == NEB_OK) {
+            set_error("sharded batch", err);
+            rc = NEB_ERR_HIP;
+        }
+    }
+    return rc;
+}
+
+NEB_API int neb_seal_batch_sharded(int alg, const neb_shard* shards, uint32_t nshards, uint32_t key_hint) {
+    return batch_sharded(alg, 0, shards, nshards, key_hint);
+}
+
+NEB_API int neb_open_batch_sharded(int alg, const neb_shard* shards, uint32_t nshards, uint32_t key_hint) {
+    return batch_sharded(alg, 1, shards, nshards, key_hint);
 }
 
 NEB_API int neb_host_alloc(size_t bytes, void** out) {

@@ -1,10 +1,10 @@
 // queue.cpp — the C ABI of the submission queue (include/nebula_aead.h): queue_core.hpp's state
-// machine over the engine. Staging is pinned, mapped host memory, each batch is one zero-copy
-// kernel launch on the queue's stream (its own mixed-key scheduler workspace), and a HIP event with
-// a system-scope release marks it done.
+// machine over the engine. Staging is pinned, mapped host memory; each batch is one zero-copy
+// kernel launch on its own stream (and mixed-key scheduler workspace).
 #include <hip/hip_runtime.h>
 
 #include <new>
+#include <vector>
 
 #include "queue_core.hpp"
 
@@ -19,18 +19,24 @@ int neb_engine_device_of(const neb_engine* e);
 
 namespace {
 
+// One stream and mixed-key scheduler workspace per staging batch: consecutive batches run
+// concurrently on the device (a small zero-copy batch is PCIe latency, not bandwidth). A batch is
+// done when its stream has drained: only that batch is ever on it (a staging batch is relaunched
+// only after every submitter has copied its results out), and a stream synchronize is what makes
+// the kernel's stores into the mapped staging visible to the host, as for the zero-copy host batch
+// (an event with a system-scope release was measured to leave a batch's statuses unwritten a few
+// times in 10^5 submissions under 64 threads).
 struct HipDev {
-    using Token = hipEvent_t;
+    using Token = uint32_t;  // the staging batch's index (its stream)
     neb_engine* e = nullptr;
     int alg = 0, open = 0;
-    hipStream_t stream = nullptr;
-    void* sched = nullptr;
-    int launch(neb_desc* desc, uint32_t n, uint8_t* arena, int32_t* status, uint32_t hint, Token& ev) {
-        int rc = neb_launch_on(e, alg, open, desc, n, arena, status, hint, stream, sched);
-        if (rc == NEB_OK && hipEventRecord(ev, stream) != hipSuccess) rc = NEB_ERR_HIP;
-        return rc;
+    std::vector<hipStream_t> stream;
+    std::vector<void*> sched;
+    int launch(uint32_t i, neb_desc* desc, uint32_t n, uint8_t* arena, int32_t* status, uint32_t hint, Token& tok) {
+        tok = i;
+        return neb_launch_on(e, alg, open, desc, n, arena, status, hint, stream[i], sched[i]);
     }
-    int wait(Token& ev) { return hipEventSynchronize(ev) == hipSuccess ? NEB_OK : NEB_ERR_HIP; }
+    int wait(Token& tok) { return hipStreamSynchronize(stream[tok]) == hipSuccess ? NEB_OK : NEB_ERR_HIP; }
     bool key_ok(uint32_t key) { return neb_key_alg(e, key) == alg; }
 };
 
@@ -55,17 +61,19 @@ NEB_API int neb_queue_create(neb_engine* e, int alg, int open, const neb_queue_c
     q->cfg = c;
     hipSetDevice(neb_engine_device_of(e));
     q->b.resize(c.depth);
-    bool ok = hipStreamCreateWithFlags(&q->dev.stream, hipStreamNonBlocking) == hipSuccess;
-    q->dev.sched = ok ? neb_sched_space_new() : nullptr;
-    ok = ok && q->dev.sched;
+    q->dev.stream.assign(c.depth, nullptr);
+    q->dev.sched.assign(c.depth, nullptr);
+    bool ok = true;
+    for (uint32_t i = 0; i < c.depth; i++) {
+        ok = ok && hipStreamCreateWithFlags(&q->dev.stream[i], hipStreamNonBlocking) == hipSuccess;
+        q->dev.sched[i] = ok ? neb_sched_space_new() : nullptr;
+        ok = ok && q->dev.sched[i];
+    }
     for (auto& x : q->b) {
         ok = ok && hipHostMalloc((void**)&x.arena, c.arena_bytes, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipHostMalloc((void**)&x.desc, (size_t)c.max_packets * sizeof(neb_desc), hipHostMallocDefault) ==
                        hipSuccess;
         ok = ok && hipHostMalloc((void**)&x.status, (size_t)c.max_packets * 4, hipHostMallocDefault) == hipSuccess;
-        // release-to-system: the kernel's stores into the mapped staging are visible to the host
-        // once the event completes
-        ok = ok && hipEventCreateWithFlags(&x.tok, hipEventDisableTiming | hipEventReleaseToSystem) == hipSuccess;
     }
     if (!ok) {
         neb_queue_destroy(q);
@@ -80,15 +88,16 @@ NEB_API int neb_queue_destroy(neb_queue* q) {
     if (!q) return NEB_ERR_INVALID;
     q->shutdown();
     hipSetDevice(neb_engine_device_of(q->dev.e));
-    if (q->dev.stream) hipStreamSynchronize(q->dev.stream);
+    for (hipStream_t st : q->dev.stream)
+        if (st) hipStreamSynchronize(st);
     for (auto& x : q->b) {
         if (x.arena) hipHostFree(x.arena);
         if (x.desc) hipHostFree(x.desc);
         if (x.status) hipHostFree(x.status);
-        if (x.tok) hipEventDestroy(x.tok);
     }
-    neb_sched_space_free(q->dev.sched);
-    if (q->dev.stream) hipStreamDestroy(q->dev.stream);
+    for (void* sp : q->dev.sched) neb_sched_space_free(sp);
+    for (hipStream_t st : q->dev.stream)
+        if (st) hipStreamDestroy(st);
     delete q;
     return NEB_OK;
 }

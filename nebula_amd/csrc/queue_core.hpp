@@ -70,7 +70,8 @@ inline bool normalize(neb_queue_config& c) {
 
 // The queue's state machine over a device policy Dev:
 //   Dev::Token                               a completion marker per staging batch
-//   int  launch(desc, n, arena, status, key_hint, Token&)  queue one batch (in launch order)
+//   int  launch(i, desc, n, arena, status, key_hint, Token&)  queue staging batch i (in launch
+//                                            order; batches may run concurrently on the device)
 //   int  wait(Token&)                        block until that batch is done and visible
 //   bool key_ok(key)                         the key is installed for the queue's algorithm
 // queue.cpp binds it to the engine (zero-copy kernels on pinned staging, HIP events); the
@@ -128,7 +129,7 @@ struct Queue {
             // one tunnel's packets run the single-key kernel, if that key is installed for this
             // algorithm (otherwise the mixed path reports NEB_STATUS_BAD_KEY per packet)
             if (hint != NEB_KEYS_MIXED && !dev.key_ok(hint)) hint = NEB_KEYS_MIXED;
-            const int rc = dev.launch(x.desc, n, x.arena, x.status, hint, x.tok);
+            const int rc = dev.launch(next_launch, x.desc, n, x.arena, x.status, hint, x.tok);
             lk.lock();
             x.rc = rc;
             x.state = BState::kLaunched;

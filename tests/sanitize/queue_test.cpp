@@ -67,7 +67,7 @@ struct CpuDev {
         cv.notify_all();
         th.join();
     }
-    int launch(neb_desc* desc, uint32_t n, uint8_t* arena, int32_t* status, uint32_t hint, Token& tok) {
+    int launch(uint32_t, neb_desc* desc, uint32_t n, uint8_t* arena, int32_t* status, uint32_t hint, Token& tok) {
         tok = std::make_shared<Job>();
         Token t = tok;
         const int a = alg, o = open;
