@@ -312,7 +312,8 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
     e->key_use.resize(max_keys);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess ||
-        hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess) {
+        hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess ||
+        hipStreamSynchronize(nullptr) != hipSuccess) {  // the null-stream memset, before any stream reads keys
         set_error("engine allocation", hipGetLastError());
         neb_engine_destroy(e);
         return NEB_ERR_HIP;
@@ -479,8 +480,11 @@ static void fill_nonce(int alg, uint64_t n, uint8_t* nb) {
     for (int i = 0; i < 8; i++) nb[4 + i] = alg == NEB_ALG_AESGCM ? (uint8_t)(n >> (56 - 8 * i)) : (uint8_t)(n >> (8 * i));
 }
 
-// Size the scheduler workspace for n packets (caller holds sched.mu).
-static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
+// Size the scheduler workspace for n packets (caller holds sched.mu). The counters are cleared on
+// the batch's own stream: a plain hipMemset runs on the null stream, which a non-blocking stream
+// does not wait for, and may still be running when the binning starts (measured: the first batches
+// of a queue lost most of their packets' statuses to it).
+static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipStream_t s) {
     if (!sp.done) {
         hipError_t err = hipEventCreateWithFlags(&sp.done, hipEventDisableTiming);
         if (err != hipSuccess) return err;
@@ -488,7 +492,8 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     if (n <= sp.n_cap && sp.mem && !sp.dirty) return hipSuccess;
     if (n <= sp.n_cap && sp.mem) {  // the bins are cleared as they are consumed, except after a failure
         hipError_t err = hipEventSynchronize(sp.done);
-        if (err == hipSuccess) err = hipMemset(sp.ws.counters, 0, (neb::kSchedCounters + 2u * neb::sched_nbins(e->max_keys)) * 4u);
+        if (err == hipSuccess)
+            err = hipMemsetAsync(sp.ws.counters, 0, (neb::kSchedCounters + 2u * neb::sched_nbins(e->max_keys)) * 4u, s);
         if (err == hipSuccess) sp.dirty = false;
         return err;
     }
@@ -523,7 +528,7 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n) {
     sp.ws.max_chunks = mc;
     sp.bytes = bytes;
     sp.n_cap = cap;
-    err = hipMemset(sp.ws.counters, 0, b_counters);  // once: the binning clears its counts as it uses them
+    err = hipMemsetAsync(sp.ws.counters, 0, b_counters, s);  // once: the binning clears its counts as it uses them
     if (err != hipSuccess) return err;
     sp.dirty = false;
     return hipSuccess;
@@ -542,7 +547,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
-        hipError_t err = sched_reserve(e, sp, n);
+        hipError_t err = sched_reserve(e, sp, n, s);
         if (err == hipSuccess) err = hipStreamWaitEvent(s, sp.done, 0);
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)

@@ -22,10 +22,8 @@ namespace {
 // One stream and mixed-key scheduler workspace per staging batch: consecutive batches run
 // concurrently on the device (a small zero-copy batch is PCIe latency, not bandwidth). A batch is
 // done when its stream has drained: only that batch is ever on it (a staging batch is relaunched
-// only after every submitter has copied its results out), and a stream synchronize is what makes
-// the kernel's stores into the mapped staging visible to the host, as for the zero-copy host batch
-// (an event with a system-scope release was measured to leave a batch's statuses unwritten a few
-// times in 10^5 submissions under 64 threads).
+// only after every submitter has copied its results out), and the stream synchronize makes the
+// kernel's stores into the mapped staging visible to the host, as for the zero-copy host batch.
 struct HipDev {
     using Token = uint32_t;  // the staging batch's index (its stream)
     neb_engine* e = nullptr;

@@ -400,6 +400,8 @@ int dw_write(neb_dwindows* d, uint32_t w, const WindowCore& c) {
     RX_HIP(hipMemcpy(v.oow + w, &c.out_of_window, 8, hipMemcpyHostToDevice));
     RX_HIP(hipMemcpy(v.bits + (size_t)w * v.words, c.words.data(), (size_t)v.words * 8, hipMemcpyHostToDevice));
     RX_HIP(hipMemcpy(v.present + w, &one, 4, hipMemcpyHostToDevice));
+    // null-stream copies: complete before a non-blocking stream's batch reads the slot
+    RX_HIP(hipStreamSynchronize(nullptr));
     return NEB_OK;
 }
 
@@ -430,7 +432,8 @@ NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, 
     while ((1u << v.words_lg) < v.words) v.words_lg++;
     const size_t b_present = neb::rx_align((size_t)count * 4), b_word = neb::rx_align((size_t)count * 8);
     const size_t bytes = b_present + 4 * b_word + (size_t)count * v.words * 8;
-    if (hipMalloc((void**)&d->mem, bytes) != hipSuccess || hipMemset(d->mem, 0, bytes) != hipSuccess) {
+    if (hipMalloc((void**)&d->mem, bytes) != hipSuccess || hipMemset(d->mem, 0, bytes) != hipSuccess ||
+        hipStreamSynchronize(nullptr) != hipSuccess) {
         if (d->mem) hipFree(d->mem);
         delete d;
         return NEB_ERR_HIP;
@@ -480,6 +483,7 @@ NEB_API int neb_dwindows_load(neb_dwindows* d, uint32_t idx, const neb_window* w
     if (!w) {
         const uint32_t zero = 0;
         RX_HIP(hipMemcpy(d->win.present + idx, &zero, 4, hipMemcpyHostToDevice));
+        RX_HIP(hipStreamSynchronize(nullptr));
         return NEB_OK;
     }
     WindowCore c;

@@ -136,3 +136,34 @@ def test_queue_failures_and_bad_descriptors(engine, oracle_mod):
         oq.close()
         for c in ciphers:
             c.destroy()
+
+
+def test_queue_first_batches_of_fresh_queues(engine, oracle_mod):
+    """The first batch of a new queue runs on a freshly allocated scheduler workspace: its counters
+    are cleared on the batch's own stream, before the binning (a null-stream clear raced the first
+    mixed-key batches and left most of their statuses unwritten). Fresh queues, one full mixed-key
+    batch each, seal then open, against the oracle."""
+    from nebula_amd.batch import SubmitQueue, install_keys, slot_desc
+
+    b = W.make_batch(L.ALG_AESGCM, 8192, 64, sizes=(90, 576, 1300), ratio=(7, 4, 1), seed=81, name="qfresh")
+    ref = b.arena.copy()
+    assert (oracle_mod.batch(L.ALG_AESGCM, 0, b.keys, b.desc, ref) == 0).all()
+    ciphers = install_keys(engine, b)
+    try:
+        d = slot_desc(b, ciphers)
+        for rep in range(6):
+            sq = SubmitQueue(engine, L.ALG_AESGCM, False, max_packets=8192, max_delay_us=100000)
+            oq = SubmitQueue(engine, L.ALG_AESGCM, True, max_packets=8192, max_delay_us=100000)
+            try:
+                a = b.arena.copy()
+                st = sq.submit(d, a)
+                assert (st == 0).all(), (rep, int((st != 0).sum()), int(st[st != 0][0]))
+                assert np.array_equal(a, ref), rep
+                st = oq.submit(d, a)
+                assert (st == 0).all(), (rep, int((st != 0).sum()), int(st[st != 0][0]))
+            finally:
+                sq.close()
+                oq.close()
+    finally:
+        for c in ciphers:
+            c.destroy()
