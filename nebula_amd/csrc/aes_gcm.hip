@@ -1151,24 +1151,9 @@ struct ChunkLds {
 //   shoup[t][v] = v·H^(e_t), t < 4: e = 1, 2, 3, 4 (FULL) or 1, 2, 4, 8 (tails)
 //   pos[r][v]   = v·x^(4r)·P, r < 8, P = H^(2^lg): XOR of the basis P·x^(4r+j) over the set bits
 //                 of v (bit 3 ↔ j = 0), the basis P·x^i (i < 32) one per lane and shuffled
-#ifndef NEB_CHUNK_TABLES_COPY
-#define NEB_CHUNK_TABLES_COPY 0  // A/B: 1 copies the record's precomputed tables instead (3 KiB per chunk)
-#endif
 template <bool FULL>
 __device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t lane, uint32_t lg, uint4* wtab,
                                                    uint4* wpos) {
-#if NEB_CHUNK_TABLES_COPY
-    if (FULL) {
-        wtab[lane] = ld_rec4(rec, kRecShoup + 4u * lane);
-    } else {
-        const uint32_t t = lane >> 4;  // 0, 1, 3, 7
-        wtab[lane] = ld_rec4(rec, kRecShoup + 64u * ((1u << t) - 1u) + 4u * (lane & 15u));
-    }
-    const uint32_t pt = rec_pos_table(lg);
-    wpos[lane] = ld_rec4(rec, pt + 4u * lane);
-    wpos[64u + lane] = ld_rec4(rec, pt + 4u * (64u + lane));
-    return;
-#endif
     const uint32_t t = lane >> 4, v = lane & 15u;
     const uint32_t e = FULL ? t + 1u : 1u << t;
     const uint4 he = ld_rec4(rec, kRecHPow + 4u * (e - 1u));
