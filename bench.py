@@ -14,7 +14,8 @@ roofline: the seal kernel's algorithmic bytes (2p+32 per packet) / its mean laun
 events recorded on the kernel's stream inside the timed region; traffic = PMC-measured HBM bytes
 per launch of this config's seal kernel from profiles/pmc_configs.json, else null.
 cpu_baseline: rank 0, N = 1 only, the OpenSSL-EVP port of the per-packet loop (oracle/) on a
-bounded sample of the same batch, on every CPU of this process's affinity and on one thread.
+bounded sample of the same batch: the best of a thread sweep up to every CPU of this process's
+affinity, and one thread.
 """
 from __future__ import annotations
 
@@ -91,12 +92,48 @@ class TimingEvent:
         return float(ms.value)
 
 
-def cpu_cores() -> int:
-    """Every CPU this process may run on (sched_getaffinity): the whole host share the box grants."""
+def cgroup_cpus():
+    """The CPU bandwidth quota of this process's cgroup, in CPUs (cgroup v2 cpu.max, else v1
+    cfs_quota/cfs_period), or None when unlimited. A box may show every CPU of the machine in the
+    affinity mask while the quota grants a share of them."""
+    import math
+
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        rel = ""
+        for line in open("/proc/self/cgroup"):
+            parts = line.strip().split(":", 2)
+            if len(parts) == 3 and parts[0] == "0":
+                rel = parts[2]
+        for base in (os.path.join("/sys/fs/cgroup", rel.lstrip("/")), "/sys/fs/cgroup"):
+            f = os.path.join(base, "cpu.max")
+            if os.path.exists(f):
+                q, per = open(f).read().split()[:2]
+                return None if q == "max" else max(1, math.ceil(int(q) / int(per)))
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_cores() -> int:
+    """The CPUs this process may run on: the affinity mask (sched_getaffinity), capped by the
+    cgroup's CPU quota when it has one. NEB_CPU_THREADS overrides."""
+    if os.environ.get("NEB_CPU_THREADS"):
+        return max(1, int(os.environ["NEB_CPU_THREADS"]))
+    try:
+        n = max(1, len(os.sched_getaffinity(0)))
     except Exception:
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cgroup_cpus()
+    return min(n, q) if q else n
+
+
+def cpu_thread_counts(n: int):
+    """Thread counts the CPU baseline sweeps up to n (every CPU of the affinity mask): on the GPU box
+    the mask lists the whole machine (256) while the box's share of it is smaller, and 256 threads
+    ran at 1.9 GiB/s against 3.4 on one, so the best of the sweep is the baseline."""
+    return sorted({c for c in (8, 16, 32, 64, n) if c <= n} or {n})
 
 
 def cpu_baseline(b, target_s: float = 4.0):
@@ -133,7 +170,11 @@ def cpu_baseline(b, target_s: float = 4.0):
         assert (st2 == 0).all()
         return 2 * payload * iters / (t_seal + t_open) / GIB, iters, t_seal + t_open
 
-    gibs, iters, tt = rate(threads, target_s)
+    sweep = {}
+    for c in cpu_thread_counts(threads):
+        sweep[c] = rate(c, target_s / 2)
+    best = max(sweep, key=lambda c: sweep[c][0])
+    gibs, iters, tt = sweep[best]
     gibs1, iters1, tt1 = rate(1, target_s / 3)
     model = "unknown"
     try:
@@ -144,11 +185,13 @@ def cpu_baseline(b, target_s: float = 4.0):
     except Exception:
         pass
     return {
-        "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": best, "kind": "port",
         "value_1thread": round(gibs1, 3),
+        "sweep": {str(c): round(v[0], 3) for c, v in sweep.items()},
+        "affinity_cpus": threads,
         "sample": f"{n} packets of the same batch ({payload / 1e6:.1f} MB payload), seal x{iters} + open x{iters} "
-                  f"({tt:.1f} s) on {threads} pinned threads (every CPU of this process's affinity), and "
-                  f"x{iters1} on 1 thread ({tt1:.1f} s); OpenSSL EVP "
+                  f"({tt:.1f} s) on {best} pinned threads, the best of a sweep up to all {threads} CPUs of this "
+                  f"process's affinity ('sweep'), and x{iters1} on 1 thread ({tt1:.1f} s); OpenSSL EVP "
                   f"{'AES-256-GCM' if b.alg == 1 else 'ChaCha20-Poly1305'} (AES-NI/VAES + PCLMUL class, as Go's "
                   f"crypto/cipher), {model}",
     }

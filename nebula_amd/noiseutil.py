@@ -107,6 +107,7 @@ class Engine:
         self.handle = h
         self.device = device
         self.max_keys = max_keys
+        self.live = {}  # id -> CipherState: the keys installed and not yet destroyed
 
     def close(self) -> None:
         if self.handle:
@@ -141,7 +142,9 @@ class CipherFunc:
         h = C.c_void_p()
         L.check(L.lib().neb_cipher_create(engine.handle, self.alg, bytes(k), C.byref(h)), "neb_cipher_create")
         cls = CipherStateAESGCM if self.alg == L.ALG_AESGCM else CipherStateChaChaPoly
-        return cls(h, engine)
+        cs = cls(h, engine)
+        engine.live[id(cs)] = cs
+        return cs
 
 
 CipherAESGCM = CipherFunc("AESGCM", L.ALG_AESGCM)
@@ -169,6 +172,8 @@ class CipherState:
         if self.handle:
             L.lib().neb_cipher_destroy(self.handle)
             self.handle = None
+            if self.engine is not None:
+                self.engine.live.pop(id(self), None)
 
     def Overhead(self) -> int:
         return int(L.lib().neb_overhead(self.handle))

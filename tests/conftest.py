@@ -29,3 +29,20 @@ def engine():
     e = Engine(0, max_keys=8192)
     yield e
     e.close()
+
+
+@pytest.fixture(autouse=True)
+def _no_leaked_keys(request):
+    """A test that leaves keys installed on the shared engine would shrink the key table for every
+    later test (C3/C5 need 4096 slots): destroy what it left and report it."""
+    yield
+    if "engine" not in request.fixturenames:
+        return
+    e = request.getfixturevalue("engine")
+    left = list(e.live.values())
+    for cs in left:
+        cs.destroy()
+    if left:
+        import warnings
+
+        warnings.warn(f"{request.node.nodeid} left {len(left)} keys installed (destroyed)")

@@ -45,6 +45,8 @@ def test_dispatch_and_unsupported(engine):  # cipher_state_test.go:23-49
     with pytest.raises(RuntimeError):
         N.NewCipherState((engine, KEY), N.CipherFunc("Fake", 99))
     assert N.CipherAESGCM.CipherName() == "AESGCM" and N.CipherChaChaPoly.CipherName() == "ChaChaPoly"
+    for cs in list(engine.live.values()):
+        cs.destroy()
 
 
 @pytest.mark.parametrize("cf", [N.CipherAESGCM, N.CipherChaChaPoly], ids=["AESGCM", "ChaChaPoly"])
@@ -56,6 +58,8 @@ def test_encrypt_rejects_exhausted_counter(engine, cf):  # cipher_state_test.go:
     enc.EncryptDanger(None, None, b"x", N.RejectAfterMessages - 1, nb)
     with pytest.raises(N.ErrMessageCounterExhausted):
         enc.EncryptDanger(None, None, b"x", N.RejectAfterMessages, nb)
+    for cs in list(engine.live.values()):
+        cs.destroy()
 
 
 def test_nil_safety():  # cipher_state_test.go:176-192
@@ -94,6 +98,8 @@ def test_in_place_decrypt(engine, cf):  # cipher_state_test.go:194-237
     out = dec.DecryptDanger(packet[hdr_len:hdr_len], packet[:hdr_len], packet[hdr_len:], 1, nb)
     assert out.bytes() == plaintext
     assert out.same_element(packet[hdr_len:])  # plaintext aliases the packet buffer
+    enc.destroy()
+    dec.destroy()
 
 
 def test_reference_aesgcm_kat_through_encrypt_danger(engine):  # fips140_test.go:13-31

@@ -539,6 +539,8 @@ def test_cipher_destroy_waits_for_queued_batches(engine, oracle_mod):
         assert again.key_id == slot
     finally:
         again.destroy()
+        for c in ciphers[1:]:
+            c.destroy()
 
 
 @pytest.mark.parametrize("alg,nkeys", [(L.ALG_AESGCM, 1), (L.ALG_AESGCM, 64), (L.ALG_CHACHAPOLY, 64)])
