@@ -486,7 +486,9 @@ static void fill_nonce(int alg, uint64_t n, uint8_t* nb) {
 // of a queue lost most of their packets' statuses to it).
 static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipStream_t s) {
     if (!sp.done) {
-        hipError_t err = hipEventCreateWithFlags(&sp.done, hipEventDisableTiming);
+        // ordering only (the host and other streams wait for the kernels, nobody reads the
+        // workspace from the host): no system-scope cache release at each record
+        hipError_t err = hipEventCreateWithFlags(&sp.done, hipEventDisableTiming | hipEventDisableSystemFence);
         if (err != hipSuccess) return err;
     }
     if (n <= sp.n_cap && sp.mem && !sp.dirty) return hipSuccess;
@@ -548,7 +550,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
         hipError_t err = sched_reserve(e, sp, n, s);
-        if (err == hipSuccess) err = hipStreamWaitEvent(s, sp.done, 0);
+        if (err == hipSuccess) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,

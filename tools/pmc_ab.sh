@@ -1,19 +1,25 @@
 #!/bin/bash
-# One LDS counter pass per build_abl variant on the C2 bench (GPU box): bank conflicts, LDS-array
-# cycles, CU-busy cycles, LDS and VALU instruction counts of the single-key kernels.
+# One counter pass per variant (the product build "base" or build_abl/<name>) over a bench config,
+# condensed to gpurun_out/pmc_ab/<variant>.json (per kernel, the mean of each counter).
+#   tools/pmc_ab.sh "<variants>" "<counters (one pass: <= 8 SQ, <= 4 TCC)>" "<bench args>"
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/pmc_ab; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-for v in $(cat $R/build_abl/variants.txt); do
-  OUT=$R/gpurun_out/pmcab_$v; mkdir -p $OUT
-  NEB_LIB_PATH=$R/build_abl/lib_$v.so timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_BUSY_CU_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU SQ_LDS_CMD_FIFO_FULL --output-format csv -d $OUT -o lds -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/run.log 2>&1 || exit 1
-  python3 - $OUT <<'PY'
-import csv, glob, sys, collections
+for v in $1; do
+    if [ "$v" = base ]; then unset NEB_LIB_PATH; else export NEB_LIB_PATH=$R/build_abl/$v/libnebula_aead.so; fi
+    rm -rf $OUT/raw_$v
+    timeout -s KILL 120 rocprofv3 --pmc $2 --output-format csv -d $OUT/raw_$v -o p -- python3 $R/bench.py --no-cpu-baseline $3 > $OUT/$v.log 2>&1 || { echo "$v rc=$?"; tail -5 $OUT/$v.log; exit 1; }
+    python3 - "$OUT/raw_$v" "$OUT/$v.json" <<'PY'
+import collections, csv, glob, json, sys
 f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
-v = collections.defaultdict(list)
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(f)):
-    if "single_kernel<false>" in r["Kernel_Name"]:
-        v[r["Counter_Name"]].append(float(r["Counter_Value"]))
-m = {k: sum(x) / len(x) for k, x in v.items()}
-print(sys.argv[1].split("_")[-1], {k: round(x / 1e6, 2) for k, x in m.items()}, "lds_busy", round(m["SQ_LDS_IDX_ACTIVE"] / m["SQ_BUSY_CU_CYCLES"], 3))
+    vals[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {k: {c: sum(x) / len(x) for c, x in cs.items()} for k, cs in vals.items()}
+json.dump(out, open(sys.argv[2], "w"), indent=1, sort_keys=True)
+for k, cs in out.items():
+    if "chunk_kernel<false>" in k or "single_kernel<false, false>" in k:
+        print(sys.argv[2].split("/")[-1], k[:40], {c: round(v) for c, v in cs.items()})
 PY
+    rm -rf $OUT/raw_$v
 done
