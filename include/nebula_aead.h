@@ -369,7 +369,10 @@ NEB_API int neb_queue_destroy(neb_queue* q);
  * they are done: the arena bytes and statuses are those of neb_seal_batch_host / neb_open_batch_host
  * on the same descriptors. Thread-safe, meant to be called by many threads at once. Every
  * descriptor is checked against arena_len first (NEB_ERR_INVALID: nothing touched). A submission
- * larger than one batch goes through in pieces. */
+ * larger than one batch goes through in pieces. An arena from neb_host_alloc (pinned, mapped) is
+ * not copied: only its descriptors are staged and the kernels work on its bytes in place
+ * (zero-copy), so it must stay allocated until the call returns; any other memory is copied
+ * into the queue's staging and back. */
 NEB_API int neb_queue_submit(neb_queue* q, const neb_desc* desc, uint32_t n, uint8_t* arena, size_t arena_len,
                              int32_t* status);
 /* Send the batch being filled to the device now, without waiting for its deadline. */

@@ -720,6 +720,7 @@ int neb_launch_on(neb_engine* e, int alg, int open, const neb_desc* desc, uint32
     }
     return NEB_OK;
 }
+bool neb_host_mapped(const void* p);
 int neb_key_alg(neb_engine* e, uint32_t key) {
     std::lock_guard<std::mutex> g(e->key_mu);
     return key < e->max_keys ? e->slot_alg[key] : 0;
@@ -734,6 +735,7 @@ static bool host_mapped(const void* p) {
     }
     return a.type == hipMemoryTypeHost && a.devicePointer == p;
 }
+bool neb_host_mapped(const void* p) { return host_mapped(p); }  // queue.cpp
 
 // Zero-copy host batch: the arena is pinned and mapped, so the kernels load and store it across
 // PCIe themselves (loads = the H2D direction, stores = D2H, both at once) with no staging copies.

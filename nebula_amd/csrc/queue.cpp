@@ -15,6 +15,7 @@ int neb_launch_on(neb_engine* e, int alg, int open, const neb_desc* desc, uint32
                   int32_t* status, uint32_t key_hint, hipStream_t s, void* sched);
 int neb_key_alg(neb_engine* e, uint32_t key);
 int neb_engine_device_of(const neb_engine* e);
+bool neb_host_mapped(const void* p);
 }
 
 namespace {
@@ -36,6 +37,7 @@ struct HipDev {
     }
     int wait(Token& tok) { return hipStreamSynchronize(stream[tok]) == hipSuccess ? NEB_OK : NEB_ERR_HIP; }
     bool key_ok(uint32_t key) { return neb_key_alg(e, key) == alg; }
+    bool mapped(const uint8_t* arena) { return neb_host_mapped(arena); }
 };
 
 }  // namespace

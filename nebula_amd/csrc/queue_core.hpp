@@ -13,6 +13,12 @@
 // A batch goes to the device when it reaches max_packets, when the next submission would not fit
 // its staging, when flush() asks, or max_delay_us after its first submission. `depth` staging
 // batches rotate: one filling, the others on the device or being copied out.
+//
+// Zero-copy submissions: when the caller's arena is pinned, mapped host memory (neb_host_alloc,
+// Dev::mapped), only its descriptors are staged. They point at the caller's arena itself — every
+// descriptor offset of a batch is relative to the batch's staging base, as a wrapping 64-bit
+// offset for a caller's arena — so the kernels read and write the caller's bytes in place, as the
+// zero-copy neb_*_batch_host does, and only the statuses are copied back.
 #pragma once
 
 #include <algorithm>
@@ -74,6 +80,7 @@ inline bool normalize(neb_queue_config& c) {
 //                                            order; batches may run concurrently on the device)
 //   int  wait(Token&)                        block until that batch is done and visible
 //   bool key_ok(key)                         the key is installed for the queue's algorithm
+//   bool mapped(arena)                       the kernels can address the arena in place
 // queue.cpp binds it to the engine (zero-copy kernels on pinned staging, HIP events); the
 // sanitizer tests (tests/sanitize/queue_test.cpp) to a CPU device running the oracle.
 template <class Dev>
@@ -90,7 +97,7 @@ struct Queue {
     std::condition_variable fcv;  // the flusher: a batch has work / was sealed / writers finished
     bool flush_req = false, quit = false;
     std::thread flusher, completer;
-    uint64_t n_batches = 0, n_packets = 0, n_subs = 0, n_bytes = 0;
+    uint64_t n_batches = 0, n_packets = 0, n_subs = 0, n_bytes = 0, n_zc = 0;
 
     // seal the filling batch and move `cur` to the next one (caller holds mu)
     void seal_current() {
@@ -167,13 +174,14 @@ struct Queue {
     // validated before anything is staged: a bad batch leaves the arena and statuses untouched
     for (uint32_t i = 0; i < n; i++)
         if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
+    const bool zc = q->dev.mapped(arena);  // stage descriptors only
     // the submission in pieces that each fit one batch
     uint32_t p0 = 0;
     while (p0 < n) {
         uint32_t cnt = 0;
         size_t bytes = 0;
         while (p0 + cnt < n && cnt < q->cfg.max_packets) {
-            const size_t sb = staged_bytes(desc[p0 + cnt], open);
+            const size_t sb = zc ? 0 : staged_bytes(desc[p0 + cnt], open);
             if (bytes + sb > q->cfg.arena_bytes) break;
             bytes += sb;
             cnt++;
@@ -217,6 +225,7 @@ struct Queue {
             c.readers++;
             q->n_subs++;
             q->n_bytes += bytes;
+            q->n_zc += zc;
             for (uint32_t i = 0; i < cnt; i++) {
                 const uint32_t k = desc[p0 + i].key_id;
                 if (c.key0 == NEB_KEYS_MIXED && c.one_key) c.key0 = k;
@@ -226,9 +235,19 @@ struct Queue {
         }
         // copy the packets into the staging (outside the lock: submitters copy in parallel)
         size_t off = off0;
+        const uint64_t rebase = (uint64_t)(uintptr_t)arena - (uint64_t)(uintptr_t)x->arena;  // wraps
         for (uint32_t i = 0; i < cnt; i++) {
             const neb_desc& d = desc[p0 + i];
             neb_desc s = d;
+            if (zc) {  // the caller's own bytes, in place
+                s.aad_off = d.aad_off + rebase;
+                s.src_off = d.src_off + rebase;
+                s.dst_off = d.dst_off + rebase;
+                s.flags = 0;
+                x->desc[pk0 + i] = s;
+                x->status[pk0 + i] = -1;
+                continue;
+            }
             const size_t src = (size_t)d.len + (open ? 16u : 0u), dst = (size_t)d.len + (open ? 0u : 16u);
             s.aad_off = off;
             if (d.aad_len) std::memcpy(x->arena + off, arena + d.aad_off, d.aad_len);
@@ -253,7 +272,9 @@ struct Queue {
             q->cv.wait(lk, [x] { return x->state == BState::kDone; });
         }
         const int rc = x->rc;
-        if (rc == NEB_OK) {
+        if (rc == NEB_OK && zc) {
+            for (uint32_t i = 0; i < cnt; i++) status[p0 + i] = x->status[pk0 + i];
+        } else if (rc == NEB_OK) {
             for (uint32_t i = 0; i < cnt; i++) {
                 const neb_desc& d = desc[p0 + i];
                 const neb_desc& s = x->desc[pk0 + i];
@@ -290,6 +311,10 @@ struct Queue {
         s[1] = n_packets;
         s[2] = n_subs;
         s[3] = n_bytes;
+    }
+    uint64_t zero_copy_submissions() {
+        std::lock_guard<std::mutex> g(mu);
+        return n_zc;
     }
     void start() {
         flusher = std::thread([this] { flush_loop(); });

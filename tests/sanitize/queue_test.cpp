@@ -12,6 +12,7 @@
 #include <deque>
 #include <memory>
 #include <random>
+#include <set>
 
 #include "../../nebula_amd/csrc/queue_core.hpp"
 
@@ -30,7 +31,18 @@ static int fails = 0;
 constexpr uint32_t kKeys = 8;
 static uint8_t g_keys[32 * kKeys];
 
-// A device that runs batches in launch order on one worker thread (as a stream would).
+// Arenas the CpuDev treats as mapped (the zero-copy submissions): registered by the test.
+static std::mutex g_mapped_mu;
+static std::set<const void*> g_mapped;
+static void set_mapped(const void* p, bool on) {
+    std::lock_guard<std::mutex> g(g_mapped_mu);
+    if (on) g_mapped.insert(p); else g_mapped.erase(p);
+}
+
+// A device that runs batches in launch order on one worker thread (as a stream would). Descriptor
+// offsets are relative to the batch's base as wrapping 64-bit offsets (a zero-copy submission's
+// point into its caller's arena): each packet is rebased to its lowest byte before the oracle runs
+// it, so no pointer arithmetic wraps here.
 struct CpuDev {
     struct Job {
         std::mutex mu;
@@ -78,7 +90,14 @@ struct CpuDev {
                     status[i] = NEB_STATUS_BAD_KEY;
                     continue;
                 }
-                ora_batch(a, o, g_keys, desc + i, 1, arena, status + i);
+                const uint64_t base = (uint64_t)(uintptr_t)arena;
+                const uint64_t aad = base + desc[i].aad_off, src = base + desc[i].src_off, dst = base + desc[i].dst_off;
+                const uint64_t lo = std::min(aad, std::min(src, dst));
+                neb_desc d = desc[i];
+                d.aad_off = aad - lo;
+                d.src_off = src - lo;
+                d.dst_off = dst - lo;
+                ora_batch(a, o, g_keys, &d, 1, reinterpret_cast<uint8_t*>((uintptr_t)lo), status + i);
             }
             std::lock_guard<std::mutex> g2(t->mu);
             t->done = true;
@@ -93,6 +112,10 @@ struct CpuDev {
         return NEB_OK;
     }
     bool key_ok(uint32_t key) { return key < kKeys; }
+    bool mapped(const uint8_t* arena) {
+        std::lock_guard<std::mutex> g(g_mapped_mu);
+        return g_mapped.count(arena) != 0;
+    }
 };
 
 using Q = neb_q::Queue<CpuDev>;
@@ -167,6 +190,8 @@ static void stress(int alg, uint32_t flush_pk, uint32_t max_packets, uint32_t de
             std::mt19937_64 rng(100 + t);
             for (int r = 0; r < rounds; r++) {
                 Flush f = make_flush(rng, flush_pk, ((uint64_t)t << 40) + (uint64_t)r * 1000);
+                const bool zc = (t + r) % 2 == 1;  // half the flushes submitted zero-copy
+                set_mapped(f.arena.data(), zc);
                 std::vector<uint8_t> ref = f.arena;
                 std::vector<int32_t> st(f.desc.size(), -1), rst(f.desc.size(), -1);
                 ora_batch(alg, 0, g_keys, f.desc.data(), f.desc.size(), ref.data(), rst.data());
@@ -177,6 +202,7 @@ static void stress(int alg, uint32_t flush_pk, uint32_t max_packets, uint32_t de
                 if (oq->submit(f.desc.data(), (uint32_t)f.desc.size(), f.arena.data(), f.arena.size(), st.data()) != NEB_OK ||
                     st != rst || f.arena != ref)
                     bad++;
+                set_mapped(f.arena.data(), false);
                 if (r % 5 == 4) sq->flush();
             }
         });
@@ -185,6 +211,7 @@ static void stress(int alg, uint32_t flush_pk, uint32_t max_packets, uint32_t de
     uint64_t s[4];
     sq->stats(s);
     CHECK(s[2] >= (uint64_t)threads * rounds);
+    CHECK(sq->zero_copy_submissions() > 0 && sq->zero_copy_submissions() < s[2]);
     free_queue(sq);
     free_queue(oq);
 }

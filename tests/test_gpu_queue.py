@@ -26,13 +26,17 @@ def _flushes(b, per):
     return out
 
 
-@pytest.mark.parametrize("alg,nkeys,threads,per", [
-    (L.ALG_AESGCM, 64, 16, 128),      # TX-sized flushes, many tunnels
-    (L.ALG_AESGCM, 1, 32, 64),        # RX-sized flushes, one tunnel: single-key batches
-    (L.ALG_CHACHAPOLY, 64, 8, 128),
+@pytest.mark.parametrize("alg,nkeys,threads,per,zc", [
+    (L.ALG_AESGCM, 64, 16, 128, False),      # TX-sized flushes, many tunnels
+    (L.ALG_AESGCM, 1, 32, 64, False),        # RX-sized flushes, one tunnel: single-key batches
+    (L.ALG_CHACHAPOLY, 64, 8, 128, False),
+    # every other flush's arena pinned and mapped (neb_host_alloc): submitted zero-copy, its
+    # descriptors pointing at the caller's bytes, in the same device batches as staged flushes
+    (L.ALG_AESGCM, 64, 16, 128, True),
+    (L.ALG_CHACHAPOLY, 64, 8, 64, True),
 ])
-def test_queue_many_threads_vs_oracle(engine, oracle_mod, alg, nkeys, threads, per):
-    from nebula_amd.batch import SubmitQueue, install_keys, slot_desc
+def test_queue_many_threads_vs_oracle(engine, oracle_mod, alg, nkeys, threads, per, zc):
+    from nebula_amd.batch import PinnedBuffer, SubmitQueue, install_keys, slot_desc
 
     b = W.make_batch(alg, 12000, nkeys, sizes=(90, 576, 1300), ratio=(7, 4, 1), seed=nkeys * 7 + per,
                      name="queue")
@@ -45,6 +49,14 @@ def test_queue_many_threads_vs_oracle(engine, oracle_mod, alg, nkeys, threads, p
     try:
         bd = W.Batch(alg, b.keys, b.remote_index, slot_desc(b, ciphers), b.arena, b.stride, "q")
         fl = _flushes(bd, per)
+        pinned = []
+        if zc:  # every other flush in pinned, mapped memory
+            for j in range(1, len(fl), 2):
+                f0, d, a, lo = fl[j]
+                pb = PinnedBuffer(a.nbytes)
+                pb.array[:] = a
+                pinned.append(pb)
+                fl[j] = (f0, d, pb.array, lo)
         results = {}
         errors = []
 
@@ -55,7 +67,7 @@ def test_queue_many_threads_vs_oracle(engine, oracle_mod, alg, nkeys, threads, p
                     st = seal_q.submit(d, a)
                     sealed = a.copy()
                     st2 = open_q.submit(d, a)
-                    results[j] = (st, sealed, st2, a)
+                    results[j] = (st, sealed, st2, a.copy())
             except Exception as ex:  # surfaced below
                 errors.append(ex)
 
@@ -78,9 +90,14 @@ def test_queue_many_threads_vs_oracle(engine, oracle_mod, alg, nkeys, threads, p
         assert s1["submissions"] == len(fl)
         # the point of the queue: far fewer device batches than flushes
         assert s1["batches"] < len(fl), s1
+        if zc:  # the pinned flushes staged nothing: only the others' bytes went through staging
+            assert 0 < s1["bytes"] < sum(a.nbytes for _, _, a, _ in fl)
     finally:
         seal_q.close()
         open_q.close()
+        if zc:
+            for pb in pinned:
+                pb.free()
         for c in ciphers:
             c.destroy()
 

@@ -16,4 +16,8 @@ for d in 50 200; do
   done
 done
 timeout -k 5 60 ./queue_bench queue 32 64 100 8192 1.5 >> $OUT/native.jsonl 2>> $OUT/native.err || exit $?
+# the same flushes from pinned, mapped arenas: submitted zero-copy
+for t in 8 16 32 64; do
+  timeout -k 5 60 ./queue_bench queuezc $t 128 50 8192 1.5 >> $OUT/native.jsonl 2>> $OUT/native.err || exit $?
+done
 cat $OUT/native.jsonl

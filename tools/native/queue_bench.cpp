@@ -4,7 +4,9 @@
 // opens it back through an open queue (listen.batch = 64, main.go:181), in a loop; or T threads
 // calling neb_encrypt_danger / neb_decrypt_danger packet by packet. Prints one JSON line per
 // configuration. Build: make -C tools/native; run on the GPU box.
-//   queue_bench queue <threads> <flush> <deadline_us> <max_packets> <seconds>
+//   queue_bench queue|queuezc <threads> <flush> <deadline_us> <max_packets> <seconds>
+//     [depth]  (queuezc: each thread's arena from neb_host_alloc, so its flushes are submitted
+//     zero-copy; depth: staging batches per queue, default 4)
 //   queue_bench percall <threads> <seconds>
 #include <algorithm>
 #include <atomic>
@@ -28,12 +30,14 @@ static double pct(std::vector<double>& v, double p) {
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
     const bool percall = !std::strcmp(argv[1], "percall");
+    const bool zc = !std::strcmp(argv[1], "queuezc");
     const int threads = argc > 2 ? std::atoi(argv[2]) : 8;
     const int flush = percall ? 1 : (argc > 3 ? std::atoi(argv[3]) : 128);
     const uint32_t deadline = percall ? 0 : (argc > 4 ? (uint32_t)std::atoi(argv[4]) : 100);
     const uint32_t maxpk = percall ? 0 : (argc > 5 ? (uint32_t)std::atoi(argv[5]) : 8192);
     const int si = percall ? 3 : 6;  // the seconds argument
     const double secs = argc > si ? std::atof(argv[si]) : 1.5;
+    const uint32_t depth = !percall && argc > 7 ? (uint32_t)std::atoi(argv[7]) : 4;
     const uint32_t kTunnels = 64, kLen = 1300, kSlot = 1344;
     neb_engine* e = nullptr;
     if (neb_engine_create(0, 4096, &e) != NEB_OK) {
@@ -48,7 +52,7 @@ int main(int argc, char** argv) {
     }
     neb_queue *sq = nullptr, *oq = nullptr;
     if (!percall) {
-        neb_queue_config c{maxpk, deadline, (uint64_t)maxpk * 1536, 4, 0};
+        neb_queue_config c{maxpk, deadline, (uint64_t)maxpk * 1536, depth, 0};
         if (neb_queue_create(e, NEB_ALG_AESGCM, 0, &c, &sq) != NEB_OK || neb_queue_create(e, NEB_ALG_AESGCM, 1, &c, &oq) != NEB_OK) {
             std::fprintf(stderr, "queue: %s\n", neb_last_error());
             return 1;
@@ -61,7 +65,27 @@ int main(int argc, char** argv) {
     std::vector<std::thread> th;
     for (int t = 0; t < threads; t++)
         th.emplace_back([&, t] {
-            std::vector<uint8_t> arena((size_t)flush * kSlot, (uint8_t)t);
+            std::vector<uint8_t> heap;
+            uint8_t* arena_p = nullptr;
+            const size_t arena_n = (size_t)flush * kSlot;
+            if (zc) {
+                void* p = nullptr;
+                if (neb_host_alloc(arena_n, &p) != NEB_OK) {
+                    errs++;
+                    return;
+                }
+                arena_p = static_cast<uint8_t*>(p);
+                std::memset(arena_p, t, arena_n);
+            } else {
+                heap.assign(arena_n, (uint8_t)t);
+                arena_p = heap.data();
+            }
+            struct View {
+                uint8_t* p;
+                size_t n;
+                uint8_t* data() { return p; }
+                size_t size() const { return n; }
+            } arena{arena_p, arena_n};
             std::vector<neb_desc> d(flush);
             std::vector<int32_t> st(flush);
             uint64_t ctr = (uint64_t)t << 40;
@@ -77,6 +101,7 @@ int main(int argc, char** argv) {
                     lat[t].clear();
                 }
                 const auto t0 = Clock::now();
+                auto t1q = t0;
                 if (percall) {
                     size_t rl = 0;
                     neb_cipher* c = keys[t % kTunnels];
@@ -91,6 +116,7 @@ int main(int argc, char** argv) {
                     int bad1 = 0;
                     for (int32_t s : st) bad1 += s != 0;
                     const auto t1 = Clock::now();
+                    t1q = t1;
                     if (counting) lat[t].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
                     const int rc2 = neb_queue_submit(oq, d.data(), flush, arena.data(), arena.size(), st.data());
                     int bad2 = 0, first = 0;
@@ -107,10 +133,16 @@ int main(int argc, char** argv) {
                 }
                 const auto t2 = Clock::now();
                 if (counting) {
-                    lat[t].push_back(std::chrono::duration<double, std::micro>(t2 - t0).count() / (percall ? 2 : 1));
+                    // per call: the two calls' mean (percall); the open submit's own time (queue; the
+                    // seal submit's was taken above)
+                    if (percall)
+                        lat[t].push_back(std::chrono::duration<double, std::micro>(t2 - t0).count() / 2);
+                    else
+                        lat[t].push_back(std::chrono::duration<double, std::micro>(t2 - t1q).count());
                     pkts += flush;
                 }
             }
+            if (zc) neb_host_free(arena_p);
         });
     std::this_thread::sleep_for(std::chrono::milliseconds(400));
     uint64_t s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
@@ -133,11 +165,11 @@ int main(int argc, char** argv) {
                     "\"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f, \"errors\": %d}\n",
                     threads, 2.0 * n / dt, gibs, p50, p99, errs.load());
     else
-        std::printf("{\"bench\": \"queue_native\", \"threads\": %d, \"flush_packets\": %d, \"deadline_us\": %u, "
-                    "\"max_packets\": %u, \"gibs\": %.3f, \"packets_per_s\": %.0f, \"submit_latency_us_p50\": %.1f, "
+        std::printf("{\"bench\": \"%s\", \"threads\": %d, \"flush_packets\": %d, \"deadline_us\": %u, "
+                    "\"max_packets\": %u, \"depth\": %u, \"gibs\": %.3f, \"packets_per_s\": %.0f, \"submit_latency_us_p50\": %.1f, "
                     "\"submit_latency_us_p99\": %.1f, \"seal_batches_per_s\": %.1f, \"mean_seal_batch_packets\": %.1f, "
                     "\"errors\": %d}\n",
-                    threads, flush, deadline, maxpk, gibs, n / dt, p50, p99, (s1[0] - s0[0]) / dt,
+                    zc ? "queue_native_zero_copy" : "queue_native", threads, flush, deadline, maxpk, depth, gibs, n / dt, p50, p99, (s1[0] - s0[0]) / dt,
                     (double)(s1[1] - s0[1]) / std::max<uint64_t>(1, s1[0] - s0[0]), errs.load());
     if (sq) neb_queue_destroy(sq);
     if (oq) neb_queue_destroy(oq);
