@@ -209,12 +209,6 @@ struct TLook4 {
 #ifndef NEB_PRIO
 #define NEB_PRIO 3
 #endif
-#ifndef NEB_RMAX_SHFL
-#define NEB_RMAX_SHFL 0
-#endif
-#ifndef NEB_CHUNK_OPAQUE_LANE
-#define NEB_CHUNK_OPAQUE_LANE 1
-#endif
 
 // AES-256 rounds FIRST..13 (full) and 14 (final) on the state s0..s3 (after round FIRST-1).
 template <int FIRST, class TL, class RK>
@@ -819,6 +813,7 @@ struct GhChunk4 {
 };
 // Tail chunks (1-8 packets at 8 or 16 lanes): Horner on the position tables of H^(2^lg), the tree
 // on M_1, M_2, M_4, M_8.
+
 struct GhChunkTree {
     const uint4* shoup;  // M_1, M_2, M_4, M_8
     const uint4* pos;    // position tables of H^(2^lg)
@@ -971,14 +966,9 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 io(b, G, ks);
             }
         };
-#if NEB_RMAX_SHFL
-        uint32_t Rmax = sh.R;
-        for (uint32_t s = LPP; s < 64u; s <<= 1) Rmax = max(Rmax, (uint32_t)__shfl_xor((int)Rmax, (int)s));
-        for (uint32_t r = 0; r < Rmax; r++) tround(r);
-#else
-        // rounds until no packet of the wave has one left (a ballot, no cross-lane reduction)
+        // rounds until no packet of the wave has one left (a ballot, no cross-lane reduction; a
+        // shuffle max of the round counts first was 4-7% slower in the chunk kernel)
         for (uint32_t r = 0; __any(r < sh.R); r++) tround(r);
-#endif
     };
     // counter caching needs every block counter of every packet in the wave below 2^8 / 2^16
     if (__all(sh.m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
@@ -1224,9 +1214,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         // are rebuilt per chunk from an opaque copy of the lane index: hoisted out of the chunk loop
         // they stay live across it and the compiler spills them (36-104 B of scratch per lane).
         uint32_t ln = lane;
-#if NEB_CHUNK_OPAQUE_LANE
         asm volatile("" : "+v"(ln));
-#endif
         const TLook T{lds.ttab, ttab_lane_base(ln)};
         const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
         const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
