@@ -237,9 +237,6 @@ struct ChachaArgs {
 // Payload and AAD blocks loaded one round ahead of their use (1) or in their round (0). Off: a
 // round ahead measured 2-3% slower on C4 (110.0 vs 107.1 µs per seal launch, rocprof A/B,
 // profiles/r2_s3/ab_chacha_prefetch): the kernel is bound by VALU issue, not by load latency.
-#ifndef NEB_CH_PREFETCH
-#define NEB_CH_PREFETCH 0
-#endif
 template <bool OPEN>
 __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs args) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -326,16 +323,11 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
             }
             return b;
         };
-        uint4 cur = NEB_CH_PREFETCH ? fetch(0u) : make_uint4(0, 0, 0, 0);
+        // (loading each round's block one round ahead measured 2-3% slower: DESIGN.md §3.3)
         for (uint32_t rho = 0; rho < rmax; rho++) {
             if (rho >= nrounds) continue;
-            const uint4 blk = NEB_CH_PREFETCH ? cur : fetch(rho);
-            if (NEB_CH_PREFETCH) cur = fetch(rho + 1u);
-#ifdef NEB_CH_ABLATE_CHACHA  // timing study only: wrong keystream
-            if (rho > kappa) ks = make_uint4(ks.x + rho, ks.y ^ rho, ks.z + j, ks.w ^ dn);
-#else
+            const uint4 blk = fetch(rho);
             if (rho > kappa) ks = chacha_quad(kConst[w], ka, kc, w == 0u ? 4u * (rho - kappa) + j : dn, w);
-#endif
             const int32_t i = (int32_t)(16u * rho + l) - (int32_t)phi;  // poly block index
             if (i < 0 || i >= (int32_t)n) continue;
             P5 mi;
@@ -352,11 +344,7 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
             } else {
                 mi = p5_from_words(d.aad_len, 0u, d.len, 0u, 1u);
             }
-#ifdef NEB_CH_ABLATE_POLY  // timing study only: wrong tag
-            A = p5_add(A, mi);
-#else
             A = p5_add(p5_mul(A, r16), mi);
-#endif
         }
         if (!run) {
             if (valid && l == 15u) args.status[p] = (int32_t)st;
