@@ -50,6 +50,9 @@ struct SchedSpace {
     uint32_t n_cap = 0;
     neb::SchedWs ws{};
     hipEvent_t done = nullptr;
+    // the stream `done` was last recorded on: a batch on that same stream is ordered after it
+    // already, and skips the cross-stream wait (a barrier packet that cost ≈ 5 µs between kernels)
+    hipStream_t last = nullptr;
     bool dirty = true;  // the bin counts need a clear (new buffer, or a batch that failed to launch)
     std::mutex mu;
 };
@@ -106,6 +109,7 @@ struct TxSpace {
     uint32_t n_cap = 0, tun_cap = 0, wire_cap = 0;
     neb::TxWs ws{};
     hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;  // the stream `done` was last recorded on (SchedSpace::last)
     uint8_t* d_io = nullptr;  // neb_tx_seal_batch_host staging
     size_t io_cap = 0;
     std::mutex mu;
@@ -550,12 +554,13 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
         hipError_t err = sched_reserve(e, sp, n, s);
-        if (err == hipSuccess) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
+        if (err == hipSuccess && sp.last != s) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                         sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count, s, hdr_from_dst);
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
+        if (err == hipSuccess) sp.last = s;
         if (err != hipSuccess) {
             // binning passes of this batch may already be queued on s: let them finish before the
             // next batch clears the counters (sched_reserve's dirty path waits on sp.done only)
@@ -951,7 +956,8 @@ void neb_rx_pipe_end(neb_engine* e) {
 static hipError_t tx_reserve(neb_engine* e, uint32_t n, uint32_t ntun, uint32_t max_wires) {
     TxSpace& tx = e->tx;
     if (!tx.done) {
-        hipError_t err = hipEventCreateWithFlags(&tx.done, hipEventDisableTiming);
+        // ordering only, as SchedSpace::done: no system-scope cache release at each record
+        hipError_t err = hipEventCreateWithFlags(&tx.done, hipEventDisableTiming | hipEventDisableSystemFence);
         if (err != hipSuccess) return err;
     }
     if (tx.mem && n <= tx.n_cap && ntun <= tx.tun_cap && max_wires <= tx.wire_cap) return hipSuccess;
@@ -980,7 +986,7 @@ static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, c
                   uint32_t max_wires, uint32_t* d_nwires, int32_t* d_pk_status, uint32_t key_hint, hipStream_t s) {
     TxSpace& tx = e->tx;
     HIP_TRY(tx_reserve(e, npk, ntun, max_wires));
-    HIP_TRY(hipStreamWaitEvent(s, tx.done, 0));
+    if (tx.last != s) HIP_TRY(hipStreamWaitEvent(s, tx.done, 0));
     HIP_TRY(neb_tx_plan(d_pk, npk, d_in, d_tun, ntun, e->d_keys, e->max_keys, alg, &tx.ws, out_cap, max_wires,
                         d_pk_status, d_nwires, s));
     // one tunnel key with AES-GCM: the seal sums the payload into the L4 checksums itself, so the
@@ -993,6 +999,7 @@ static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, c
                          cs ? 2 : (int)neb::kTxSealFromInput));
     HIP_TRY(neb_tx_finish(d_tun, npk, ntun, &tx.ws, s));
     HIP_TRY(hipEventRecord(tx.done, s));
+    tx.last = s;
     return NEB_OK;
 }
 
