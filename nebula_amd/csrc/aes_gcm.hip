@@ -913,18 +913,28 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         CtrConst cc{};
         if constexpr (CM == 2) cc = aes_ctr_prep8(c1, c2, T, rk);
         else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
-        // round r's payload XOR and GHASH fold, given G = A·H^LPP (the rounds before) and the keystream
-        auto io = [&](const LaneBlock& b, uint4 G, uint4 ks) {
-            // the common round: every active lane holds a full payload block with a 16-B aligned
-            // destination (the arena base counts too: a caller may pass an arena at any byte
-            // address); a source off 16-B alignment (a TX segment inside its TUN read) is read as
-            // two aligned blocks and shifted
+        // The common round: every active lane holds a full payload block with a 16-B aligned
+        // destination (the arena base counts too: a caller may pass an arena at any byte address);
+        // a source off 16-B alignment (a TX segment inside its TUN read) is read as two aligned
+        // blocks and shifted. Its block is loaded at the top of the round (fast_load), so the load's
+        // latency overlaps the round's GHASH and AES instead of following them: a wave's round is
+        // a chain of dependent LDS lookups, and the mixed-key kernel's last chunks run with few
+        // waves per CU to hide it (C3 +2.7%, C2 equal; tools/wave_trace.py).
+        auto fast_round = [&](const LaneBlock& b) {
             const uint32_t off = 16u * (b.k - 1u);
-            const bool full = b.is_ct && off + 16u <= d.len && off >= hdr &&
-                              ((d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u;
-            if (__all(full)) {
-                const uint8_t* sp = args.arena + d.src_off + off;
-                const uint4 in = __all(((uint32_t)(uintptr_t)sp & 3u) == 0u) ? load_u4_a4(sp) : load_shifted16(sp);
+            return __all(b.is_ct && off + 16u <= d.len && off >= hdr &&
+                         ((d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u);
+        };
+        auto fast_load = [&](const LaneBlock& b) {
+            const uint8_t* sp = args.arena + d.src_off + 16u * (b.k - 1u);
+            return __all(((uint32_t)(uintptr_t)sp & 3u) == 0u) ? load_u4_a4(sp) : load_shifted16(sp);
+        };
+        // round r's payload XOR and GHASH fold, given G = A·H^LPP (the rounds before), the keystream
+        // and (a common round) the block loaded at the round's top
+        auto io = [&](const LaneBlock& b, uint4 G, uint4 ks, bool fast, uint4 pre) {
+            const uint32_t off = 16u * (b.k - 1u);
+            if (fast) {
+                const uint4 in = pre;
                 if constexpr (CS) {
                     if (cs_on) cs_acc += le16_sum(in);
                 }
@@ -957,13 +967,16 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         auto tround = [&](uint32_t r) {
             if (r < sh.R) {
                 const LaneBlock b = lane_block(sh, r, l, lg);
+                const bool fast = fast_round(b);
+                uint4 pre = make_uint4(0, 0, 0, 0);
+                if (fast) pre = fast_load(b);
                 const uint4 G = horner(r);
                 __builtin_amdgcn_sched_barrier(0);
                 // a round with no ciphertext or length block in the wave needs no keystream: the
                 // AAD-only rounds of GMAC (relay verify, connection_state.go:121-148) skip the AES
                 uint4 ks = make_uint4(0, 0, 0, 0);
                 if (__any(b.is_ct || b.is_len)) ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
-                io(b, G, ks);
+                io(b, G, ks, fast, pre);
             }
         };
         // rounds until no packet of the wave has one left (a ballot, no cross-lane reduction; a
@@ -1119,6 +1132,23 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
 
 // ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------
 
+// Wave timeline of the chunk kernel, for tools/wave_trace.py only (a build with -DNEB_WAVE_TRACE=1;
+// the product build has none of it): per chunk {workgroup << 20 | wave << 16 | count << 8 | lg << 4
+// | full, chunk index, start, end} in s_memrealtime ticks (100 MHz), and per wave {…, ~0u, kernel
+// start, tables filled}.
+#ifdef NEB_WAVE_TRACE
+// fixed slots per wave (no shared counter: one atomic word serialised the waves and skewed the
+// timeline it was meant to record): slot 0 the wave's start, slot 1 + k its k-th chunk
+constexpr uint32_t kWaveTraceSlots = 64, kWaveTraceWaves = 8192, kWaveTraceCap = kWaveTraceSlots * kWaveTraceWaves;
+__device__ uint4 g_wtrace[kWaveTraceCap];
+__device__ __forceinline__ void wave_trace(uint32_t lane, uint32_t slot, uint32_t a, uint32_t b, uint64_t t0,
+                                           uint64_t t1) {
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (lane == 0u && w < kWaveTraceWaves && slot < kWaveTraceSlots)
+        g_wtrace[w * kWaveTraceSlots + slot] = make_uint4(a | 0x80000000u, b, (uint32_t)t0, (uint32_t)t1);
+}
+#endif
+
 // One kernel, two code paths, each specialised for its chunk shape (one path with a run-time lanes
 // per packet spilled 52-64 B per lane at 128 VGPRs, inside the chunk loop):
 //  front chunks (chunks[0, F)): groups of 16 packets at 4 lanes each, the layout of the single-key
@@ -1166,7 +1196,7 @@ struct ChunkArgs {
     const uint32_t* sorted;
     const uint4* chunks;
     uint32_t* counters;  // the scheduler's counters (sched.hpp kCnt*)
-    uint32_t max_chunks;
+    uint32_t max_chunks, max_short;
 };
 
 // Chunk order: the chunks of each kind come longest first (size class). Workgroup w owns chunks w,
@@ -1183,16 +1213,27 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
     const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
-    const uint32_t nback = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
-    // chunk index space: [0, nfront) the front chunks, then the tails (chunks[max - 1 - j])
+    const uint32_t nlong = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
+    const uint32_t nback = nlong + min(__builtin_amdgcn_readfirstlane(ca.counters[kCntShortChunks]), ca.max_short);
+    // chunk index space: [0, nfront) the front chunks, then the long tails (chunks[max - 1 - j]),
+    // then the short ones (chunks[max + j])
     const uint32_t c0 = 0u, nch = nfront + nback;
     if (c0 + blockIdx.x >= nch) return;  // owns no chunk (uniform over the workgroup)
+#ifdef NEB_WAVE_TRACE
+    const uint64_t tk0 = __builtin_amdgcn_s_memrealtime();
+#endif
     fill_ttab<256u * 32u, kChunkThreads>(lds.ttab, tid, ttab_entry);
     if (tid == 0) wg_cursor = kChunkWaves;
     __syncthreads();
+#ifdef NEB_WAVE_TRACE
+    uint32_t trace_k = 1;
+    wave_trace(lane, 0, blockIdx.x << 20 | wave << 16, ~0u, tk0, __builtin_amdgcn_s_memrealtime());
+#endif
     uint4* wtab = &lds.shoup[wave][0][0];
     uint4* wpos = &lds.pos[wave][0];
-    auto chunk_at = [&](uint32_t c) { return ca.chunks[c < nfront ? c : ca.max_chunks - 1u - (c - nfront)]; };
+    auto chunk_at = [&](uint32_t c) {
+        return ca.chunks[c < nfront ? c : c < nfront + nlong ? ca.max_chunks - 1u - (c - nfront) : ca.max_chunks + (c - nfront - nlong)];
+    };
     // Workgroup w owns chunks w, w + G, w + 2G, ... (front chunks first: the longest) and its waves
     // draw them from an LDS cursor, one chunk ahead. Drawing the last 10-50% from a global cursor
     // instead (dynamic balance across workgroups) made the C3 kernel 26-50% slower: the returning
@@ -1206,6 +1247,9 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     while (c < nch) {
         const uint4 ch = ch_next;
         const bool full = c < nfront;
+#ifdef NEB_WAVE_TRACE
+        const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
+#endif
         uint32_t cn = 0;
         if (lane == 0u) cn = chunk_of(atomicAdd(&wg_cursor, 1u));
         cn = __builtin_amdgcn_readfirstlane(cn);
@@ -1251,6 +1295,12 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef NEB_WAVE_TRACE
+        wave_trace(lane, trace_k++,
+                   blockIdx.x << 20 | wave << 16 | min((uint32_t)__builtin_amdgcn_readfirstlane(ch.y), 255u) << 8 |
+                       (full ? 2u : (uint32_t)__builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift)) << 4 | (full ? 1u : 0u),
+                   c, tc0, __builtin_amdgcn_s_memrealtime());
+#endif
         c = cn;
     }
 }
@@ -1544,13 +1594,27 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
 
 // Mixed keys: the batch has been regrouped into chunks by neb_sched_build.
 
+#ifdef NEB_WAVE_TRACE
+// tools/wave_trace.py: copy out (at most max entries) and reset the chunk kernel's wave timeline
+extern "C" NEB_API int neb_debug_wave_trace(void* out, uint32_t max) {
+    void* d = nullptr;
+    if (hipDeviceSynchronize() != hipSuccess || hipGetSymbolAddress(&d, HIP_SYMBOL(neb::g_wtrace)) != hipSuccess)
+        return -1;
+    const uint32_t n = std::min(neb::kWaveTraceCap, max);
+    if (hipMemcpy(out, d, (size_t)n * 16u, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(d, 0, (size_t)neb::kWaveTraceCap * 16u) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return -1;
+    return (int)n;
+}
+#endif
+
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
-                                            uint32_t* d_counters, uint32_t max_chunks, int cu_count,
-                                            hipStream_t s, int hdr_from_dst) {
+                                            uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
+                                            int cu_count, hipStream_t s, int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
-    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks};
+    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks, max_short};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
     // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.

@@ -29,8 +29,8 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
-                                            uint32_t* d_counters, uint32_t max_chunks, int cu_count,
-                                            hipStream_t s, int hdr_from_dst);
+                                            uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
+                                            int cu_count, hipStream_t s, int hdr_from_dst);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int hdr_from_dst);
 #ifndef NEB_TX_CSUM_SEAL
@@ -505,10 +505,10 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     }
     const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
     const uint32_t nb = neb::sched_nbins(e->max_keys);
-    const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys);
+    const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys), ms = neb::sched_max_short(cap, e->max_keys);
     const size_t b_counters = align_up((neb::kSchedCounters + 2u * (size_t)nb) * 4u, 256);
     const size_t b_base = align_up((size_t)nb * 4u, 256);
-    const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = (size_t)mc * 16u;
+    const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = ((size_t)mc + ms) * 16u;
     const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
@@ -532,6 +532,7 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     m += b_idx;
     sp.ws.chunks = (uint4*)m;
     sp.ws.max_chunks = mc;
+    sp.ws.max_short = ms;
     sp.bytes = bytes;
     sp.n_cap = cap;
     err = hipMemsetAsync(sp.ws.counters, 0, b_counters, s);  // once: the binning clears its counts as it uses them
@@ -558,7 +559,8 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess)
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count, s, hdr_from_dst);
+                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, e->cu_count, s,
+                                        hdr_from_dst);
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
         if (err == hipSuccess) sp.last = s;
         if (err != hipSuccess) {

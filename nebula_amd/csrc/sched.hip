@@ -22,7 +22,8 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
                                   uint32_t max_keys, uint32_t lpp, SchedWs ws) {
     // the cursors are cleared here (the previous batch's crypto kernel has finished with them);
     // the bin counts were cleared by the previous batch's pass 2 as it read them
-    if (blockIdx.x == 0 && threadIdx.x < kSchedCounters) ws.counters[threadIdx.x] = 0;
+    if (blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < kSchedCounters; i += blockDim.x) ws.counters[i] = 0;
     if (dn) n = min(n, *dn);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const neb_desc d = desc[i];
@@ -40,7 +41,7 @@ constexpr int kAllocThreads = 256;
 __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
     using Scan = hipcub::BlockScan<uint32_t, kAllocThreads>;
     __shared__ typename Scan::TempStorage tmp;
-    __shared__ uint32_t wg_base[3];
+    __shared__ uint32_t wg_base[4];
     const uint32_t nb = sched_nbins(max_keys);
     const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
     const uint32_t c = b < nb ? ws.hist[b] : 0u;
@@ -56,16 +57,21 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t fpk = nfull * kChunkPkts + (tail && lg == 2u ? tail : 0u);
     const uint32_t cpk = sched_groups(cls) * kChunkPkts;  // packets per front chunk
     const uint32_t nfront = (fpk + cpk - 1u) / cpk, nback = tail && lg != 2u ? 1u : 0u;
-    uint32_t off_p, off_f, off_b, tot_p, tot_f, tot_b;
+    const bool lng = sched_tail_long(cls, lg);
+    const uint32_t nlong = lng ? nback : 0u, nshort = lng ? 0u : nback;
+    uint32_t off_p, off_f, off_l, off_s, tot_p, tot_f, tot_l, tot_s;
     Scan(tmp).ExclusiveSum(c, off_p, tot_p);
     __syncthreads();
     Scan(tmp).ExclusiveSum(nfront, off_f, tot_f);
     __syncthreads();
-    Scan(tmp).ExclusiveSum(nback, off_b, tot_b);
+    Scan(tmp).ExclusiveSum(nlong, off_l, tot_l);
+    __syncthreads();
+    Scan(tmp).ExclusiveSum(nshort, off_s, tot_s);
     if (threadIdx.x == 0) {
         wg_base[0] = tot_p ? atomicAdd(&ws.counters[kCntPackets], tot_p) : 0u;
         wg_base[1] = tot_f ? atomicAdd(&ws.counters[kCntFrontChunks], tot_f) : 0u;
-        wg_base[2] = tot_b ? atomicAdd(&ws.counters[kCntBackChunks], tot_b) : 0u;
+        wg_base[2] = tot_l ? atomicAdd(&ws.counters[kCntBackChunks], tot_l) : 0u;
+        wg_base[3] = tot_s ? atomicAdd(&ws.counters[kCntShortChunks], tot_s) : 0u;
     }
     __syncthreads();
     if (c == 0u) return;
@@ -75,9 +81,14 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
         ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));
     if (nback) {
-        const uint32_t t = wg_base[2] + off_b;
-        if (t < ws.max_chunks)
-            ws.chunks[ws.max_chunks - 1u - t] = make_uint4(base + fpk, tail, key, cls | (lg << kChunkLgShift));
+        const uint4 ch = make_uint4(base + fpk, tail, key, cls | (lg << kChunkLgShift));
+        if (lng) {
+            const uint32_t t = wg_base[2] + off_l;
+            if (t < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - t] = ch;
+        } else {
+            const uint32_t t = wg_base[3] + off_s;
+            if (t < ws.max_short) ws.chunks[ws.max_chunks + t] = ch;
+        }
     }
 }
 

@@ -40,8 +40,8 @@ constexpr uint32_t kMaxChunkPkts = 8u * kChunkPkts;
 // counters[] slots
 constexpr uint32_t kCntPackets = 0;      // cursor into sorted[]
 constexpr uint32_t kCntFrontChunks = 1;  // chunks of groups at 4 lanes per packet, chunks[0, F)
-constexpr uint32_t kCntBackChunks = 2;   // tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
-constexpr uint32_t kCntWork = 3;         // the crypto kernel's chunk cursor (front chunks first)
+constexpr uint32_t kCntBackChunks = 2;   // long tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
+constexpr uint32_t kCntShortChunks = 3;  // short tails, chunks[max_chunks + j] (sched_tail_long)
 constexpr uint32_t kSchedCounters = 4;
 
 struct SchedWs {          // device workspace, sized for n packets and nbins bins
@@ -52,8 +52,9 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
     uint32_t* binof;      // [n] bin of each packet
     uint32_t* binpos;     // [n] rank of each packet within its bin (the histogram atomic's return)
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
-    uint4* chunks;        // [max_chunks] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
-    uint32_t max_chunks;
+    uint4* chunks;        // [max_chunks + max_short] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
+    uint32_t max_chunks;  // fronts from 0 up, long tails from max_chunks - 1 down
+    uint32_t max_short;   // short tails from max_chunks up
 };
 
 __host__ __device__ inline uint32_t sched_nbins(uint32_t max_keys) { return kSizeClasses * (max_keys + 1u); }
@@ -61,6 +62,16 @@ __host__ __device__ inline uint32_t sched_max_chunks(uint32_t n, uint32_t max_ke
     const uint32_t nb = sched_nbins(max_keys);
     return (n + kChunkPkts - 1u) / kChunkPkts + (n < nb ? n : nb);
 }
+// at most one tail per bin
+__host__ __device__ inline uint32_t sched_max_short(uint32_t n, uint32_t max_keys) {
+    const uint32_t nb = sched_nbins(max_keys);
+    return n < nb ? n : nb;
+}
+// The tails are handed out longest first (a workgroup's waves take them as their front chunks end,
+// and a long tail taken last runs on with few waves beside it): a tail at 2^lg lanes of size class
+// cls takes up to 2^(cls + 2 - lg) rounds; "long" (>= 16: 1300-B packets at 8 lanes, 11 rounds)
+// ahead of "short" (1300 B at 16 lanes: 6 rounds; everything shorter).
+__host__ __device__ inline bool sched_tail_long(uint32_t cls, uint32_t lg) { return cls >= lg + 2u; }
 
 }  // namespace neb
 
