@@ -811,11 +811,11 @@ struct GhChunk4 {
                           [&](uint4 a, uint32_t off) { return gf_mul_shoup(a, off, shoup); });
     }
 };
-// Tail chunks (1-8 packets at 8 or 16 lanes): Horner on the position tables of H^(2^lg), the tree
-// on M_1, M_2, M_4, M_8.
+// Tail chunks (1-8 packets at 8-64 lanes): Horner on the position tables of H^(2^lg), the tree on
+// M_1, M_2, M_4, ..., M_(2^(lg-1)).
 
 struct GhChunkTree {
-    const uint4* shoup;  // M_1, M_2, M_4, M_8
+    const uint4* shoup;  // M_1, M_2, M_4, ..., M_32
     const uint4* pos;    // position tables of H^(2^lg)
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
@@ -1159,8 +1159,9 @@ constexpr int kChunkWaves = 16;
 constexpr int kChunkWpe = 4;  // launch bound: waves per SIMD (at most 128 VGPRs)
 constexpr int kChunkThreads = kChunkWaves * kWave;
 
+constexpr uint32_t kChunkMaxLg = 6;  // tails run at up to 64 lanes per packet (sched_tail_lg)
 struct ChunkLds {
-    uint4 shoup[kChunkWaves][4][16];  // per wave: Shoup tables (1 KiB): M_1..M_4 (full), M_1, M_2, M_4, M_8 (tails)
+    uint4 shoup[kChunkWaves][kChunkMaxLg][16];  // per wave: Shoup tables (1.5 KiB): M_1..M_4 (full), M_(2^i), i < lg (tails)
     uint4 pos[kChunkWaves][8 * 16];   // per wave: position tables of H^(2^lg) (2 KiB)
     uint2 ttab[256 * 32];             // 64 KiB T-table pairs, 32 copies
 };
@@ -1168,17 +1169,22 @@ struct ChunkLds {
 // Stage a chunk key's GHASH tables in the wave's LDS slice, computed from the record's raw powers
 // H^1..H^16 (16 B each) rather than copied from its precomputed tables: 128 B of key material per
 // chunk instead of 3 KiB, which for IMIX-sized chunks was a third of the kernel's memory traffic.
-//   shoup[t][v] = v·H^(e_t), t < 4: e = 1, 2, 3, 4 (FULL) or 1, 2, 4, 8 (tails)
+//   shoup[t][v] = v·H^(e_t): t < 4, e = 1, 2, 3, 4 (FULL); t < lg, e = 2^t (tails)
 //   pos[r][v]   = v·x^(4r)·P, r < 8, P = H^(2^lg): XOR of the basis P·x^(4r+j) over the set bits
 //                 of v (bit 3 ↔ j = 0), the basis P·x^i (i < 32) one per lane and shuffled
+// H^32 and H^64 (tails at 32 and 64 lanes) are entry 8 (= 1·P) of their Shoup tables in the record.
+__device__ __forceinline__ uint32_t rec_hpow2(uint32_t j) {  // raw H^(2^j), j <= 6
+    return j <= 4u ? kRecHPow + 4u * ((1u << j) - 1u) : rec_shoup_pow2(j) + 4u * 8u;
+}
 template <bool FULL>
 __device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t lane, uint32_t lg, uint4* wtab,
                                                    uint4* wpos) {
     const uint32_t t = lane >> 4, v = lane & 15u;
-    const uint32_t e = FULL ? t + 1u : 1u << t;
-    const uint4 he = ld_rec4(rec, kRecHPow + 4u * (e - 1u));
-    const uint4 P = ld_rec4(rec, kRecHPow + 4u * ((1u << lg) - 1u));
+    const uint4 he = ld_rec4(rec, FULL ? kRecHPow + 4u * t : rec_hpow2(t));
+    const uint4 P = ld_rec4(rec, FULL ? kRecHPow + 4u * 3u : rec_hpow2(lg));
     wtab[lane] = gf_tab_entry(he, v);
+    if (!FULL && lg > 4u && lane < 16u * (lg - 4u))  // M_16, M_32
+        wtab[64u + lane] = gf_tab_entry(ld_rec4(rec, rec_hpow2(4u + t)), v);
     const uint4 B = gf_mul_xpow32(P, lane & 31u);
     uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -1281,7 +1287,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                 gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
             }
         } else {
-            const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
+            const uint32_t lg = min((uint32_t)__builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift), kChunkMaxLg);  // 3-6
             stage_chunk_tables<false>(rec, ln, lg, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
