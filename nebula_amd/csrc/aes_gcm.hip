@@ -811,11 +811,11 @@ struct GhChunk4 {
                           [&](uint4 a, uint32_t off) { return gf_mul_shoup(a, off, shoup); });
     }
 };
-// Tail chunks (1-8 packets at 8-64 lanes): Horner on the position tables of H^(2^lg), the tree on
-// M_1, M_2, M_4, ..., M_(2^(lg-1)).
+// Tail chunks (1-8 packets at 8 or 16 lanes): Horner on the position tables of H^(2^lg), the tree
+// on M_1, M_2, M_4, M_8.
 
 struct GhChunkTree {
-    const uint4* shoup;  // M_1, M_2, M_4, ..., M_32
+    const uint4* shoup;  // M_1, M_2, M_4, M_8
     const uint4* pos;    // position tables of H^(2^lg)
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
@@ -1006,6 +1006,23 @@ __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rk
     for (int i = 0; i < 60; i++) rks[i] = __builtin_amdgcn_readfirstlane(rec[kRecRoundKeys + i]);
 }
 
+// Wave timeline of the single-key and chunk kernels, for tools/wave_trace.py only (a build with -DNEB_WAVE_TRACE=1;
+// the product build has none of it): per chunk {workgroup << 20 | wave << 16 | count << 8 | lg << 4
+// | full, chunk index, start, end} in s_memrealtime ticks (100 MHz), and per wave {…, ~0u, kernel
+// start, tables filled}.
+#ifdef NEB_WAVE_TRACE
+// fixed slots per wave (no shared counter: one atomic word serialised the waves and skewed the
+// timeline it was meant to record): slot 0 the wave's start, slot 1 + k its k-th chunk
+constexpr uint32_t kWaveTraceSlots = 64, kWaveTraceWaves = 8192, kWaveTraceCap = kWaveTraceSlots * kWaveTraceWaves;
+__device__ uint4 g_wtrace[kWaveTraceCap];
+__device__ __forceinline__ void wave_trace(uint32_t lane, uint32_t slot, uint32_t a, uint32_t b, uint64_t t0,
+                                           uint64_t t1) {
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (lane == 0u && w < kWaveTraceWaves && slot < kWaveTraceSlots)
+        g_wtrace[w * kWaveTraceSlots + slot] = make_uint4(a | 0x80000000u, b, (uint32_t)t0, (uint32_t)t1);
+}
+#endif
+
 // ---- one tunnel key for the whole batch -------------------------------------------------------
 
 // Four-table AES (TLook4, 128 KiB) + the GHASH tables: one 1024-lane workgroup per CU, 4 waves per
@@ -1032,6 +1049,9 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
     const uint32_t* srec = args.keys + (size_t)args.key_hint * kKeyRecDwords;
+#ifdef NEB_WAVE_TRACE
+    const uint64_t tk0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // the record's GHASH tables: loaded before the T-table fill and stored after it, so their
     // latency overlaps the fill's instead of following it
     static_assert(kSingleThreads >= 512, "one full-table entry per thread");
@@ -1044,6 +1064,7 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
     if (tid < 512u) lds.full[tid] = r_full;
     if (tid < 128u) lds.pos1[tid] = r_h;
     if (tid < 256u) lds.pos23[tid >> 7][tid & 127u] = r_p;
+
     const uint4* cs_pow = nullptr;
     if constexpr (CS) {
         if (tid < 160u) lds.pow2[tid] = ld_rec4(srec, rec_shoup_pow2(tid >> 4) + 4u * (tid & 15u));
@@ -1070,9 +1091,20 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
     // groups go to workgroups first (group g: workgroup g mod G, wave g / G), so a batch of fewer
     // groups than waves spreads over as many CUs as it can instead of filling a few (a 2048-packet
     // batch on 8 CUs ran as long as a whole 64 Ki pass)
+#ifdef NEB_WAVE_TRACE
+    uint32_t trace_k = 1;
+    wave_trace(lane, 0, blockIdx.x << 20 | wave << 16, ~0u, tk0, __builtin_amdgcn_s_memrealtime());
+#endif
     for (uint32_t grp = blockIdx.x + wave * gridDim.x; grp < main_groups; grp += slots) {
+#ifdef NEB_WAVE_TRACE
+        const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const uint32_t p = grp * kPpw + lane / kLpp;
         gcm_packet_group<OPEN, CS>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, cs_pow);
+#ifdef NEB_WAVE_TRACE
+        wave_trace(lane, trace_k++, blockIdx.x << 20 | wave << 16 | 16u << 8 | 2u << 4 | 1u, grp, tc0,
+                   __builtin_amdgcn_s_memrealtime());
+#endif
     }
 }
 
@@ -1132,22 +1164,6 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
 
 // ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------
 
-// Wave timeline of the chunk kernel, for tools/wave_trace.py only (a build with -DNEB_WAVE_TRACE=1;
-// the product build has none of it): per chunk {workgroup << 20 | wave << 16 | count << 8 | lg << 4
-// | full, chunk index, start, end} in s_memrealtime ticks (100 MHz), and per wave {…, ~0u, kernel
-// start, tables filled}.
-#ifdef NEB_WAVE_TRACE
-// fixed slots per wave (no shared counter: one atomic word serialised the waves and skewed the
-// timeline it was meant to record): slot 0 the wave's start, slot 1 + k its k-th chunk
-constexpr uint32_t kWaveTraceSlots = 64, kWaveTraceWaves = 8192, kWaveTraceCap = kWaveTraceSlots * kWaveTraceWaves;
-__device__ uint4 g_wtrace[kWaveTraceCap];
-__device__ __forceinline__ void wave_trace(uint32_t lane, uint32_t slot, uint32_t a, uint32_t b, uint64_t t0,
-                                           uint64_t t1) {
-    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (lane == 0u && w < kWaveTraceWaves && slot < kWaveTraceSlots)
-        g_wtrace[w * kWaveTraceSlots + slot] = make_uint4(a | 0x80000000u, b, (uint32_t)t0, (uint32_t)t1);
-}
-#endif
 
 // One kernel, two code paths, each specialised for its chunk shape (one path with a run-time lanes
 // per packet spilled 52-64 B per lane at 128 VGPRs, inside the chunk loop):
@@ -1159,9 +1175,8 @@ constexpr int kChunkWaves = 16;
 constexpr int kChunkWpe = 4;  // launch bound: waves per SIMD (at most 128 VGPRs)
 constexpr int kChunkThreads = kChunkWaves * kWave;
 
-constexpr uint32_t kChunkMaxLg = 6;  // tails run at up to 64 lanes per packet (sched_tail_lg)
 struct ChunkLds {
-    uint4 shoup[kChunkWaves][kChunkMaxLg][16];  // per wave: Shoup tables (1.5 KiB): M_1..M_4 (full), M_(2^i), i < lg (tails)
+    uint4 shoup[kChunkWaves][4][16];  // per wave: Shoup tables (1 KiB): M_1..M_4 (full), M_1, M_2, M_4, M_8 (tails)
     uint4 pos[kChunkWaves][8 * 16];   // per wave: position tables of H^(2^lg) (2 KiB)
     uint2 ttab[256 * 32];             // 64 KiB T-table pairs, 32 copies
 };
@@ -1169,22 +1184,17 @@ struct ChunkLds {
 // Stage a chunk key's GHASH tables in the wave's LDS slice, computed from the record's raw powers
 // H^1..H^16 (16 B each) rather than copied from its precomputed tables: 128 B of key material per
 // chunk instead of 3 KiB, which for IMIX-sized chunks was a third of the kernel's memory traffic.
-//   shoup[t][v] = v·H^(e_t): t < 4, e = 1, 2, 3, 4 (FULL); t < lg, e = 2^t (tails)
+//   shoup[t][v] = v·H^(e_t), t < 4: e = 1, 2, 3, 4 (FULL) or 1, 2, 4, 8 (tails)
 //   pos[r][v]   = v·x^(4r)·P, r < 8, P = H^(2^lg): XOR of the basis P·x^(4r+j) over the set bits
 //                 of v (bit 3 ↔ j = 0), the basis P·x^i (i < 32) one per lane and shuffled
-// H^32 and H^64 (tails at 32 and 64 lanes) are entry 8 (= 1·P) of their Shoup tables in the record.
-__device__ __forceinline__ uint32_t rec_hpow2(uint32_t j) {  // raw H^(2^j), j <= 6
-    return j <= 4u ? kRecHPow + 4u * ((1u << j) - 1u) : rec_shoup_pow2(j) + 4u * 8u;
-}
 template <bool FULL>
 __device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t lane, uint32_t lg, uint4* wtab,
                                                    uint4* wpos) {
     const uint32_t t = lane >> 4, v = lane & 15u;
-    const uint4 he = ld_rec4(rec, FULL ? kRecHPow + 4u * t : rec_hpow2(t));
-    const uint4 P = ld_rec4(rec, FULL ? kRecHPow + 4u * 3u : rec_hpow2(lg));
+    const uint32_t e = FULL ? t + 1u : 1u << t;
+    const uint4 he = ld_rec4(rec, kRecHPow + 4u * (e - 1u));
+    const uint4 P = ld_rec4(rec, kRecHPow + 4u * ((1u << lg) - 1u));
     wtab[lane] = gf_tab_entry(he, v);
-    if (!FULL && lg > 4u && lane < 16u * (lg - 4u))  // M_16, M_32
-        wtab[64u + lane] = gf_tab_entry(ld_rec4(rec, rec_hpow2(4u + t)), v);
     const uint4 B = gf_mul_xpow32(P, lane & 31u);
     uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -1287,7 +1297,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                 gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
             }
         } else {
-            const uint32_t lg = min((uint32_t)__builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift), kChunkMaxLg);  // 3-6
+            const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
             stage_chunk_tables<false>(rec, ln, lg, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();

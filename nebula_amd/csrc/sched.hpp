@@ -28,17 +28,9 @@ constexpr uint32_t kSizeClasses = 8;  // round-count classes at 4 lanes per pack
 // of the key's tables and round keys, so short packets (IMIX 90 B: 2 rounds per group) do not pay
 // the staging per 16 packets. Tails at 8 or 16 lanes are "back" chunks of their own.
 constexpr uint32_t kChunkLgShift = 8;  // chunk.w = size class | lg << kChunkLgShift
-#ifndef NEB_WIDE_TAILS
-#define NEB_WIDE_TAILS 0
-#endif
 __host__ __device__ inline uint32_t sched_tail_lg(uint32_t count, uint32_t cls) {
-#if NEB_WIDE_TAILS
-    const uint32_t fit = count <= 1u ? 6u : count <= 2u ? 5u : count <= 4u ? 4u : (count <= 8u ? 3u : 2u);
-    const uint32_t size = cls + 2u;
-#else
     const uint32_t fit = count <= 4u ? 4u : (count <= 8u ? 3u : 2u);
     const uint32_t size = cls == 0u ? 2u : (cls == 1u ? 3u : 4u);
-#endif
     return fit < size ? fit : size;
 }
 // groups of 16 packets per front chunk: about 8 rounds of work per chunk for the short classes

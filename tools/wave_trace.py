@@ -1,4 +1,4 @@
-"""Wave timeline of the mixed-key chunk kernel (gcm_chunk_kernel) on one batch.
+"""Wave timeline of the AES-GCM kernels (gcm_chunk_kernel; gcm_single_kernel for --config 1) on one batch.
 
 Needs the trace build (tools/build_variant.sh wtrace -DNEB_WAVE_TRACE=1) selected with
 NEB_LIB_PATH=build_abl/wtrace/libnebula_aead.so. Seals (and opens) a BASELINE config once after a
@@ -118,7 +118,9 @@ def main():
     lib = L.lib()
     lib.neb_debug_wave_trace.restype = ctypes.c_int
     lib.neb_debug_wave_trace.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-    b = W.make_batch(L.ALG_AESGCM, 65536, 4096, name="C3") if args.config == 2 else W.config(4)
+    b = {1: lambda: W.make_batch(L.ALG_AESGCM, 65536, 1, name="C2"),
+         2: lambda: W.make_batch(L.ALG_AESGCM, 65536, 4096, name="C3"),
+         4: lambda: W.config(4)}[args.config]()
     eng = Engine(0, max_keys=max(4096, b.nkeys))
     ciphers = install_keys(eng, b)
     db = DeviceBatch(eng, b, ciphers)
