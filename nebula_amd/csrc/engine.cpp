@@ -499,15 +499,15 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     if (n <= sp.n_cap && sp.mem) {  // the bins are cleared as they are consumed, except after a failure
         hipError_t err = hipEventSynchronize(sp.done);
         if (err == hipSuccess)
-            err = hipMemsetAsync(sp.ws.counters, 0, (neb::kSchedCounters + 2u * neb::sched_nbins(e->max_keys)) * 4u, s);
+            err = hipMemsetAsync(sp.ws.counters, 0, (neb::kSchedCounters + (size_t)neb::kSubBins * neb::sched_nbins(e->max_keys)) * 4u, s);
         if (err == hipSuccess) sp.dirty = false;
         return err;
     }
     const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
     const uint32_t nb = neb::sched_nbins(e->max_keys);
     const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys), ms = neb::sched_max_short(cap, e->max_keys);
-    const size_t b_counters = align_up((neb::kSchedCounters + 2u * (size_t)nb) * 4u, 256);
-    const size_t b_base = align_up((size_t)nb * 4u, 256);
+    const size_t b_counters = align_up((neb::kSchedCounters + (size_t)neb::kSubBins * nb) * 4u, 256);
+    const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = ((size_t)mc + ms) * 16u;
     const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
@@ -520,7 +520,6 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     uint8_t* m = sp.mem;
     sp.ws.counters = (uint32_t*)m;
     sp.ws.hist = sp.ws.counters + neb::kSchedCounters;
-    sp.ws.fill = sp.ws.hist + nb;
     m += b_counters;
     sp.ws.base = (uint32_t*)m;
     m += b_base;

@@ -28,7 +28,7 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const neb_desc d = desc[i];
         const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
-        const uint32_t b = size_class(d, lpp) * (max_keys + 1u) + key;
+        const uint32_t b = (size_class(d, lpp) * (max_keys + 1u) + key) * kSubBins + (blockIdx.x & (kSubBins - 1u));
         ws.binof[i] = b;
         ws.binpos[i] = atomicAdd(&ws.hist[b], 1u);
     }
@@ -44,8 +44,15 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     __shared__ uint32_t wg_base[4];
     const uint32_t nb = sched_nbins(max_keys);
     const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
-    const uint32_t c = b < nb ? ws.hist[b] : 0u;
-    if (c) ws.hist[b] = 0;  // clear for the next batch
+    uint32_t sc[kSubBins], c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kSubBins; j++) {
+        sc[j] = b < nb ? ws.hist[b * kSubBins + j] : 0u;
+        c += sc[j];
+    }
+    if (c)  // clear for the next batch
+#pragma unroll
+        for (uint32_t j = 0; j < kSubBins; j++) ws.hist[b * kSubBins + j] = 0u;
     const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
     const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
     const uint32_t lg = tail ? sched_tail_lg(tail, cls) : 2u;
@@ -76,7 +83,12 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     __syncthreads();
     if (c == 0u) return;
     const uint32_t base = wg_base[0] + off_p;
-    ws.base[b] = base;
+    uint32_t sb = base;
+#pragma unroll
+    for (uint32_t j = 0; j < kSubBins; j++) {
+        ws.base[b * kSubBins + j] = sb;
+        sb += sc[j];
+    }
     const uint32_t cf = wg_base[1] + off_f;
     for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
         ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));

@@ -44,12 +44,21 @@ constexpr uint32_t kCntBackChunks = 2;   // long tails at 8 or 16 lanes per pack
 constexpr uint32_t kCntShortChunks = 3;  // short tails, chunks[max_chunks + j] (sched_tail_long)
 constexpr uint32_t kSchedCounters = 4;
 
+// Each bin counts its packets in kSubBins sub-bins (sub-bin = the counting workgroup's index mod
+// kSubBins), so the returning atomics of one bin's packets spread over kSubBins words: a 4096-key
+// IMIX batch of 1 Mi packets put ≈ 85 adds on each word, and the memory-side atomics on one address
+// run one after another (pass 1 took 56 µs).
+#ifndef NEB_SUB_BINS
+#define NEB_SUB_BINS 8
+#endif
+constexpr uint32_t kSubBins = NEB_SUB_BINS;
+static_assert(kSubBins == 1 || kSubBins == 2 || kSubBins == 4 || kSubBins == 8, "sub-bins: a power of two <= 8");
+
 struct SchedWs {          // device workspace, sized for n packets and nbins bins
-    uint32_t* counters;   // [kSchedCounters] counters, then hist[nbins], fill[nbins]
-    uint32_t* hist;
-    uint32_t* fill;
-    uint32_t* base;       // [nbins] output offset of each non-empty bin
-    uint32_t* binof;      // [n] bin of each packet
+    uint32_t* counters;   // [kSchedCounters] counters, then hist[nbins * kSubBins]
+    uint32_t* hist;       // [bin * kSubBins + sub] packets counted
+    uint32_t* base;       // [bin * kSubBins + sub] output offset of each non-empty sub-bin
+    uint32_t* binof;      // [n] sub-bin (bin * kSubBins + sub) of each packet
     uint32_t* binpos;     // [n] rank of each packet within its bin (the histogram atomic's return)
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
     uint4* chunks;        // [max_chunks + max_short] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
