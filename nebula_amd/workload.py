@@ -70,22 +70,30 @@ class Batch:
         return int((2 * self.desc["len"].astype(np.int64) + 2 * 16).sum())
 
 
+def key_ids(npkt: int, nkeys: int, seed: int = SEED) -> np.ndarray:
+    """Each packet's tunnel key: uniform over nkeys (a Poisson(npkt / nkeys) count per key)."""
+    if nkeys == 1:
+        return np.zeros(npkt, np.uint32)
+    return (splitmix64(seed ^ 0x4B494453, npkt) % np.uint64(nkeys)).astype(np.uint32)
+
+
+def payload_lens(npkt: int, sizes=(1300,), ratio=(1,), seed: int = SEED) -> np.ndarray:
+    """Payload sizes: one size, or a mix in the given ratio (IMIX 90/576/1300 at 7:4:1), shuffled."""
+    if len(sizes) == 1:
+        return np.full(npkt, sizes[0], np.uint32)
+    pool = np.repeat(np.asarray(sizes, np.uint32), ratio)
+    reps = -(-npkt // len(pool))
+    lens = np.tile(pool, reps)[:npkt]
+    order = np.argsort(splitmix64(seed ^ 0x494D4958, npkt), kind="stable")
+    return lens[order]
+
+
 def make_batch(alg: int, npkt: int, nkeys: int, sizes=(1300,), ratio=(1,), seed: int = SEED,
                name: str = "") -> Batch:
     keys = random_bytes(seed ^ 0x4B455953, 32 * nkeys)                      # "KEYS"
     remote_index = (splitmix64(seed ^ 0x52494458, nkeys) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-    if nkeys == 1:
-        kid = np.zeros(npkt, np.uint32)
-    else:
-        kid = (splitmix64(seed ^ 0x4B494453, npkt) % np.uint64(nkeys)).astype(np.uint32)
-    if len(sizes) == 1:
-        lens = np.full(npkt, sizes[0], np.uint32)
-    else:
-        pool = np.repeat(np.asarray(sizes, np.uint32), ratio)
-        reps = -(-npkt // len(pool))
-        lens = np.tile(pool, reps)[:npkt]
-        order = np.argsort(splitmix64(seed ^ 0x494D4958, npkt), kind="stable")
-        lens = lens[order]
+    kid = key_ids(npkt, nkeys, seed)
+    lens = payload_lens(npkt, sizes, ratio, seed)
     # per-key counters in emission order
     order = np.argsort(kid, kind="stable")
     sk = kid[order]
