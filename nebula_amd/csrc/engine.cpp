@@ -445,14 +445,20 @@ NEB_API int neb_cipher_destroy(neb_cipher* c) {
     const uint32_t slot = c->key_id;
     hipSetDevice(e->device);
     // Asynchronous batches the engine enqueued that may read this record: the last single-key
-    // batch with this key on each stream, and the last mixed-key batch on each stream (note_use).
-    // Only those are waited for — not the device, so another tunnel's batches in flight elsewhere
-    // do not stall a teardown or rekey. The caller stops enqueuing with a key before destroying it.
+    // batch with this key on each stream, the last mixed-key batch on each stream (note_use), and
+    // the mixed-key AES-GCM batches of the engine's scheduler workspace (its `done` event: the last
+    // user's, and each user waited for the one before). Only those are waited for — not the
+    // device, so another tunnel's batches in flight elsewhere do not stall a teardown or rekey.
+    // The caller stops enqueuing with a key before destroying it.
     std::vector<hipEvent_t> wait;
     {
         std::lock_guard<std::mutex> g(e->use_mu);
         for (KeyUse& u : e->key_use[slot]) wait.push_back(u.ev);
         for (KeyUse& u : e->mixed_use) wait.push_back(u.ev);
+    }
+    {
+        std::lock_guard<std::mutex> g(e->sched.mu);
+        if (e->sched.done) wait.push_back(e->sched.done);
     }
     for (hipEvent_t ev : wait) (void)hipEventSynchronize(ev);
     int rc = NEB_OK;
@@ -673,7 +679,11 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
         set_error("batch launch", err);
         return NEB_ERR_HIP;
     }
-    note_use(e, key_hint, s);
+    // A mixed-key AES-GCM batch ran through the engine's scheduler workspace, whose `done` event
+    // is recorded after it and orders every later user of the workspace after it:
+    // neb_cipher_destroy waits on that event, so the batch needs no marker of its own (each marker
+    // between two batches cost ≈ 5 µs, C3 +3.5-5%, profiles/r3_ab/use_events.log).
+    if (!(alg == NEB_ALG_AESGCM && key_hint == NEB_KEYS_MIXED)) note_use(e, key_hint, s);
     return NEB_OK;
 }
 
