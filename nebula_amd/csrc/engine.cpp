@@ -25,7 +25,7 @@ extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, h
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                           int hdr_from_dst);
+                                           int hdr_from_dst, hipEvent_t stop);
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
@@ -261,6 +261,19 @@ static void note_use(neb_engine* e, uint32_t key_hint, hipStream_t s) {
     if (hipEventCreateWithFlags(&u.ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return;
     (void)hipEventRecord(u.ev, s);
     v.push_back(u);
+}
+
+// The key-use event of (key_hint, s), created on first use, for a batch to bind to its last
+// kernel (neb_gcm_batch_single's `stop`) instead of note_use's marker after it.
+static hipEvent_t use_event(neb_engine* e, uint32_t key_hint, hipStream_t s) {
+    std::lock_guard<std::mutex> g(e->use_mu);
+    std::vector<KeyUse>& v = key_hint == NEB_KEYS_MIXED ? e->mixed_use : e->key_use[key_hint];
+    for (KeyUse& u : v)
+        if (u.s == s) return u.ev;
+    KeyUse u{s, nullptr};
+    if (hipEventCreateWithFlags(&u.ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return nullptr;
+    v.push_back(u);
+    return u.ev;
 }
 
 extern "C" {
@@ -551,11 +564,11 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
 // descriptors (tx.hip) read their first `flags` plaintext bytes from the destination.
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr,
-                               SchedSpace* sched = nullptr, int hdr_from_dst = 0) {
+                               SchedSpace* sched = nullptr, int hdr_from_dst = 0, hipEvent_t stop = nullptr) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
             return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
-                                        e->cu_count, s, hdr_from_dst);
+                                        e->cu_count, s, hdr_from_dst, stop);
         // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
@@ -674,11 +687,15 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
     if (!d_desc || !d_arena || !d_status) return NEB_ERR_INVALID;
     hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream, as for any HIP launch
-    hipError_t err = launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s);
+    // a single-key AES-GCM batch binds its key-use event to its last kernel (no marker after it)
+    const bool bound = alg == NEB_ALG_AESGCM && key_hint != NEB_KEYS_MIXED;
+    hipEvent_t stop = bound ? use_event(e, key_hint, s) : nullptr;
+    hipError_t err = launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s, nullptr, nullptr, 0, stop);
     if (err != hipSuccess) {
         set_error("batch launch", err);
         return NEB_ERR_HIP;
     }
+    if (bound && stop) return NEB_OK;
     // A mixed-key AES-GCM batch ran through the engine's scheduler workspace, whose `done` event
     // is recorded after it and orders every later user of the workspace after it:
     // neb_cipher_destroy waits on that event, so the batch needs no marker of its own (each marker

@@ -509,15 +509,17 @@ def test_host_rejects_invalid_descriptor_untouched(engine, mode, case, monkeypat
             c.destroy()
 
 
-def test_cipher_destroy_waits_for_queued_batches(engine, oracle_mod):
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_cipher_destroy_waits_for_queued_batches(engine, oracle_mod, cfg):
     """neb_cipher_destroy right after an asynchronous seal was enqueued behind other work on the
     caller's stream: the batch still runs with the installed key (destroy waits for it), so the
-    output equals the oracle; the slot is free afterwards."""
+    output equals the oracle; the slot is free afterwards. Single key (its key-use event bound to
+    the batch's last kernel) and mixed keys (the scheduler workspace's event)."""
     import torch
 
     from nebula_amd.batch import DeviceBatch, install_keys
 
-    b = W.config(2, 1 / 16)
+    b = W.config(cfg, 1 / 16)
     ref, _ = oracle_seal(oracle_mod, b)
     ciphers = install_keys(engine, b)
     db = DeviceBatch(engine, b, ciphers)
