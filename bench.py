@@ -419,22 +419,26 @@ def bench_inproc(args):
 
     from nebula_amd import _lib as L
     from nebula_amd import workload as W
-    from nebula_amd.batch import DeviceBatch, install_keys
+    from nebula_amd.batch import DeviceBatch, install_keys_multi
     from nebula_amd.noiseutil import Engine
 
     cfg, m = args.config, args.gpus
     ndev = max(1, torch.cuda.device_count())
     spec = {1: (L.ALG_AESGCM, 65536, 1), 2: (L.ALG_AESGCM, 65536, 4096), 3: (L.ALG_CHACHAPOLY, 65536, 4096)}
-    engines, batches, ciphers, dbs = [], [], [], []
+    engines, batches, dbs = [], [], []
     for k in range(m):
         dev = k % ndev
         torch.cuda.set_device(dev)
         b = W.make_batch(*spec[cfg], seed=W.SEED ^ k, name=f"C{cfg + 1}") if cfg in spec else W.config(4)
-        e = Engine(dev, max_keys=4096)
-        cs = install_keys(e, b)
-        engines.append(e)
+        if batches:
+            b.keys = batches[0].keys  # one tunnel table over every engine (each its own packets)
+        engines.append(Engine(dev, max_keys=4096))
         batches.append(b)
-        ciphers.append(cs)
+    # each tunnel key is one install on every engine (neb_cipher_create_multi): the sharded calls
+    # refuse a shard whose engine holds another install in a slot its packets use
+    ciphers = install_keys_multi(engines, batches[0])
+    for e, b, cs in zip(engines, batches, ciphers):
+        torch.cuda.set_device(e.device)
         dbs.append(DeviceBatch(e, b, cs))
     streams = [torch.cuda.Stream(device=db.dev) for db in dbs]
     arr = (L.Shard * m)()

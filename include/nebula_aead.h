@@ -109,6 +109,12 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out);
 NEB_API int neb_engine_destroy(neb_engine* e);
 /* Device pointer to the engine's key table and the bytes per key record (for diagnostics). */
 NEB_API int neb_engine_info(const neb_engine* e, int* device, uint32_t* max_keys, uint32_t* key_record_bytes);
+/* stats[0..3]: slots of the per-packet pool (fixed, 4: streams + pinned staging shared by every
+ * thread's neb_encrypt_danger / neb_decrypt_danger), per-packet calls, calls that waited for a
+ * slot, keys installed (since creation). */
+NEB_API int neb_engine_stats(const neb_engine* e, uint64_t stats[4]);
+/* Every entry point restores the calling thread's current HIP device before it returns. Streams
+ * passed to the batch calls must stay alive until the work enqueued on them has completed. */
 /* Human-readable text of a return code. */
 NEB_API const char* neb_strerror(int rc);
 /* Detail of the last NEB_ERR_HIP / NEB_ERR_NO_DEVICE on the calling thread (HIP error string). */
@@ -119,6 +125,20 @@ NEB_API const char* neb_last_error(void);
 /* Install a 32-byte key: AES-256 key schedule + H = E_K(0^128) + H^1..H^16 (AESGCM), or the raw
  * ChaCha20 key (ChaChaPoly), computed on the device into the engine's key table. */
 NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out);
+/* Install n keys at once (keys = n x 32 bytes; out[n]): the tunnel keys a lighthouse or a rekey
+ * storm completes in one go (handshake_manager.go:752,877 -> connection_state.go:55-75 per tunnel).
+ * One launch of n workgroups and one synchronize instead of n; each key gets the lowest free
+ * slot in turn, as n calls of neb_cipher_create would. NEB_ERR_NO_KEY_SLOT (nothing installed)
+ * when fewer than n slots are free. */
+NEB_API int neb_cipher_create_batch(neb_engine* e, int alg, const uint8_t* keys, uint32_t n, neb_cipher** out);
+/* Install ONE tunnel key on every engine of a set (one per GPU; the engines used together by
+ * neb_*_batch_host_multi / neb_*_batch_sharded): the same key_id on all of them — the lowest slot
+ * free on every engine, reserved on all at once — or on none (NEB_ERR_NO_KEY_SLOT, or the error of
+ * the failing engine with the others rolled back). out[k] is the key's cipher on engines[k]; each
+ * is destroyed on its own. The installs share one identity that the multi-engine batch calls
+ * check (below). A tunnel has exactly one eKey / dKey (connection_state.go:37-49, 55-75). */
+NEB_API int neb_cipher_create_multi(neb_engine* const* engines, uint32_t nengines, int alg, const uint8_t key[32],
+                                    neb_cipher** out);
 /* Waits for the asynchronous batches this engine enqueued that may read the key — the last
  * single-key batch with it on each stream and the last mixed-key batch on each stream — then
  * clears the key record and frees its slot. Other work on the device is not waited for. The caller
@@ -186,12 +206,15 @@ NEB_API int neb_open_batch_host(neb_engine* e, int alg, const neb_desc* desc, ui
 
 /* ---- several GPUs in one process: contiguous shards, no collective ------------ */
 /* Packets are independent, so a batch shards by contiguous packet range over engines (one per GPU,
- * or several on one GPU): shard k takes packets [n*k/m, n*(k+1)/m) of m engines. Every engine must
- * hold the batch's keys at the same key_ids (install each tunnel key on every engine in the same
- * order: neb_cipher_create hands out the lowest free slot). */
+ * or several on one GPU): shard k takes packets [n*k/m, n*(k+1)/m) of m engines. A batch's keys
+ * are engine 0's: install each tunnel key on the set with neb_cipher_create_multi. A packet of
+ * shard k whose key_id names a slot where engine k does not hold the same install as engine 0
+ * (not installed there, destroyed and reinstalled on one engine, keys installed engine by engine)
+ * gets NEB_STATUS_BAD_KEY and is not touched — never sealed or opened with another key. */
 /* Host-resident batch (the arena in host memory, pinned or not): one host thread per engine runs
  * neb_seal_batch_host / neb_open_batch_host on its shard; returns when every shard is done, with
- * the first failing shard's return code (the other shards still complete). */
+ * the first failing shard's return code (the other shards still complete). A staged (not pinned)
+ * arena whose shards' byte spans overlap runs the shards one after another. */
 NEB_API int neb_seal_batch_host_multi(neb_engine* const* engines, uint32_t nengines, int alg, const neb_desc* desc,
                                       uint32_t n, uint8_t* arena, size_t arena_len, int32_t* status,
                                       uint32_t key_hint);
@@ -266,6 +289,12 @@ typedef struct neb_rx_packet {
 } neb_rx_packet;
 #define NEB_STATUS_NOT_MESSAGE 7 /* a valid header of an unencrypted type (handshake, recv error,
                                     outside.go:83-89): left to the control plane, untouched */
+/* Or-ed into neb_rx_packet.len by the caller for a datagram that readOutsidePackets' double-
+ * encryption check refuses (outside.go:66-74: not relayed, and the UDP source address is inside the
+ * node's own VPN networks, f.myVpnNetworksTable). The batch does not carry source addresses, so the
+ * caller makes that lookup; the gate then drops the packet as the reference does, right after
+ * IsValidSubType and before the handshake hand-off: NEB_STATUS_INVALID, nothing touched. */
+#define NEB_RX_OWN_SOURCE 0x80000000u
 /* Per packet, readOutsidePackets up to the decrypt, then Decrypt or VerifyRelay: h.Parse (len < 16:
  * NEB_STATUS_INVALID, header.go:143-146); version 1 and IsValidSubType (header.go:192-205), else
  * NEB_STATUS_INVALID (outside.go:49-64); Handshake / RecvError types -> NEB_STATUS_NOT_MESSAGE; no

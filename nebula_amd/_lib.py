@@ -42,6 +42,7 @@ HEADER_LEN = 16
 REJECT_HEADROOM = 1 << 40
 REJECT_AFTER_MESSAGES = (1 << 64) - 1 - REJECT_HEADROOM
 KEYS_MIXED = 0xFFFFFFFF
+RX_OWN_SOURCE = 0x80000000  # or-ed into neb_rx_packet.len: outside.go:66-74 refused the datagram
 
 # neb_desc (include/nebula_aead.h)
 DESC_DTYPE = np.dtype(
@@ -62,6 +63,9 @@ SIGNATURES = {
     "neb_strerror": (C.c_char_p, [_i]),
     "neb_last_error": (C.c_char_p, []),
     "neb_cipher_create": (_i, [_vp, _i, _u8p, C.POINTER(_vp)]),
+    "neb_cipher_create_batch": (_i, [_vp, _i, _u8p, _u32, _vp]),
+    "neb_cipher_create_multi": (_i, [_vp, _u32, _i, _u8p, _vp]),
+    "neb_engine_stats": (_i, [_vp, _vp]),
     "neb_cipher_destroy": (_i, [_vp]),
     "neb_cipher_key_id": (_u32, [_vp]),
     "neb_cipher_alg": (_i, [_vp]),

@@ -17,9 +17,18 @@ from .workload import Batch
 
 
 def install_keys(engine: Engine, b: Batch) -> List[CipherState]:
-    """Install every key of the batch (noise CipherFunc.Cipher) and return the CipherStates."""
+    """Install every key of the batch (noise CipherFunc.Cipher for each, in one device launch:
+    neb_cipher_create_batch) and return the CipherStates."""
     cf = CipherAESGCM if b.alg == L.ALG_AESGCM else CipherChaChaPoly
-    return [cf.Cipher(engine, bytes(b.keys[32 * i:32 * i + 32])) for i in range(b.nkeys)]
+    return cf.CipherBatch(engine, [bytes(b.keys[32 * i:32 * i + 32]) for i in range(b.nkeys)])
+
+
+def install_keys_multi(engines: List[Engine], b: Batch) -> List[List[CipherState]]:
+    """Every key of the batch on every engine of a set, each tunnel key one install shared by all
+    of them (neb_cipher_create_multi); result[k] = engine k's CipherStates, same key_ids on all."""
+    cf = CipherAESGCM if b.alg == L.ALG_AESGCM else CipherChaChaPoly
+    per_key = [cf.CipherMulti(engines, bytes(b.keys[32 * i:32 * i + 32])) for i in range(b.nkeys)]
+    return [[cs[k] for cs in per_key] for k in range(len(engines))]
 
 
 def slot_desc(b: Batch, ciphers: List[CipherState]) -> np.ndarray:

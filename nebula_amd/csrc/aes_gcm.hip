@@ -1329,7 +1329,14 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
 __device__ uint8_t sbox_b(uint32_t x) { return (uint8_t)(c_T0.t[x & 255u] >> 8); }
 __device__ uint8_t xtime_d(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
 
-__global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __restrict__ key, uint32_t* __restrict__ rec) {
+// One workgroup per key of a batch install (neb_cipher_create_batch: n keys in one launch); the
+// workgroup first clears its record (the slot may have held another key or algorithm).
+__global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ slots,
+                                                            uint32_t* __restrict__ table) {
+    const uint8_t* key = keys + 32u * blockIdx.x;
+    uint32_t* rec = table + (size_t)slots[blockIdx.x] * kKeyRecDwords;
+    for (uint32_t j = threadIdx.x; j < kKeyRecDwords; j += blockDim.x) rec[j] = 0u;
     __shared__ uint4 hp[16];      // H^1..H^16
     __shared__ uint4 basis[128];  // x^i · H^kFullPow
     __shared__ uint4 basis8[32];  // x^i · H^8
@@ -1521,8 +1528,10 @@ extern "C" hipError_t neb_gcm_probe(void) {
     return hipFuncGetAttributes(&attr, (const void*)neb::gcm_single_kernel<false>);
 }
 
-extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s) {
-    hipLaunchKernelGGL(neb::gcm_key_setup_kernel, dim3(1), dim3(256), 0, s, d_key, d_rec);
+extern "C" hipError_t neb_gcm_key_setup(const uint8_t* keys, const uint32_t* slots, uint32_t n, uint32_t* table,
+                                        hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(neb::gcm_key_setup_kernel, dim3(n), dim3(256), 0, s, keys, slots, table);
     return hipGetLastError();
 }
 

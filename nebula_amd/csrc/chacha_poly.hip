@@ -379,18 +379,29 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
     }
 }
 
-__global__ void chacha_key_setup_kernel(const uint8_t* __restrict__ key, uint32_t* __restrict__ rec) {
+// Key install of a batch of keys, one workgroup per key: the record is cleared (it may have held
+// another algorithm's key) and the raw key written, its algorithm tag last.
+__global__ __launch_bounds__(256) void chacha_key_setup_kernel(const uint8_t* __restrict__ keys,
+                                                               const uint32_t* __restrict__ slots,
+                                                               uint32_t* __restrict__ table) {
+    const uint8_t* key = keys + 32u * blockIdx.x;
+    uint32_t* rec = table + (size_t)slots[blockIdx.x] * kKeyRecDwords;
+    for (uint32_t j = threadIdx.x; j < kKeyRecDwords; j += blockDim.x) rec[j] = 0u;
+    __syncthreads();
     const uint32_t i = threadIdx.x;
     if (i < 8u)
         rec[kRecChaKey + i] = (uint32_t)key[4 * i] | (uint32_t)key[4 * i + 1] << 8 | (uint32_t)key[4 * i + 2] << 16 |
                               (uint32_t)key[4 * i + 3] << 24;
+    __syncthreads();
     if (i == 0) rec[kRecAlg] = NEB_ALG_CHACHAPOLY;
 }
 
 }  // namespace neb
 
-extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s) {
-    hipLaunchKernelGGL(neb::chacha_key_setup_kernel, dim3(1), dim3(64), 0, s, d_key, d_rec);
+extern "C" hipError_t neb_chacha_key_setup(const uint8_t* keys, const uint32_t* slots, uint32_t n, uint32_t* table,
+                                           hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(neb::chacha_key_setup_kernel, dim3(n), dim3(256), 0, s, keys, slots, table);
     return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -16,12 +17,19 @@
 #include <vector>
 
 #include "../../include/nebula_aead.h"
+#include "hip_guard.hpp"
 #include "host_common.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
 #include "tx.hpp"
 
-extern "C" hipError_t neb_gcm_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
+// n keys (32 B each, mapped host memory) into the records of key slots slots[0..n): one launch
+extern "C" hipError_t neb_gcm_key_setup(const uint8_t* keys, const uint32_t* slots, uint32_t n, uint32_t* table,
+                                        hipStream_t s);
+extern "C" hipError_t neb_chacha_key_setup(const uint8_t* keys, const uint32_t* slots, uint32_t n, uint32_t* table,
+                                           hipStream_t s);
+extern "C" hipError_t neb_fence_keys(const neb_desc* in, neb_desc* out, uint32_t n, const uint8_t* bad,
+                                     uint32_t nbad, hipStream_t s);
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
@@ -36,7 +44,6 @@ extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int
 #ifndef NEB_TX_CSUM_SEAL
 #define NEB_TX_CSUM_SEAL 1  // 0: the segment kernel sums every checksum (A/B)
 #endif
-extern "C" hipError_t neb_chacha_key_setup(const uint8_t* d_key, uint32_t* d_rec, hipStream_t s);
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
@@ -115,12 +122,28 @@ struct TxSpace {
     std::mutex mu;
 };
 
-// Per-packet staging of one thread on one engine: pinned, mapped host memory the kernel reads and
-// writes in place ([desc 64 B | status 64 B | aad | payload + tag]), and the thread's own stream.
+// Per-packet CipherState calls (neb_encrypt_danger / neb_decrypt_danger) and key installs share a
+// fixed pool of kPktSlots slots per engine: a stream and pinned, mapped staging the kernel reads
+// and writes in place ([desc 64 B | status 64 B | aad | payload + tag]). The box grants a process 4
+// hardware queues, so more streams only queue behind each other in the driver. A call takes a
+// ticket t and runs on slot t mod kPktSlots once that slot's turn reaches t / kPktSlots: FIFO per
+// slot, so a call waits only for the calls ahead of it, however many threads call. (Round 3 gave
+// every calling OS thread its own slot and stream, kept until the engine died: the count grew with
+// the threads cgo ever used, a thread alternating over more than 8 engines leaked one per call, and
+// at 64 threads p99 was 100x p50.)
+constexpr uint32_t kPktSlots = 4;
 struct PktSlot {
     hipStream_t stream = nullptr;
     uint8_t* h = nullptr;
     size_t cap = 0;
+    std::atomic<uint64_t> turn{0};
+    std::mutex mu;
+    std::condition_variable cv;
+};
+struct PktPool {
+    std::atomic<uint64_t> ticket{0};
+    std::atomic<uint64_t> calls{0}, waits{0};
+    PktSlot slot[kPktSlots];
 };
 struct KeyUse {
     hipStream_t s;
@@ -133,13 +156,16 @@ struct neb_engine {
     hipStream_t stream = nullptr;
     uint32_t max_keys = 0;
     uint32_t* d_keys = nullptr;
-    std::vector<int> slot_alg;  // 0 = free
+    std::vector<int> slot_alg;  // 0 = free, -1 = reserved by an install in progress
+    // Install id of the key in each slot (0 = none): unique per neb_cipher_create /
+    // neb_cipher_create_batch key, shared by the engines of one neb_cipher_create_multi. Batches
+    // over several engines check that every shard's engine holds the same install as engine 0.
+    std::vector<uint64_t> slot_tag;
+    uint64_t key_epoch = 0;  // bumped by every install and destroy (under key_mu)
     std::mutex key_mu;
-    uint64_t gen = 0;  // unique per engine (a thread's cached packet slot names its engine by it)
+    uint64_t installs = 0;
 
-    // Per-packet CipherState calls: one staging slot and stream per calling thread (PktSlot).
-    std::mutex pkt_mu;
-    std::vector<PktSlot*> pkt_slots;
+    PktPool pkt;  // per-packet calls and key installs
 
     // Asynchronous batches still queued when a key is destroyed: per key slot, the last
     // single-key batch the engine launched on each stream, and the last mixed-key batch per
@@ -183,6 +209,7 @@ struct neb_cipher {
     neb_engine* e;
     uint32_t key_id;
     int alg;
+    uint64_t tag;  // neb_engine::slot_tag of the install
 };
 
 static thread_local char g_last_error[256] = "";
@@ -200,51 +227,55 @@ static void set_error(const char* where, hipError_t err) {
         }                                           \
     } while (0)
 
-// The calling thread's packet slot on engine e, with room for `bytes` (created on first use).
-// A thread caches its slots by engine generation: a destroyed engine's slots are never used again,
-// even if a new engine lands at the same address.
-static std::atomic<uint64_t> g_engine_gen{1};
-static PktSlot* pkt_slot(neb_engine* e, size_t bytes) {
-    struct Cached {
-        uint64_t gen;
-        PktSlot* s;
-    };
-    thread_local Cached cache[8] = {};
-    PktSlot* sl = nullptr;
-    for (auto& c : cache)
-        if (c.gen == e->gen) sl = c.s;
-    if (!sl) {
-        sl = new (std::nothrow) PktSlot;
-        if (!sl) return nullptr;
-        if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) {
-            set_error("hipStreamCreateWithFlags", hipGetLastError());
-            delete sl;
-            return nullptr;
+// Exclusive use of one slot of e's per-packet pool for the lifetime of the lease (PktPool).
+class PktLease {
+  public:
+    explicit PktLease(PktPool& p) {
+        const uint64_t t = p.ticket.fetch_add(1, std::memory_order_relaxed);
+        s_ = &p.slot[t % kPktSlots];
+        want_ = t / kPktSlots;
+        p.calls.fetch_add(1, std::memory_order_relaxed);
+        if (s_->turn.load(std::memory_order_acquire) == want_) return;
+        p.waits.fetch_add(1, std::memory_order_relaxed);
+        // a call holds its slot ≈ 30 µs: yield a few times before sleeping on the slot
+        for (int i = 0; i < 16; i++) {
+            std::this_thread::yield();
+            if (s_->turn.load(std::memory_order_acquire) == want_) return;
         }
-        {
-            std::lock_guard<std::mutex> g(e->pkt_mu);
-            e->pkt_slots.push_back(sl);
-        }
-        Cached* victim = &cache[0];
-        for (auto& c : cache)
-            if (c.gen == 0) victim = &c;
-        *victim = {e->gen, sl};
+        std::unique_lock<std::mutex> g(s_->mu);
+        s_->cv.wait(g, [&] { return s_->turn.load(std::memory_order_acquire) == want_; });
     }
-    if (bytes > sl->cap) {
-        if (sl->h) hipHostFree(sl->h);
-        sl->h = nullptr;
-        sl->cap = 0;
+    ~PktLease() {
+        {
+            std::lock_guard<std::mutex> g(s_->mu);  // no lost wake-up between a waiter's check and its sleep
+            s_->turn.store(want_ + 1, std::memory_order_release);
+        }
+        s_->cv.notify_all();
+    }
+    PktLease(const PktLease&) = delete;
+    PktLease& operator=(const PktLease&) = delete;
+    PktSlot* operator->() const { return s_; }
+    // room for `bytes` of staging (the slot is exclusively ours; its stream is idle between leases)
+    bool reserve(size_t bytes) {
+        if (bytes <= s_->cap) return true;
+        if (s_->h) hipHostFree(s_->h);
+        s_->h = nullptr;
+        s_->cap = 0;
         const size_t cap = std::max(kStageMin, align_up(bytes, 1 << 16));
-        hipError_t err = hipHostMalloc((void**)&sl->h, cap, hipHostMallocDefault);
+        hipError_t err = hipHostMalloc((void**)&s_->h, cap, hipHostMallocDefault);
         if (err != hipSuccess) {
             set_error("hipHostMalloc", err);
-            sl->h = nullptr;
-            return nullptr;
+            s_->h = nullptr;
+            return false;
         }
-        sl->cap = cap;
+        s_->cap = cap;
+        return true;
     }
-    return sl;
-}
+
+  private:
+    PktSlot* s_ = nullptr;
+    uint64_t want_ = 0;
+};
 
 // After an asynchronous batch is enqueued on stream s: remember it for neb_cipher_destroy (the
 // key_hint's slot, or every slot for a mixed-key batch). Events skip the system-scope cache
@@ -309,6 +340,7 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
         return NEB_ERR_NO_DEVICE;
     }
     int cus = 0;
+    DeviceGuard dg;
     if ((err = hipSetDevice(device)) != hipSuccess ||
         (err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess) {
         set_error("hipSetDevice/hipDeviceGetAttribute", err);
@@ -324,13 +356,17 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
     e->device = device;
     e->cu_count = cus;
     e->max_keys = max_keys;
-    e->gen = g_engine_gen.fetch_add(1);
     e->slot_alg.assign(max_keys, 0);
+    e->slot_tag.assign(max_keys, 0);
     e->key_use.resize(max_keys);
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess ||
-        hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) != hipSuccess ||
-        hipStreamSynchronize(nullptr) != hipSuccess) {  // the null-stream memset, before any stream reads keys
+    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) == hipSuccess &&
+              hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) == hipSuccess &&
+              hipStreamSynchronize(nullptr) == hipSuccess;  // the null-stream memset, before any stream reads keys
+    for (PktSlot& sl : e->pkt.slot)
+        ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess &&
+             hipHostMalloc((void**)&sl.h, kStageMin, hipHostMallocDefault) == hipSuccess && (sl.cap = kStageMin);
+    if (!ok) {
         set_error("engine allocation", hipGetLastError());
         neb_engine_destroy(e);
         return NEB_ERR_HIP;
@@ -341,7 +377,7 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
 
 NEB_API int neb_engine_destroy(neb_engine* e) {
     if (!e) return NEB_ERR_INVALID;
-    hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     if (e->stream) hipStreamSynchronize(e->stream);
     for (auto& s : e->pipe) {
         if (s.stream) { hipStreamSynchronize(s.stream); hipStreamDestroy(s.stream); }
@@ -378,10 +414,9 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
     if (e->zc_desc) hipFree(e->zc_desc);
     if (e->zc_status) hipFree(e->zc_status);
     if (e->d_keys) hipFree(e->d_keys);
-    for (PktSlot* sl : e->pkt_slots) {
-        if (sl->stream) { hipStreamSynchronize(sl->stream); hipStreamDestroy(sl->stream); }
-        if (sl->h) hipHostFree(sl->h);
-        delete sl;
+    for (PktSlot& sl : e->pkt.slot) {
+        if (sl.stream) { hipStreamSynchronize(sl.stream); hipStreamDestroy(sl.stream); }
+        if (sl.h) hipHostFree(sl.h);
     }
     for (auto& v : e->key_use)
         for (KeyUse& u : v) hipEventDestroy(u.ev);
@@ -399,69 +434,196 @@ NEB_API int neb_engine_info(const neb_engine* e, int* device, uint32_t* max_keys
     return NEB_OK;
 }
 
+NEB_API int neb_engine_stats(const neb_engine* e, uint64_t stats[4]) {
+    if (!e || !stats) return NEB_ERR_INVALID;
+    stats[0] = kPktSlots;
+    stats[1] = e->pkt.calls.load(std::memory_order_relaxed);
+    stats[2] = e->pkt.waits.load(std::memory_order_relaxed);
+    std::lock_guard<std::mutex> g(const_cast<neb_engine*>(e)->key_mu);
+    stats[3] = e->installs;
+    return NEB_OK;
+}
+
 NEB_API const char* neb_cipher_name(int alg) {
     return alg == NEB_ALG_AESGCM ? "AESGCM" : alg == NEB_ALG_CHACHAPOLY ? "ChaChaPoly" : nullptr;
 }
 
-NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out) {
-    if (!e || !key || !out || (alg != NEB_ALG_AESGCM && alg != NEB_ALG_CHACHAPOLY)) return NEB_ERR_INVALID;
-    *out = nullptr;
-    uint32_t slot;
-    {
-        std::lock_guard<std::mutex> g(e->key_mu);
-        auto it = std::find(e->slot_alg.begin(), e->slot_alg.end(), 0);
-        if (it == e->slot_alg.end()) return NEB_ERR_NO_KEY_SLOT;
-        slot = (uint32_t)(it - e->slot_alg.begin());
-        *it = -1;  // reserved
+static std::atomic<uint64_t> g_key_tag{1};
+
+// Reserve the n lowest free slots of e (caller holds e->key_mu); false if fewer are free.
+static bool reserve_slots(neb_engine* e, uint32_t n, uint32_t* slots) {
+    uint32_t k = 0;
+    for (uint32_t s = 0; s < e->max_keys && k < n; s++)
+        if (e->slot_alg[s] == 0) slots[k++] = s;
+    if (k < n) return false;
+    for (uint32_t i = 0; i < n; i++) e->slot_alg[slots[i]] = -1;
+    return true;
+}
+
+// Key install of n keys into the reserved slots slots[0..n), one launch: the keys and slot numbers go
+// through one slot of the per-packet pool (pinned, mapped: the setup kernel reads them there), each
+// workgroup clears its record and installs one key, and the staged key bytes are wiped afterwards.
+// On failure the records are cleared again, so no slot is left holding a half-written record
+// whose algorithm tag a batch could accept.
+static int install_records(neb_engine* e, int alg, const uint8_t* keys, const uint32_t* slots, uint32_t n) {
+    DeviceGuard dg(e->device);
+    PktLease sl(e->pkt);
+    const size_t kb = align_up((size_t)n * 32u, 64);
+    if (!sl.reserve(kb + (size_t)n * 4u)) return NEB_ERR_HIP;
+    std::memcpy(sl->h, keys, (size_t)n * 32u);
+    std::memcpy(sl->h + kb, slots, (size_t)n * 4u);
+    hipError_t err = alg == NEB_ALG_AESGCM
+                         ? neb_gcm_key_setup(sl->h, (const uint32_t*)(sl->h + kb), n, e->d_keys, sl->stream)
+                         : neb_chacha_key_setup(sl->h, (const uint32_t*)(sl->h + kb), n, e->d_keys, sl->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(sl->stream);
+    std::memset(sl->h, 0, (size_t)n * 32u);
+    if (err != hipSuccess) {
+        set_error("key setup", err);
+        for (uint32_t i = 0; i < n; i++)
+            (void)hipMemsetAsync(e->d_keys + (size_t)slots[i] * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, sl->stream);
+        (void)hipStreamSynchronize(sl->stream);
+        return NEB_ERR_HIP;
     }
-    int rc = NEB_OK;
-    {
-        // the key goes through the calling thread's pinned slot: the setup kernel reads it there
-        // (mapped host memory) on the thread's stream, then the slot's copy is wiped
-        hipSetDevice(e->device);
-        PktSlot* sl = pkt_slot(e, 64);
-        if (!sl) {
-            rc = NEB_ERR_HIP;
-        } else {
-            std::memcpy(sl->h, key, 32);
-            uint32_t* rec = e->d_keys + (size_t)slot * neb::kKeyRecDwords;
-            hipError_t err = hipMemsetAsync(rec, 0, neb::kKeyRecBytes, sl->stream);
-            if (err == hipSuccess)
-                err = alg == NEB_ALG_AESGCM ? neb_gcm_key_setup(sl->h, rec, sl->stream)
-                                            : neb_chacha_key_setup(sl->h, rec, sl->stream);
-            if (err == hipSuccess) err = hipStreamSynchronize(sl->stream);
-            std::memset(sl->h, 0, 32);
-            if (err != hipSuccess) {
-                set_error("key setup", err);
-                rc = NEB_ERR_HIP;
-            }
+    return NEB_OK;
+}
+
+// Publish (rc == NEB_OK) or release the reserved slots; caller holds e->key_mu.
+static void commit_slots(neb_engine* e, int alg, const uint32_t* slots, const uint64_t* tags, uint32_t n, bool ok) {
+    for (uint32_t i = 0; i < n; i++) {
+        e->slot_alg[slots[i]] = ok ? alg : 0;
+        e->slot_tag[slots[i]] = ok ? tags[i] : 0;
+    }
+    if (ok) {
+        e->installs += n;
+        e->key_epoch++;
+    }
+}
+
+static bool valid_alg(int alg) { return alg == NEB_ALG_AESGCM || alg == NEB_ALG_CHACHAPOLY; }
+
+NEB_API int neb_cipher_create_batch(neb_engine* e, int alg, const uint8_t* keys, uint32_t n, neb_cipher** out) {
+    if (!e || !out || !valid_alg(alg) || (n && !keys)) return NEB_ERR_INVALID;
+    if (n == 0) return NEB_OK;
+    for (uint32_t i = 0; i < n; i++) out[i] = nullptr;
+    std::vector<uint32_t> slots(n);
+    std::vector<uint64_t> tags(n);
+    std::vector<neb_cipher*> cs(n, nullptr);
+    for (uint32_t i = 0; i < n; i++) {
+        cs[i] = new (std::nothrow) neb_cipher{e, 0, alg, 0};
+        if (!cs[i]) {
+            for (neb_cipher* c : cs) delete c;
+            return NEB_ERR_INVALID;
         }
     }
+    {
+        std::lock_guard<std::mutex> g(e->key_mu);
+        if (!reserve_slots(e, n, slots.data())) {
+            for (neb_cipher* c : cs) delete c;
+            return NEB_ERR_NO_KEY_SLOT;
+        }
+    }
+    const int rc = install_records(e, alg, keys, slots.data(), n);
+    const uint64_t t0 = g_key_tag.fetch_add(n);
+    for (uint32_t i = 0; i < n; i++) tags[i] = t0 + i;
     std::lock_guard<std::mutex> g(e->key_mu);
-    if (rc != NEB_OK) {
-        e->slot_alg[slot] = 0;
-        return rc;
+    commit_slots(e, alg, slots.data(), tags.data(), n, rc == NEB_OK);
+    for (uint32_t i = 0; i < n; i++) {
+        if (rc != NEB_OK) {
+            delete cs[i];
+            continue;
+        }
+        cs[i]->key_id = slots[i];
+        cs[i]->tag = tags[i];
+        out[i] = cs[i];
     }
-    neb_cipher* c = new (std::nothrow) neb_cipher{e, slot, alg};
-    if (!c) {
-        e->slot_alg[slot] = 0;
-        return NEB_ERR_INVALID;
+    return rc;
+}
+
+NEB_API int neb_cipher_create(neb_engine* e, int alg, const uint8_t key[32], neb_cipher** out) {
+    if (!e || !key || !out || !valid_alg(alg)) return NEB_ERR_INVALID;
+    *out = nullptr;
+    return neb_cipher_create_batch(e, alg, key, 1, out);
+}
+
+NEB_API int neb_cipher_create_multi(neb_engine* const* engines, uint32_t m, int alg, const uint8_t key[32],
+                                    neb_cipher** out) {
+    if (!engines || m == 0 || !key || !out || !valid_alg(alg)) return NEB_ERR_INVALID;
+    std::vector<neb_engine*> es(engines, engines + m);
+    for (uint32_t k = 0; k < m; k++) {
+        out[k] = nullptr;
+        if (!es[k]) return NEB_ERR_INVALID;
     }
-    e->slot_alg[slot] = alg;
-    *out = c;
-    return NEB_OK;
+    std::vector<neb_engine*> order = es;
+    std::sort(order.begin(), order.end());
+    if (std::adjacent_find(order.begin(), order.end()) != order.end()) return NEB_ERR_INVALID;  // an engine twice
+    std::vector<neb_cipher*> cs(m, nullptr);
+    for (uint32_t k = 0; k < m; k++)
+        if (!(cs[k] = new (std::nothrow) neb_cipher{es[k], 0, alg, 0})) {
+            for (neb_cipher* c : cs) delete c;
+            return NEB_ERR_INVALID;
+        }
+    // the lowest slot free on every engine, reserved on all of them at once (engines locked in
+    // address order, so two concurrent multi-installs cannot deadlock)
+    uint32_t slot = 0;
+    {
+        for (neb_engine* e : order) e->key_mu.lock();
+        uint32_t lim = ~0u;
+        for (neb_engine* e : es) lim = std::min(lim, e->max_keys);
+        bool found = false;
+        for (; slot < lim && !found; slot++) {
+            found = true;
+            for (neb_engine* e : es) found = found && e->slot_alg[slot] == 0;
+            if (found) break;
+        }
+        if (found)
+            for (neb_engine* e : es) e->slot_alg[slot] = -1;
+        for (neb_engine* e : order) e->key_mu.unlock();
+        if (!found) {
+            for (neb_cipher* c : cs) delete c;
+            return NEB_ERR_NO_KEY_SLOT;
+        }
+    }
+    int rc = NEB_OK;
+    std::vector<int> done(m, 0);
+    for (uint32_t k = 0; k < m && rc == NEB_OK; k++) {
+        rc = install_records(es[k], alg, key, &slot, 1);
+        done[k] = rc == NEB_OK;
+    }
+    const uint64_t tag = g_key_tag.fetch_add(1);
+    for (uint32_t k = 0; k < m; k++) {
+        neb_engine* e = es[k];
+        if (rc != NEB_OK && done[k]) {  // roll back the engines that had installed it
+            DeviceGuard dg(e->device);
+            PktLease sl(e->pkt);
+            (void)hipMemsetAsync(e->d_keys + (size_t)slot * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, sl->stream);
+            (void)hipStreamSynchronize(sl->stream);
+        }
+        std::lock_guard<std::mutex> g(e->key_mu);
+        commit_slots(e, alg, &slot, &tag, 1, rc == NEB_OK);
+        if (rc == NEB_OK) {
+            cs[k]->key_id = slot;
+            cs[k]->tag = tag;
+            out[k] = cs[k];
+        } else {
+            delete cs[k];
+        }
+    }
+    return rc;
 }
 
 NEB_API int neb_cipher_destroy(neb_cipher* c) {
     if (!c) return NEB_ERR_INVALID;
     neb_engine* e = c->e;
     const uint32_t slot = c->key_id;
-    hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     // Asynchronous batches the engine enqueued that may read this record: the last single-key
     // batch with this key on each stream, the last mixed-key batch on each stream (note_use), and
-    // the mixed-key AES-GCM batches of the engine's scheduler workspace (its `done` event: the last
-    // user's, and each user waited for the one before). Only those are waited for — not the
-    // device, so another tunnel's batches in flight elsewhere do not stall a teardown or rekey.
+    // the mixed-key AES-GCM batches of the engine's scheduler workspace. Those have no key-use
+    // marker of their own (it cost ≈ 5 µs per batch): the workspace's `done` event is recorded
+    // after each and every later user waits for it, so the destroy waits for the workspace's
+    // latest batch — which may be another tunnel's batch enqueued after the last one that used
+    // this key, so a teardown can wait behind unrelated mixed-key traffic on this engine (at most
+    // the batches enqueued before the destroy; never the whole device).
     // The caller stops enqueuing with a key before destroying it.
     std::vector<hipEvent_t> wait;
     {
@@ -475,11 +637,13 @@ NEB_API int neb_cipher_destroy(neb_cipher* c) {
     }
     for (hipEvent_t ev : wait) (void)hipEventSynchronize(ev);
     int rc = NEB_OK;
-    PktSlot* sl = pkt_slot(e, 64);
-    if (!sl || hipMemsetAsync(e->d_keys + (size_t)slot * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, sl->stream) !=
-                   hipSuccess ||
-        hipStreamSynchronize(sl->stream) != hipSuccess)
-        rc = NEB_ERR_HIP;
+    {
+        PktLease sl(e->pkt);
+        if (hipMemsetAsync(e->d_keys + (size_t)slot * neb::kKeyRecDwords, 0, neb::kKeyRecBytes, sl->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(sl->stream) != hipSuccess)
+            rc = NEB_ERR_HIP;
+    }
     {
         std::lock_guard<std::mutex> g(e->use_mu);
         for (KeyUse& u : e->key_use[slot]) hipEventDestroy(u.ev);
@@ -488,6 +652,8 @@ NEB_API int neb_cipher_destroy(neb_cipher* c) {
     {
         std::lock_guard<std::mutex> g(e->key_mu);
         e->slot_alg[slot] = 0;
+        e->slot_tag[slot] = 0;
+        e->key_epoch++;
     }
     delete c;
     return rc;
@@ -593,20 +759,19 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
                             s, hdr_from_dst);
 }
 
-// One packet through the device, on the calling thread's own slot and stream (PktSlot): the packet
-// is copied into the slot's pinned, mapped buffer ([desc | status | aad | payload (+tag)]), the
-// batch kernel seals or opens it there in place (zero-copy: no DMA either way) and the result is
-// copied out. Threads never share a slot, so concurrent calls from Nebula's routines run side by
-// side instead of queueing on one lock.
+// One packet through the device, on a slot of the engine's per-packet pool (PktPool): the packet is
+// copied into the slot's pinned, mapped buffer ([desc | status | aad | payload (+tag)]), the batch
+// kernel seals or opens it there in place (zero-copy: no DMA either way) and the result is copied
+// out. Up to kPktSlots calls run side by side; later ones wait their turn in FIFO order.
 static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len, const uint8_t* in, size_t in_len,
                       size_t pay_len, uint64_t n, uint8_t* dst, int32_t* st_out) {
     neb_engine* e = c->e;
     const size_t o_desc = 0, o_status = 64, o_aad = 128;
     const size_t o_pay = align_up(o_aad + ad_len, 16);
     const size_t total = o_pay + pay_len + 16;
-    hipSetDevice(e->device);
-    PktSlot* sl = pkt_slot(e, total);
-    if (!sl) return NEB_ERR_HIP;
+    DeviceGuard dg(e->device);
+    PktLease sl(e->pkt);
+    if (!sl.reserve(total)) return NEB_ERR_HIP;
     uint8_t* h = sl->h;
     neb_desc d{};
     d.src_off = o_pay - o_aad;
@@ -685,7 +850,7 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
     if (rc != NEB_OK) return rc;
     if (n == 0) return NEB_OK;
     if (!d_desc || !d_arena || !d_status) return NEB_ERR_INVALID;
-    hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream, as for any HIP launch
     // a single-key AES-GCM batch binds its key-use event to its last kernel (no marker after it)
     const bool bound = alg == NEB_ALG_AESGCM && key_hint != NEB_KEYS_MIXED;
@@ -744,7 +909,7 @@ void neb_sched_space_free(void* p) {
 int neb_launch_on(neb_engine* e, int alg, int open, const neb_desc* desc, uint32_t n, uint8_t* arena,
                   int32_t* status, uint32_t key_hint, hipStream_t s, void* sched) {
     if (n == 0) return NEB_OK;
-    hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     hipError_t err = launch_batch(e, alg, open, desc, n, arena, status, key_hint, s, nullptr,
                                   static_cast<SchedSpace*>(sched));
     if (err != hipSuccess) {
@@ -815,7 +980,7 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
     for (uint32_t i = 0; i < n; i++)
         if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
     std::lock_guard<std::mutex> g(e->pipe_mu);
-    hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     // The kernels' vector fast path tests the absolute address (arena base + offset), so a mapped
     // arena at any byte address runs zero-copy. A staged arena lands in a device buffer with the
     // same alignment modulo 16, so the kernels take the same paths either way.
@@ -1041,7 +1206,7 @@ NEB_API int neb_tx_seal_batch(neb_engine* e, int alg, neb_tx_tunnel* d_tunnels, 
     if (!d_nwires || (npackets && (!d_packets || !d_in || !d_packet_status || !d_tunnels)) ||
         (max_wires && (!d_out || !d_wires || !d_wire_status)))
         return NEB_ERR_INVALID;
-    hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     hipStream_t s = (hipStream_t)stream;
     if (npackets == 0) {
         HIP_TRY(hipMemsetAsync(d_nwires, 0, sizeof(uint32_t), s));
@@ -1085,7 +1250,7 @@ NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnel
     std::vector<neb_tx_packet> rebased(packets, packets + npackets);
     for (auto& p : rebased) p.in_off -= lo;
     std::lock_guard<std::mutex> g(e->tx.mu);
-    hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     TxSpace& tx = e->tx;
     hipStream_t s = e->stream;
     if (total > tx.io_cap) {
@@ -1128,6 +1293,50 @@ NEB_API int neb_tx_seal_batch_host(neb_engine* e, int alg, neb_tx_tunnel* tunnel
 
 // ---- several engines --------------------------------------------------------------
 
+// One tunnel key is one install on every engine (a tunnel has exactly one eKey / dKey,
+// connection_state.go:37-49): shard k may use a key slot only if engine k holds there the same
+// install (slot_tag) as engine 0, whose key table defines the batch's keys. Keys put on every
+// engine by one neb_cipher_create_multi agree; anything else — a slot destroyed and reinstalled
+// on one engine, keys installed engine by engine — does not, and the packets of shard k that name
+// such a slot get NEB_STATUS_BAD_KEY instead of being sealed or opened with another tunnel's key.
+// bad[k] flags engine k's disagreeing slots (empty when all agree; any = some engine disagrees).
+struct KeyFence {
+    std::vector<std::vector<uint8_t>> bad;
+    bool any = false;
+    bool bad_key(uint32_t k, uint32_t key) const { return key < bad[k].size() && bad[k][key]; }
+};
+static KeyFence key_fence(neb_engine* const* es, uint32_t m) {
+    KeyFence f;
+    f.bad.resize(m);
+    std::vector<neb_engine*> order(es, es + m);
+    std::sort(order.begin(), order.end());
+    order.erase(std::unique(order.begin(), order.end()), order.end());
+    if (order.size() < 2) return f;
+    for (neb_engine* e : order) e->key_mu.lock();
+    for (uint32_t k = 1; k < m; k++) {
+        neb_engine* a = es[0];
+        neb_engine* b = es[k];
+        if (a == b) continue;
+        const uint32_t nk = std::max(a->max_keys, b->max_keys);
+        std::vector<uint8_t> v(nk, 0);
+        bool anyk = false;
+        for (uint32_t s = 0; s < nk; s++) {
+            const uint64_t ta = s < a->max_keys ? a->slot_tag[s] : 0, tb = s < b->max_keys ? b->slot_tag[s] : 0;
+            const int aa = s < a->max_keys ? a->slot_alg[s] : 0, ab = s < b->max_keys ? b->slot_alg[s] : 0;
+            if (ta != tb || aa != ab) v[s] = 1, anyk = true;
+        }
+        if (anyk) {
+            f.bad[k] = std::move(v);
+            f.any = true;
+        }
+    }
+    for (neb_engine* e : order) e->key_mu.unlock();
+    return f;
+}
+
+// Shard k of m: packets [n*k/m, n*(k+1)/m).
+static inline uint32_t shard_lo(uint32_t n, uint32_t k, uint32_t m) { return (uint32_t)((uint64_t)n * k / m); }
+
 static int batch_host_multi(neb_engine* const* engines, uint32_t m, int alg, int open, const neb_desc* desc,
                             uint32_t n, uint8_t* arena, size_t arena_len, int32_t* status, uint32_t key_hint) {
     if (!engines || m == 0 || (n && (!desc || !arena || !status))) return NEB_ERR_INVALID;
@@ -1136,16 +1345,65 @@ static int batch_host_multi(neb_engine* const* engines, uint32_t m, int alg, int
     // every descriptor checked before any shard starts: an invalid batch touches nothing
     for (uint32_t i = 0; i < n; i++)
         if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
-    std::vector<int> rc(m, NEB_OK);
-    std::vector<std::thread> th;
-    for (uint32_t k = 1; k < m; k++) {
-        const uint32_t b = (uint32_t)((uint64_t)n * k / m), c = (uint32_t)((uint64_t)n * (k + 1) / m) - b;
-        th.emplace_back([&, k, b, c] {
-            rc[k] = batch_host(engines[k], alg, open, desc + b, c, arena, arena_len, status + b, key_hint);
-        });
+    DeviceGuard dg;
+    const KeyFence fence = key_fence(engines, m);
+    // a shard whose engine disagrees on some keys runs on a copy of its descriptors with those
+    // packets' key_id pointing past every key table (the kernels give them NEB_STATUS_BAD_KEY); a
+    // single-key shard whose key disagrees is refused whole without a launch
+    std::vector<std::vector<neb_desc>> fenced(m);
+    std::vector<uint8_t> skip(m, 0);
+    if (fence.any)
+        for (uint32_t k = 1; k < m; k++) {
+            if (fence.bad[k].empty()) continue;
+            const uint32_t b = shard_lo(n, k, m), c = shard_lo(n, k + 1, m) - b;
+            if (key_hint != NEB_KEYS_MIXED) {
+                if (fence.bad_key(k, key_hint)) {
+                    skip[k] = 1;
+                    for (uint32_t i = 0; i < c; i++) status[b + i] = NEB_STATUS_BAD_KEY;
+                }
+                continue;
+            }
+            fenced[k].assign(desc + b, desc + b + c);
+            for (neb_desc& d : fenced[k])
+                if (fence.bad_key(k, d.key_id)) d.key_id = NEB_KEYS_MIXED - 1u;
+        }
+    auto run = [&](uint32_t k) -> int {
+        const uint32_t b = shard_lo(n, k, m), c = shard_lo(n, k + 1, m) - b;
+        if (skip[k]) return NEB_OK;
+        const neb_desc* dk = fenced[k].empty() ? desc + b : fenced[k].data();
+        return batch_host(engines[k], alg, open, dk, c, arena, arena_len, status + b, key_hint);
+    };
+    // A staged (not zero-copy) shard copies its whole arena span [lo & ~15, hi) in and back. Shards
+    // whose spans meet (packed, unaligned or interleaved descriptors) would write stale bytes over
+    // each other's results, so they run one after another; disjoint spans run side by side.
+    bool serial = false;
+    if (!(host_mode() == kHostZeroCopy && host_mapped(arena))) {
+        std::vector<std::pair<uint64_t, uint64_t>> span;
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t b = shard_lo(n, k, m), c = shard_lo(n, k + 1, m) - b;
+            if (c == 0 || skip[k]) continue;
+            uint64_t lo = ~0ULL, hi = 0;
+            for (uint32_t i = b; i < b + c; i++) {
+                const neb_desc& d = desc[i];
+                const uint64_t pay = (uint64_t)d.len + (open ? 16u : 0u), outl = (uint64_t)d.len + (open ? 0u : 16u);
+                lo = std::min({lo, d.src_off, d.dst_off, d.aad_off});
+                hi = std::max({hi, d.src_off + pay, d.dst_off + outl, d.aad_off + d.aad_len});
+            }
+            span.push_back({lo & ~(uint64_t)15, hi});
+        }
+        std::sort(span.begin(), span.end());
+        for (size_t i = 1; i < span.size(); i++)
+            if (span[i].first < span[i - 1].second) serial = true;
     }
-    rc[0] = batch_host(engines[0], alg, open, desc, (uint32_t)((uint64_t)n / m), arena, arena_len, status, key_hint);
-    for (auto& t : th) t.join();
+    std::vector<int> rc(m, NEB_OK);
+    if (serial) {
+        for (uint32_t k = 0; k < m; k++) rc[k] = run(k);
+    } else {
+        std::vector<std::thread> th;
+        for (uint32_t k = 1; k < m; k++) th.emplace_back([&, k] { rc[k] = run(k); });
+        rc[0] = run(0);
+        for (auto& t : th) t.join();
+    }
     for (int r : rc)
         if (r != NEB_OK) return r;
     return NEB_OK;
@@ -1165,13 +1423,51 @@ NEB_API int neb_open_batch_host_multi(neb_engine* const* engines, uint32_t nengi
 
 static int batch_sharded(int alg, int open, const neb_shard* sh, uint32_t m, uint32_t key_hint) {
     if (!sh || m == 0) return NEB_ERR_INVALID;
+    for (uint32_t k = 0; k < m; k++)
+        if (!sh[k].e) return NEB_ERR_INVALID;
+    DeviceGuard dg;
+    std::vector<neb_engine*> es(m);
+    for (uint32_t k = 0; k < m; k++) es[k] = sh[k].e;
+    const KeyFence fence = key_fence(es.data(), m);
+    // device copies of a fenced shard's descriptors (KeyFence; batch_host_multi), freed at the end
+    std::vector<void*> temps;
     int rc = NEB_OK;
     uint32_t launched = 0;
-    for (; launched < m && rc == NEB_OK; launched++)  // every shard queued first, then all waited for
-        rc = batch_device(sh[launched].e, alg, open, sh[launched].d_desc, sh[launched].n, sh[launched].d_arena,
-                          sh[launched].d_status, key_hint, sh[launched].stream);
+    for (; launched < m && rc == NEB_OK; launched++) {  // every shard queued first, then all waited for
+        const neb_shard& s = sh[launched];
+        const neb_desc* d_desc = s.d_desc;
+        if (fence.any && !fence.bad[launched].empty() && s.n) {
+            hipSetDevice(s.e->device);
+            hipStream_t st = (hipStream_t)s.stream;
+            if (key_hint != NEB_KEYS_MIXED) {
+                if (fence.bad_key(launched, key_hint)) {
+                    if (!s.d_status || hipMemsetD32Async((hipDeviceptr_t)s.d_status, NEB_STATUS_BAD_KEY, s.n, st) !=
+                                           hipSuccess)
+                        rc = s.d_status ? NEB_ERR_HIP : NEB_ERR_INVALID;
+                    continue;
+                }
+            } else {
+                const std::vector<uint8_t>& bad = fence.bad[launched];
+                void* t = nullptr;
+                const size_t db = align_up((size_t)s.n * sizeof(neb_desc), 256);
+                if (!s.d_desc || hipMalloc(&t, db + bad.size()) != hipSuccess) {
+                    rc = s.d_desc ? NEB_ERR_HIP : NEB_ERR_INVALID;
+                    continue;
+                }
+                temps.push_back(t);
+                uint8_t* d_bad = (uint8_t*)t + db;
+                if (hipMemcpyAsync(d_bad, bad.data(), bad.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+                    neb_fence_keys(s.d_desc, (neb_desc*)t, s.n, d_bad, (uint32_t)bad.size(), st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess) {  // `bad` is pageable and local
+                    rc = NEB_ERR_HIP;
+                    continue;
+                }
+                d_desc = (const neb_desc*)t;
+            }
+        }
+        rc = batch_device(s.e, alg, open, d_desc, s.n, s.d_arena, s.d_status, key_hint, s.stream);
+    }
     for (uint32_t k = 0; k < launched; k++) {
-        if (!sh[k].e) continue;
         hipSetDevice(sh[k].e->device);
         const hipError_t err = hipStreamSynchronize((hipStream_t)sh[k].stream);
         if (err != hipSuccess && rc == NEB_OK) {
@@ -1179,6 +1475,7 @@ static int batch_sharded(int alg, int open, const neb_shard* sh, uint32_t m, uin
             rc = NEB_ERR_HIP;
         }
     }
+    for (void* t : temps) hipFree(t);
     return rc;
 }
 

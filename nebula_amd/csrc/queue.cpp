@@ -6,6 +6,7 @@
 #include <new>
 #include <vector>
 
+#include "hip_guard.hpp"
 #include "queue_core.hpp"
 
 extern "C" {  // engine.cpp, internal
@@ -59,7 +60,7 @@ NEB_API int neb_queue_create(neb_engine* e, int alg, int open, const neb_queue_c
     q->dev.open = open;
     q->open = open;
     q->cfg = c;
-    hipSetDevice(neb_engine_device_of(e));
+    DeviceGuard dg(neb_engine_device_of(e));
     q->b.resize(c.depth);
     q->dev.stream.assign(c.depth, nullptr);
     q->dev.sched.assign(c.depth, nullptr);
@@ -87,7 +88,7 @@ NEB_API int neb_queue_create(neb_engine* e, int alg, int open, const neb_queue_c
 NEB_API int neb_queue_destroy(neb_queue* q) {
     if (!q) return NEB_ERR_INVALID;
     q->shutdown();
-    hipSetDevice(neb_engine_device_of(q->dev.e));
+    DeviceGuard dg(neb_engine_device_of(q->dev.e));
     for (hipStream_t st : q->dev.stream)
         if (st) hipStreamSynchronize(st);
     for (auto& x : q->b) {

@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) void rx_wire_kernel(const neb_rx_packet* __res
     if (i >= n) return;
     const neb_rx_packet p = pk[i];
     uint8_t h[16];
-    if (p.len >= 16u)
+    if (neb_rx_len(p) >= 16u)
         for (int k = 0; k < 16; k++) h[k] = arena[p.off + k];
     neb_desc d{p.off, p.off, p.off, 0, 0, 0, NEB_KEYS_MIXED, 0};
     const int32_t g = neb_rx_wire_gate(h, p, &d);

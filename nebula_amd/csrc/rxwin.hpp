@@ -132,17 +132,22 @@ extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const
 // NEB_STATUS_OK with *d describing the Decrypt (header as AAD, in place) or the VerifyRelay (GMAC
 // over packet[:len-16]), or the status the packet ends with. h: the first 16 bytes (read only when
 // len >= 16). Shared by the host (window.cpp) and the device (rx_wire_kernel) forms.
+__host__ __device__ inline uint32_t neb_rx_len(const neb_rx_packet& p) { return p.len & ~NEB_RX_OWN_SOURCE; }
 __host__ __device__ inline int32_t neb_rx_wire_gate(const uint8_t* h, const neb_rx_packet& p, neb_desc* d) {
-    if (p.len < 16u) return NEB_STATUS_INVALID;  // h.Parse: ErrHeaderTooShort (header.go:144-146)
+    const uint32_t len = neb_rx_len(p);
+    if (len < 16u) return NEB_STATUS_INVALID;  // h.Parse: ErrHeaderTooShort (header.go:144-146)
     const uint32_t ver = h[0] >> 4, type = h[0] & 15u, sub = h[1];
     if (ver != 1u) return NEB_STATUS_INVALID;  // header.Version (outside.go:49-55)
     // IsValidSubType (header.go:192-205): Message 0/1, Handshake 0 (IXPSK0), Test 0/1, RecvError,
     // LightHouse, CloseTunnel, Control 0
     const bool valid = (type == 1u || type == 4u) ? sub <= 1u : (type == 0u || (type >= 2u && type <= 6u)) && sub == 0u;
     if (!valid) return NEB_STATUS_INVALID;
+    // the caller's double-encryption check (outside.go:66-74: not relayed, UDP source inside the
+    // node's own VPN networks), which needs the source address the batch does not carry
+    if (p.len & NEB_RX_OWN_SOURCE) return NEB_STATUS_INVALID;
     if (type == 0u || type == 2u) return NEB_STATUS_NOT_MESSAGE;  // handshake, recv error (outside.go:83-89)
     if (p.key_id == NEB_KEYS_MIXED) return NEB_STATUS_BAD_KEY;    // no hostinfo (outside.go:100-106)
-    if (p.len < 32u) return NEB_STATUS_INVALID;                   // header.Len + Overhead (outside.go:108-114)
+    if (len < 32u) return NEB_STATUS_INVALID;                     // header.Len + Overhead (outside.go:108-114)
     uint64_t c = 0;
     for (int i = 8; i < 16; i++) c = c << 8 | h[i];
     d->counter = c;
@@ -150,13 +155,13 @@ __host__ __device__ inline int32_t neb_rx_wire_gate(const uint8_t* h, const neb_
     d->flags = 0;
     d->aad_off = p.off;
     if (type == 1u && sub == 1u) {  // VerifyRelay: AD = everything but the trailing tag
-        d->aad_len = p.len - 16u;
-        d->src_off = d->dst_off = p.off + p.len - 16u;
+        d->aad_len = len - 16u;
+        d->src_off = d->dst_off = p.off + len - 16u;
         d->len = 0;
     } else {  // Decrypt: in place after the header
         d->aad_len = 16u;
         d->src_off = d->dst_off = p.off + 16u;
-        d->len = p.len - 32u;
+        d->len = len - 32u;
     }
     return NEB_STATUS_OK;
 }

@@ -111,7 +111,27 @@ __global__ void sched_scatter_kernel(uint32_t n, const uint32_t* dn, SchedWs ws)
         ws.sorted[ws.base[ws.binof[i]] + ws.binpos[i]] = i;
 }
 
+// Descriptors of a shard whose engine disagrees with engine 0 on some key slots (engine.cpp
+// KeyFence): copied with those packets' key_id pointing past every key table, so the batch kernels
+// give them NEB_STATUS_BAD_KEY instead of sealing with another tunnel's key.
+__global__ void fence_keys_kernel(const neb_desc* __restrict__ in, neb_desc* __restrict__ out, uint32_t n,
+                                  const uint8_t* __restrict__ bad, uint32_t nbad) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        neb_desc d = in[i];
+        if (d.key_id < nbad && bad[d.key_id]) d.key_id = NEB_KEYS_MIXED - 1u;
+        out[i] = d;
+    }
+}
+
 }  // namespace neb
+
+extern "C" hipError_t neb_fence_keys(const neb_desc* in, neb_desc* out, uint32_t n, const uint8_t* bad, uint32_t nbad,
+                                     hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (n + 255u) / 256u < 1024u ? (n + 255u) / 256u : 1024u;
+    hipLaunchKernelGGL(neb::fence_keys_kernel, dim3(g), dim3(256), 0, s, in, out, n, bad, nbad);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
                                       uint32_t lpp, const neb::SchedWs* ws, hipStream_t s) {

@@ -36,6 +36,7 @@
 #include "../../include/nebula_aead.h"
 #include "host_common.hpp"
 #include "rxwin.hpp"
+#include "hip_guard.hpp"
 #include "window_core.hpp"
 
 // engine.cpp
@@ -123,6 +124,7 @@ NEB_API int neb_rx_open_batch_host(neb_engine* e, int alg, neb_window* const* wi
                                    int32_t* status, uint32_t key_hint) {
     if (!e || (n && (!desc || !arena || !status || !windows))) return NEB_ERR_INVALID;
     if (n == 0) return NEB_OK;
+    DeviceGuard dg;
     static const bool prof = std::getenv("NEB_RX_PROF") != nullptr;  // phase times to stderr
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -420,7 +422,7 @@ NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, 
     if (!e || !out || count == 0 || length == 0 || (length & (length - 1)) || length > (1ull << 24))
         return NEB_ERR_INVALID;
     *out = nullptr;
-    hipSetDevice(neb_engine_device_of(e));
+    DeviceGuard dg(neb_engine_device_of(e));
     neb_dwindows* d = new (std::nothrow) neb_dwindows;
     if (!d) return NEB_ERR_INVALID;
     d->e = e;
@@ -462,7 +464,7 @@ NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, 
 
 NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
     if (!d) return NEB_ERR_INVALID;
-    hipSetDevice(neb_engine_device_of(d->e));
+    DeviceGuard dg(neb_engine_device_of(d->e));
     {
         // neb_rx_open_batch returns only once its stream has run the batch, and holds d->mu
         // throughout: with the lock taken, nothing of this window set is in flight
@@ -479,7 +481,7 @@ NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
 NEB_API int neb_dwindows_load(neb_dwindows* d, uint32_t idx, const neb_window* w) {
     if (!d || idx >= d->win.count) return NEB_ERR_INVALID;
     std::lock_guard<std::mutex> g(d->mu);
-    hipSetDevice(neb_engine_device_of(d->e));
+    DeviceGuard dg(neb_engine_device_of(d->e));
     if (!w) {
         const uint32_t zero = 0;
         RX_HIP(hipMemcpy(d->win.present + idx, &zero, 4, hipMemcpyHostToDevice));
@@ -498,7 +500,7 @@ NEB_API int neb_dwindows_load(neb_dwindows* d, uint32_t idx, const neb_window* w
 NEB_API int neb_dwindows_store(neb_dwindows* d, uint32_t idx, neb_window* w) {
     if (!d || !w || idx >= d->win.count) return NEB_ERR_INVALID;
     std::lock_guard<std::mutex> g(d->mu);
-    hipSetDevice(neb_engine_device_of(d->e));
+    DeviceGuard dg(neb_engine_device_of(d->e));
     uint32_t present = 0;
     RX_HIP(hipMemcpy(&present, d->win.present + idx, 4, hipMemcpyDeviceToHost));
     if (!present) return NEB_ERR_INVALID;
@@ -717,6 +719,7 @@ NEB_API int neb_rx_open_batch(neb_engine* e, int alg, neb_dwindows* d, const neb
     int rc = neb_check_batch_args(e, alg, key_hint);
     if (rc != NEB_OK) return rc;
     if (n == 0) return NEB_OK;
+    DeviceGuard dg;
     std::lock_guard<std::mutex> g(d->mu);
     return rx_open_batch_locked(e, alg, d, d_desc, n, d_arena, d_status, key_hint, stream);
 }
@@ -730,7 +733,7 @@ NEB_API int neb_rx_open_wire_batch_host(neb_engine* e, int alg, neb_window* cons
     if (!e || (n && (!pk || !arena || !status || !windows))) return NEB_ERR_INVALID;
     if (n == 0) return NEB_OK;
     for (uint32_t i = 0; i < n; i++)  // every wire packet inside the arena (sums cannot wrap)
-        if (pk[i].off > arena_len || pk[i].len > arena_len - pk[i].off) return NEB_ERR_INVALID;
+        if (pk[i].off > arena_len || neb_rx_len(pk[i]) > arena_len - pk[i].off) return NEB_ERR_INVALID;
     std::vector<neb_desc> desc(n);
     std::vector<int32_t> gate(n);
     for (uint32_t i = 0; i < n; i++) {
@@ -753,7 +756,7 @@ NEB_API int neb_rx_open_wire_batch(neb_engine* e, int alg, neb_dwindows* d, cons
     if (rc != NEB_OK) return rc;
     if (n == 0) return NEB_OK;
     std::lock_guard<std::mutex> g(d->mu);
-    hipSetDevice(neb_engine_device_of(e));
+    DeviceGuard dg(neb_engine_device_of(e));
     hipStream_t s = (hipStream_t)stream;
     if (n > d->wire_n) {
         RX_HIP(hipStreamSynchronize(s));

@@ -109,6 +109,11 @@ class Engine:
         self.max_keys = max_keys
         self.live = {}  # id -> CipherState: the keys installed and not yet destroyed
 
+    def stats(self) -> dict:
+        v = (C.c_uint64 * 4)()
+        L.check(L.lib().neb_engine_stats(self.handle, v), "neb_engine_stats")
+        return {"pkt_slots": v[0], "pkt_calls": v[1], "pkt_waits": v[2], "installs": v[3]}
+
     def close(self) -> None:
         if self.handle:
             L.lib().neb_engine_destroy(self.handle)
@@ -145,6 +150,34 @@ class CipherFunc:
         cs = cls(h, engine)
         engine.live[id(cs)] = cs
         return cs
+
+
+    def _wrap(self, h, engine: Engine) -> "CipherState":
+        cls = CipherStateAESGCM if self.alg == L.ALG_AESGCM else CipherStateChaChaPoly
+        cs = cls(C.c_void_p(h), engine)
+        engine.live[id(cs)] = cs
+        return cs
+
+    def CipherBatch(self, engine: Engine, keys) -> "list[CipherState]":
+        """Cipher(k) for many keys in one device launch (neb_cipher_create_batch): the tunnels a
+        lighthouse or a rekey storm completes together (handshake_manager.go:752,877)."""
+        keys = [bytes(k) for k in keys]
+        assert all(len(k) == 32 for k in keys)
+        if not keys:
+            return []
+        out = (C.c_void_p * len(keys))()
+        L.check(L.lib().neb_cipher_create_batch(engine.handle, self.alg, b"".join(keys), len(keys), out),
+                "neb_cipher_create_batch")
+        return [self._wrap(h, engine) for h in out]
+
+    def CipherMulti(self, engines, k: bytes) -> "list[CipherState]":
+        """One tunnel key on every engine of a set, at one key_id (neb_cipher_create_multi): the
+        install the multi-engine batch calls require (connection_state.go:37-49, one eKey/dKey)."""
+        assert len(k) == 32
+        hs = (C.c_void_p * len(engines))(*[e.handle.value for e in engines])
+        out = (C.c_void_p * len(engines))()
+        L.check(L.lib().neb_cipher_create_multi(hs, len(engines), self.alg, bytes(k), out), "neb_cipher_create_multi")
+        return [self._wrap(h, e) for h, e in zip(out, engines)]
 
 
 CipherAESGCM = CipherFunc("AESGCM", L.ALG_AESGCM)

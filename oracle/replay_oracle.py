@@ -138,9 +138,10 @@ def rx_sequential(windows, keys, counters, verdicts):
     return status, decrypted
 
 
-def read_outside_gate(packet: bytes, has_tunnel: bool):
+def read_outside_gate(packet: bytes, has_tunnel: bool, own_source: bool = False):
     """readOutsidePackets (outside.go:30-114) up to the decrypt, restated: h.Parse
-    (header.go:143-156), the version and IsValidSubType checks (header.go:192-205), the unencrypted
+    (header.go:143-156), the version and IsValidSubType checks (header.go:192-205), the caller's
+    double-encryption check (outside.go:66-74, `own_source`), the unencrypted
     types handed elsewhere (outside.go:83-89), the hostinfo lookup (outside.go:94-106) and the size
     check (outside.go:108-114). Returns (status, None) for a packet that stops here, or
     (None, (kind, counter)) with kind "decrypt" (Decrypt, header as AD, in place) or "relay"
@@ -157,6 +158,8 @@ def read_outside_gate(packet: bytes, has_tunnel: bool):
     else:
         valid = False
     if not valid:
+        return INVALID, None
+    if own_source:  # outside.go:66-74: not relayed, UDP source inside the node's own VPN networks
         return INVALID, None
     if typ in (0, 2):
         return NOT_MESSAGE, None

@@ -148,8 +148,8 @@ def test_append_semantics(engine, cf):
 
 def test_concurrent_encrypt_decrypt_danger(engine, oracle_mod):
     """EncryptDanger / DecryptDanger from 16 threads at once on shared CipherStates (Nebula calls
-    them from every routine, lock-free: noiseutil/notboring.go:12): each thread has its own slot
-    and stream in the engine, and every output equals the oracle's."""
+    them from every routine, lock-free: noiseutil/notboring.go:12): 16 threads over the engine's
+    fixed pool of 4 slots, and every output equals the oracle's."""
     import threading
 
     from nebula_amd import _lib as L
@@ -231,3 +231,129 @@ def test_destroy_does_not_wait_for_another_tunnels_batch(engine, oracle_mod):
     finally:
         for c in ciphers:
             c.destroy()
+
+
+def test_per_packet_pool_bounded_over_many_engines(oracle_mod):
+    """One thread alternating over 10 engines (round 3's 8-entry per-thread cache leaked a stream and
+    a pinned buffer per call here): every engine keeps its fixed pool of 4 slots, and every packet
+    still equals the oracle. Then 48 threads on one engine: still 4 slots, FIFO turns."""
+    import threading
+
+    from nebula_amd import _lib as L
+    from nebula_amd.noiseutil import CipherAESGCM, Engine
+
+    engines = [Engine(0, max_keys=4) for _ in range(10)]
+    try:
+        keys = [bytes([i + 1] * 32) for i in range(10)]
+        cs = [CipherAESGCM.Cipher(e, k) for e, k in zip(engines, keys)]
+        for j in range(5):
+            for i, (c, k) in enumerate(zip(cs, keys)):
+                n = j * 10 + i
+                pt = bytes([j, i]) * 300
+                ct = c.EncryptDanger(None, b"h" * 16, pt, n).bytes()
+                assert ct == oracle_mod.seal(L.ALG_AESGCM, k, oracle_mod.nonce(L.ALG_AESGCM, n), b"h" * 16, pt)
+        for e in engines:
+            st = e.stats()
+            assert st["pkt_slots"] == 4 and st["pkt_calls"] >= 5
+        errors = []
+
+        def worker(t):
+            try:
+                for j in range(20):
+                    pt = bytes([t, j]) * 50
+                    ct = cs[0].EncryptDanger(None, b"", pt, t * 100 + j)
+                    if cs[0].DecryptDanger(None, b"", ct, t * 100 + j).bytes() != pt:
+                        raise AssertionError(f"round trip t={t} j={j}")
+            except Exception as ex:
+                errors.append(ex)
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(48)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errors, errors[:3]
+        st = engines[0].stats()
+        assert st["pkt_slots"] == 4 and st["pkt_calls"] >= 48 * 40
+        for c in cs:
+            c.destroy()
+    finally:
+        for e in engines:
+            e.close()
+
+
+@pytest.mark.parametrize("alg", [1, 2])
+def test_cipher_create_batch_c3_shape(oracle_mod, alg):
+    """4096 tunnel keys installed by one neb_cipher_create_batch (one launch), then a C3-shaped batch
+    (16 packets per key on average) sealed and opened through them, bit-exact against the oracle."""
+    import torch
+
+    from nebula_amd import workload as W
+    from nebula_amd.batch import DeviceBatch, install_keys
+    from nebula_amd.noiseutil import Engine
+
+    b = W.make_batch(alg, 8192, 4096, seed=41, name="batch-install")
+    ref = b.arena.copy()
+    assert (oracle_mod.batch(alg, 0, b.keys, b.desc, ref) == 0).all()
+    with Engine(0, 4096) as eng:
+        cs = install_keys(eng, b)
+        assert len(cs) == 4096 and sorted(c.key_id for c in cs) == list(range(4096))
+        assert eng.stats()["installs"] == 4096
+        db = DeviceBatch(eng, b, cs)
+        db.seal()
+        torch.cuda.synchronize()
+        assert (db.status_host() == 0).all()
+        assert np.array_equal(db.arena_host(), ref)
+        db.open()
+        torch.cuda.synchronize()
+        exp = ref.copy()
+        oracle_mod.batch(alg, 1, b.keys, b.desc, exp)
+        assert (db.status_host() == 0).all() and np.array_equal(db.arena_host(), exp)
+        for c in cs[::2]:
+            c.destroy()
+        # reinstall over freed slots, another algorithm's records cleared on the way
+        other = 3 - alg
+        b2 = W.make_batch(other, 512, 2048, seed=42, name="reinstall")
+        cs2 = install_keys(eng, b2)
+        assert sorted(c.key_id for c in cs2) == list(range(0, 4096, 2))
+        ref2 = b2.arena.copy()
+        assert (oracle_mod.batch(other, 0, b2.keys, b2.desc, ref2) == 0).all()
+        db2 = DeviceBatch(eng, b2, cs2)
+        db2.seal()
+        torch.cuda.synchronize()
+        assert (db2.status_host() == 0).all() and np.array_equal(db2.arena_host(), ref2)
+        for c in cs[1::2] + cs2:
+            c.destroy()
+
+
+def test_entry_points_restore_current_device():
+    """Every entry point restores the caller's current HIP device (hip_guard.hpp). With two or more
+    devices an engine on device 1 is driven while torch's current device is 0."""
+    import torch
+
+    from nebula_amd import _lib as L
+    from nebula_amd import workload as W
+    from nebula_amd.batch import DeviceBatch, host_batch, install_keys, slot_desc
+    from nebula_amd.noiseutil import CipherAESGCM, Engine
+
+    ndev = torch.cuda.device_count()
+    dev = 1 if ndev > 1 else 0
+    torch.cuda.set_device(0)
+    b = W.make_batch(L.ALG_AESGCM, 300, 3, seed=7, name="guard")
+    with Engine(dev, 16) as eng:
+        assert torch.cuda.current_device() == 0
+        cs = install_keys(eng, b)
+        c1 = CipherAESGCM.Cipher(eng, bytes(32))
+        assert torch.cuda.current_device() == 0
+        c1.EncryptDanger(None, b"", b"x" * 40, 1)
+        assert torch.cuda.current_device() == 0
+        host_batch(eng, L.ALG_AESGCM, False, slot_desc(b, cs), b.arena.copy())
+        assert torch.cuda.current_device() == 0
+        db = DeviceBatch(eng, b, cs, device=dev)
+        db.seal(stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        assert torch.cuda.current_device() == 0
+        for c in cs + [c1]:
+            c.destroy()
+        assert torch.cuda.current_device() == 0
+    assert torch.cuda.current_device() == 0

@@ -587,16 +587,16 @@ def _wire_batch(oracle_mod, alg, keys, seed=3, n_rand=600):
     return arena, packets
 
 
-def _wire_expected(oracle_mod, R, alg, keys, arena, packets, window_len):
+def _wire_expected(oracle_mod, R, alg, keys, arena, packets, window_len, own=frozenset()):
     wins = {t: R.Bits(window_len) for t in range(len(keys))}
     for w in wins.values():
         w.update(1)
         w.update(2)
     exp = arena.copy()
     status = []
-    for off, ln, t in packets:
+    for i, (off, ln, t) in enumerate(packets):
         pkt = bytes(arena[off:off + ln])
-        st, go = R.read_outside_gate(pkt, t is not None)
+        st, go = R.read_outside_gate(pkt, t is not None, i in own)
         if st is not None:
             status.append(st)
             continue
@@ -634,13 +634,15 @@ def test_rx_wire_gate_matches_read_outside_packets(engine, oracle_mod, alg, devi
     rng = random.Random(alg * 5 + device)
     keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(3)]
     arena, packets = _wire_batch(oracle_mod, alg, keys, seed=alg + 2 * device)
-    exp_status, exp_arena, owins = _wire_expected(oracle_mod, R, alg, keys, arena, packets, 256)
+    # the caller's double-encryption check (outside.go:66-74) refuses every 17th datagram
+    own = frozenset(range(3, len(packets), 17))
+    exp_status, exp_arena, owins = _wire_expected(oracle_mod, R, alg, keys, arena, packets, 256, own)
     cf = CipherAESGCM if alg == L.ALG_AESGCM else CipherChaChaPoly
     ciphers = [cf.Cipher(engine, k) for k in keys]
     try:
         pk = np.zeros(len(packets), L.RX_PACKET_DTYPE)
         for i, (off, ln, t) in enumerate(packets):
-            pk[i] = (off, ln, ciphers[t].key_id if t is not None else L.KEYS_MIXED)
+            pk[i] = (off, ln | (0x80000000 if i in own else 0), ciphers[t].key_id if t is not None else L.KEYS_MIXED)
         ewins = []
         for c in ciphers:
             w = Bits(256)
