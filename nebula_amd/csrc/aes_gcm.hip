@@ -1322,6 +1322,288 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     }
 }
 
+// ---- mixed keys, in two passes (round 4): the CTR pass and the GHASH pass ----------------------
+//
+// The fused chunk kernel above needs one key per wave for both halves of GCM, so a wave's lanes
+// idle whenever a key's packets do not fill its groups (C3: ≈ 16 packets per key, 87% of the
+// lane-rounds busy) and the per-wave GHASH tables leave room for the two-table AES only. But only
+// GHASH needs per-key tables: the AES-CTR half needs a key's round keys, which fit in each lane's
+// registers. So a mixed-key batch runs as
+//  * gcm_ctr_kernel: keystream, payload XOR and E_K(J0) of every packet, 16 packets of the
+//    scheduler's order per group at 4 lanes each, each lane with its own packet's round keys in
+//    VGPRs — groups need not be single-key, so they are full (C3 and C5: all but the last), and
+//    the four-table AES fills the LDS (128 KiB, nothing per wave) as in the single-key kernel;
+//  * gcm_ghash_kernel: GHASH over AAD || CT || lengths per single-key chunk of the scheduler (the
+//    fused kernel's chunk shapes and per-wave tables), with no AES and no T-tables — a quarter of
+//    the LDS work, so its partly filled groups cost a quarter as much.
+// seal: CTR (ciphertext into dst, E_K(J0) into the tag slot), then GHASH (tag = E_K(J0) ^ S there,
+//       statuses);
+// open: GHASH (S into the scheduler's per-packet sums), then CTR (plaintext into dst, the tag
+//       checked against E_K(J0) ^ S, the payload zeroed on a mismatch, statuses).
+
+struct RkLane {  // per-lane round keys (VGPRs): the lanes of a CTR group hold their own packets' keys
+    uint32_t k[60];
+    static constexpr bool kUniform = false;
+    __device__ __forceinline__ uint4 get(int r) const {
+        return make_uint4(k[4 * r], k[4 * r + 1], k[4 * r + 2], k[4 * r + 3]);
+    }
+};
+
+// One CTR group: packet p on lanes 4·(lane/4) .. +3. A packet's AES blocks are its m ciphertext
+// blocks (counters 2 .. m+1) and J0 (counter 1): block j = 4r + l in round r on lane l, J0 last.
+template <bool OPEN, class TL>
+__device__ __forceinline__ void gcm_ctr_group(const GcmArgs& args, uint32_t p, bool valid, const TL& T,
+                                              uint32_t lane, const uint4* sums) {
+    const uint32_t l = lane & 3u;
+    neb_desc d = {};
+    if (valid) d = args.desc[p];
+    const bool key_in = d.key_id < args.max_keys;
+    const uint32_t* rec = args.keys + (size_t)(key_in ? d.key_id : 0u) * kKeyRecDwords;
+    uint32_t st = NEB_STATUS_OK;
+    if (!key_in || rec[kRecAlg] != NEB_ALG_AESGCM) st = NEB_STATUS_BAD_KEY;
+    if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
+    const bool run = valid && st == NEB_STATUS_OK;
+    RkLane rk;
+#pragma unroll
+    for (int i = 0; i < 15; i++) {
+        const uint4 v = run ? ld_rec4(rec, kRecRoundKeys + 4u * i) : make_uint4(0, 0, 0, 0);
+        rk.k[4 * i] = v.x;
+        rk.k[4 * i + 1] = v.y;
+        rk.k[4 * i + 2] = v.z;
+        rk.k[4 * i + 3] = v.w;
+    }
+    const uint32_t hdr = args.hdr_from_dst ? d.flags & kCsHdrMask : 0u;
+    const uint32_t m = (d.len + 15u) >> 4;
+    const uint32_t R = run ? (m + 4u) >> 2 : 0u;  // m + 1 blocks over 4 lanes
+    const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32)), c2 = bswap32((uint32_t)d.counter);
+    uint4 ej0 = make_uint4(0, 0, 0, 0);
+    auto rounds = [&](auto cm) {
+        constexpr int CM = decltype(cm)::value;
+        CtrConst cc{};
+        if constexpr (CM == 2) cc = aes_ctr_prep8(c1, c2, T, rk);
+        else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
+        for (uint32_t r = 0; __any(r < R); r++) {
+            if (r < R) {
+                const uint32_t j = 4u * r + l, off = 16u * j;
+                const bool is_ct = j < m, is_j0 = j == m;
+                // a common round: every active lane a full ciphertext block at a 16-B aligned
+                // destination (source: dword-aligned or shifted, as in gcm_packet_group)
+                const bool fast = __all(is_ct && off + 16u <= d.len && off >= hdr &&
+                                        ((d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u);
+                uint4 pre = make_uint4(0, 0, 0, 0);
+                if (fast) {
+                    const uint8_t* sp = args.arena + d.src_off + off;
+                    pre = __all(((uint32_t)(uintptr_t)sp & 3u) == 0u) ? load_u4_a4(sp) : load_shifted16(sp);
+                }
+                LaneBlock b;
+                b.ctr = is_ct ? j + 2u : 1u;
+                const uint4 ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
+                if (fast) {
+                    *reinterpret_cast<uint4*>(args.arena + d.dst_off + off) = xor4(pre, ks);
+                } else if (is_ct) {
+                    const uint32_t nb = min(16u, d.len - off);
+                    const uint4 in = off < hdr ? load_block_hdr(args.arena + d.dst_off + off, args.arena + d.src_off + off,
+                                                                nb, hdr - off)
+                                               : load_block(args.arena + d.src_off + off, nb);
+                    store_block(args.arena + d.dst_off + off, xor4(in, mask_block(ks, nb)), nb);
+                }
+                if (is_j0) ej0 = ks;
+            }
+        }
+    };
+    if (__all(m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
+    else if (__all(m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
+    else rounds(std::integral_constant<int, 0>{});
+    const uint32_t jl = m & 3u;  // the lane that computed E_K(J0)
+    if constexpr (!OPEN) {
+        // the GHASH pass turns it into the tag (E_K(J0) ^ S) and writes the status
+        if (run && l == jl) store_block(args.arena + d.dst_off + d.len, ej0, 16);
+    } else {
+        uint32_t fail = 0;
+        if (run && l == jl) {
+            const uint4 tag = xor4(ej0, bswap4(sums[p]));
+            const uint4 df = xor4(load_block(args.arena + d.src_off + d.len, 16), tag);
+            fail = (df.x | df.y | df.z | df.w) != 0u;
+        }
+        fail = (uint32_t)__shfl((int)fail, (int)((lane & ~3u) | jl));
+        if (run && fail)
+            for (uint32_t off = 16u * l; off < d.len; off += 64u)
+                store_block(args.arena + d.dst_off + off, make_uint4(0, 0, 0, 0), min(16u, d.len - off));
+        if (valid && l == jl) args.status[p] = run ? (fail ? NEB_STATUS_AUTH_FAILED : NEB_STATUS_OK) : (int32_t)st;
+    }
+}
+
+constexpr int kCtrWaves = 16;
+constexpr int kCtrThreads = kCtrWaves * kWave;
+struct CtrLds {
+    uint2 ttab[2 * 256 * 32];  // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each (TLook4)
+};
+
+// Groups of 16 consecutive packets of the scheduler's order (sorted: bins by size class, then key,
+// so a group's packets are alike in size); group g on workgroup g mod G, as in gcm_single_kernel.
+template <bool OPEN>
+__global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, const uint32_t* __restrict__ sorted,
+                                                                 const uint4* __restrict__ sums) {
+    __shared__ CtrLds lds;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint32_t npkt = args.npkt;
+    if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
+    const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
+    if (blockIdx.x >= ngroups) return;  // uniform over the workgroup
+    fill_ttab<2u * 256u * 32u, kCtrThreads>(lds.ttab, tid, ttab4_entry);
+    __syncthreads();
+    const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
+    const uint32_t slots = gridDim.x * kCtrWaves;
+    for (uint32_t grp = blockIdx.x + wave * gridDim.x; grp < ngroups; grp += slots) {
+        const uint32_t q = grp * kPpw + (lane >> 2);
+        const bool valid = q < npkt;
+        const uint32_t p = valid ? sorted[q] : 0u;
+        gcm_ctr_group<OPEN>(args, p, valid, T, lane, sums);
+    }
+}
+
+// The GHASH half of a packet group of the mixed-key split (lanes and padding as gcm_packet_group:
+// lane l owns padded blocks 2^lg·r + l + 1 of AAD || CT || lengths), reading the ciphertext (seal:
+// written by the CTR pass at dst; open: at src). Each round's block is loaded a round ahead.
+template <bool OPEN, class GH>
+__device__ __forceinline__ void ghash_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
+                                                   bool key_ok, const GH& gh, uint32_t lane, uint32_t lg,
+                                                   uint4* sums) {
+    const uint32_t LPP = 1u << lg;
+    const uint32_t l = lane & (LPP - 1u);
+    neb_desc d = {};
+    if (valid) d = args.desc[p];
+    uint32_t st = NEB_STATUS_OK;
+    if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
+    if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
+    const bool run = valid && st == NEB_STATUS_OK;
+    PktShape sh;
+    sh.na = (d.aad_len + 15u) >> 4;
+    sh.m = (d.len + 15u) >> 4;
+    sh.n = sh.na + sh.m + 1u;
+    sh.R = run ? (sh.n + LPP - 1u) >> lg : 0u;
+    sh.pad = (sh.R << lg) - sh.n;
+    const uint8_t* ct = args.arena + (OPEN ? d.src_off : d.dst_off);
+    auto load = [&](uint32_t r) -> uint4 {  // round r's GHASH input block (big-endian words)
+        uint4 X = make_uint4(0, 0, 0, 0);
+        if (r >= sh.R) return X;
+        const LaneBlock b = lane_block(sh, r, l, lg);
+        if (b.is_ct) {
+            const uint32_t off = 16u * (b.k - 1u);
+            const uint8_t* q = ct + off;
+            X = off + 16u <= d.len && ((uint32_t)(uintptr_t)q & 3u) == 0u ? load_u4_a4(q) : load_block(q, min(16u, d.len - off));
+        } else if (b.is_aad) {
+            const uint32_t off = 16u * (uint32_t)(b.g - 1);
+            X = load_block(args.arena + d.aad_off + off, min(16u, d.aad_len - off));
+        }
+        X = bswap4(X);
+        if (b.is_len) {
+            const uint64_t abits = (uint64_t)d.aad_len * 8u, cbits = (uint64_t)d.len * 8u;
+            X = make_uint4((uint32_t)(abits >> 32), (uint32_t)abits, (uint32_t)(cbits >> 32), (uint32_t)cbits);
+        }
+        return X;
+    };
+    uint4 A = make_uint4(0, 0, 0, 0);
+    uint4 X = load(0);
+    for (uint32_t r = 0; __any(r < sh.R); r++) {
+        const uint4 Xn = load(r + 1u);
+        if (r < sh.R) A = r == 0u ? X : xor4(gh.horner(A, lg), X);
+        X = Xn;
+    }
+    const uint4 V = gh.final(A, lane, lg);  // every lane: the final shuffles across lanes
+    if (l == LPP - 1u) {
+        if constexpr (!OPEN) {
+            if (run) {
+                uint8_t* tp = args.arena + d.dst_off + d.len;
+                store_block(tp, xor4(load_block(tp, 16), bswap4(V)), 16);  // E_K(J0) ^ S
+            }
+            if (valid) args.status[p] = (int32_t)st;
+        } else {
+            if (run) sums[p] = V;
+        }
+    }
+}
+
+constexpr int kGhWaves = 8;
+constexpr int kGhThreads = kGhWaves * kWave;
+#ifndef NEB_GH_WPE
+#define NEB_GH_WPE 4  // launch bound: waves per SIMD (2 workgroups of 8 waves per CU; 5 spills)
+#endif
+struct GhLds {
+    uint4 shoup[kGhWaves][4][16];  // per wave: M_1..M_4 (full chunks), M_1, M_2, M_4, M_8 (tails)
+    uint4 pos[kGhWaves][8 * 16];   // per wave: position tables of H^(2^lg)
+};
+
+// The scheduler's chunks (sched.hpp), owned and drawn as in gcm_chunk_kernel (workgroup w: chunks
+// w, w + G, ..., its waves through an LDS cursor one chunk ahead).
+template <bool OPEN>
+__global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmArgs args, ChunkArgs ca, uint4* sums) {
+    __shared__ GhLds lds;
+    __shared__ uint32_t wg_cursor;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
+    const uint32_t nlong = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
+    const uint32_t nback = nlong + min(__builtin_amdgcn_readfirstlane(ca.counters[kCntShortChunks]), ca.max_short);
+    const uint32_t nch = nfront + nback;
+    if (blockIdx.x >= nch) return;
+    if (tid == 0) wg_cursor = kGhWaves;
+    __syncthreads();
+    uint4* wtab = &lds.shoup[wave][0][0];
+    uint4* wpos = &lds.pos[wave][0];
+    auto chunk_at = [&](uint32_t c) {
+        return ca.chunks[c < nfront ? c : c < nfront + nlong ? ca.max_chunks - 1u - (c - nfront) : ca.max_chunks + (c - nfront - nlong)];
+    };
+    auto chunk_of = [&](uint32_t k) -> uint32_t { return blockIdx.x + k * gridDim.x; };
+    uint32_t c = 0;
+    if (lane == 0u) c = chunk_of(wave);
+    c = __builtin_amdgcn_readfirstlane(c);
+    uint4 ch_next = make_uint4(0, 0, 0, 0);
+    if (c < nch) ch_next = chunk_at(c);
+    while (c < nch) {
+        const uint4 ch = ch_next;
+        const bool full = c < nfront;
+        uint32_t cn = 0;
+        if (lane == 0u) cn = chunk_of(atomicAdd(&wg_cursor, 1u));
+        cn = __builtin_amdgcn_readfirstlane(cn);
+        if (cn < nch) ch_next = chunk_at(cn);
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
+        const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
+        const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
+        const uint32_t* rec = args.keys + (size_t)(key < args.max_keys ? key : 0u) * kKeyRecDwords;
+        const bool key_ok = key < args.max_keys && rec[kRecAlg] == NEB_ALG_AESGCM;
+        if (full) {
+            stage_chunk_tables<true>(rec, ln, 2u, wtab, wpos);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const GhChunk4 gh{wtab, wpos};
+            for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
+                const uint32_t q = g0 + (ln >> 2);
+                const bool valid = q < count;
+                const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+                ghash_packet_group<OPEN>(args, p, valid, key, key_ok, gh, ln, 2u, sums);
+            }
+        } else {
+            const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
+            stage_chunk_tables<false>(rec, ln, lg, wtab, wpos);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t q = ln >> lg;
+            const bool valid = q < count;
+            const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+            const GhChunkTree gh{wtab, wpos};
+            ghash_packet_group<OPEN>(args, p, valid, key, key_ok, gh, ln, lg, sums);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        c = cn;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Key install: AES-256 key expansion, H = E_K(0), H^1..H^16, and the GHASH tables.
 // Runs once per tunnel key (one workgroup of 256 lanes).
@@ -1657,4 +1939,34 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
     const uint32_t bound = max_chunks * (uint32_t)neb::kChunkWaves;
     return open ? launch_grid(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, a, ca)
                 : launch_grid(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, a, ca);
+}
+
+// Mixed keys in two passes (gcm_ctr_kernel + gcm_ghash_kernel): seal CTR then GHASH, open GHASH then
+// CTR. d_sums: 16 B per packet (the open's GHASH values between the passes).
+template <bool OPEN>
+static hipError_t launch_split(const neb::GcmArgs& a, const neb::ChunkArgs& ca, uint32_t max_chunks, uint4* d_sums,
+                               int cu_count, hipStream_t s) {
+    const uint32_t groups = (a.npkt + neb::kPpw - 1u) / neb::kPpw;
+    auto ctr = [&]() {
+        return launch_grid(neb::gcm_ctr_kernel<OPEN>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves, cu_count, s,
+                           a, ca.sorted, (const uint4*)d_sums);
+    };
+    auto gh = [&]() {
+        return launch_grid(neb::gcm_ghash_kernel<OPEN>, neb::kGhThreads, max_chunks * (uint32_t)neb::kGhWaves, cu_count,
+                           s, a, ca, d_sums);
+    };
+    hipError_t e = OPEN ? gh() : ctr();
+    if (e != hipSuccess) return e;
+    return OPEN ? ctr() : gh();
+}
+
+extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
+                                          uint8_t* d_arena, const uint32_t* d_keys, uint32_t max_keys,
+                                          int32_t* d_status, const uint32_t* d_sorted, const uint4* d_chunks,
+                                          uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
+                                          uint4* d_sums, int cu_count, hipStream_t s, int hdr_from_dst) {
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
+    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks, max_short};
+    return open ? launch_split<true>(a, ca, max_chunks, d_sums, cu_count, s)
+                : launch_split<false>(a, ca, max_chunks, d_sums, cu_count, s);
 }

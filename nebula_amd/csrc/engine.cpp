@@ -39,6 +39,11 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst);
+extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
+                                          uint8_t* d_arena, const uint32_t* d_keys, uint32_t max_keys,
+                                          int32_t* d_status, const uint32_t* d_sorted, const uint4* d_chunks,
+                                          uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
+                                          uint4* d_sums, int cu_count, hipStream_t s, int hdr_from_dst);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int hdr_from_dst);
 #ifndef NEB_TX_CSUM_SEAL
@@ -693,8 +698,9 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys), ms = neb::sched_max_short(cap, e->max_keys);
     const size_t b_counters = align_up((neb::kSchedCounters + (size_t)neb::kSubBins * nb) * 4u, 256);
     const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
-    const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = ((size_t)mc + ms) * 16u;
-    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks;
+    const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up(((size_t)mc + ms) * 16u, 256);
+    const size_t b_sums = (size_t)cap * 16u;
+    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_sums;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
     if (sp.mem) hipFree(sp.mem);
@@ -715,6 +721,8 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     sp.ws.sorted = (uint32_t*)m;
     m += b_idx;
     sp.ws.chunks = (uint4*)m;
+    m += b_chunks;
+    sp.ws.sums = (uint4*)m;
     sp.ws.max_chunks = mc;
     sp.ws.max_short = ms;
     sp.bytes = bytes;
@@ -723,6 +731,13 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     if (err != hipSuccess) return err;
     sp.dirty = false;
     return hipSuccess;
+}
+
+// Mixed-key AES-GCM: the CTR + GHASH passes (aes_gcm.hip gcm_ctr_kernel / gcm_ghash_kernel), or with
+// NEB_MIXED_FUSED=1 (read per batch) round 3's fused chunk kernel, kept for A/B comparison.
+static bool mixed_split() {
+    const char* v = std::getenv("NEB_MIXED_FUSED");
+    return !(v && v[0] == '1');
 }
 
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
@@ -741,10 +756,16 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         hipError_t err = sched_reserve(e, sp, n, s);
         if (err == hipSuccess && sp.last != s) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
-        if (err == hipSuccess)
-            err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, e->cu_count, s,
-                                        hdr_from_dst);
+        if (err == hipSuccess) {
+            if (mixed_split())
+                err = neb_gcm_batch_split(open, d_desc, n, d_n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
+                                          sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, sp.ws.sums,
+                                          e->cu_count, s, hdr_from_dst);
+            else
+                err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
+                                            sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
+                                            e->cu_count, s, hdr_from_dst);
+        }
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
         if (err == hipSuccess) sp.last = s;
         if (err != hipSuccess) {
