@@ -408,6 +408,11 @@ NEB_API int neb_queue_submit(neb_queue* q, const neb_desc* desc, uint32_t n, uin
 NEB_API int neb_queue_flush(neb_queue* q);
 /* stats[0..3]: device batches launched, packets, submissions, staged bytes (since creation). */
 NEB_API int neb_queue_stats(neb_queue* q, uint64_t stats[4]);
+/* Where a submission's time goes, in nanoseconds summed since creation: per device batch ns[0] fill
+ * (first submission -> sealed), ns[1] drain (sealed -> launched: the last copy-ins), ns[2] device
+ * (launched -> done: launch, kernel, completion); per submission ns[3] copy-in, ns[4] wait (copy-in
+ * done -> its batch done), ns[5] copy-out. Divide by neb_queue_stats' batches / submissions. */
+NEB_API int neb_queue_phases(neb_queue* q, uint64_t ns[6]);
 
 /* ---- header (the AAD) --------------------------------------------------------------------- */
 

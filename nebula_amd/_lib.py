@@ -109,6 +109,7 @@ SIGNATURES = {
     "neb_queue_submit": (_i, [_vp, _vp, _u32, _vp, _sz, _vp]),
     "neb_queue_flush": (_i, [_vp]),
     "neb_queue_stats": (_i, [_vp, _vp]),
+    "neb_queue_phases": (_i, [_vp, _vp]),
 }
 
 

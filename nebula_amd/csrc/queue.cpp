@@ -111,6 +111,12 @@ NEB_API int neb_queue_stats(neb_queue* q, uint64_t stats[4]) {
     return NEB_OK;
 }
 
+NEB_API int neb_queue_phases(neb_queue* q, uint64_t ns[6]) {
+    if (!q || !ns) return NEB_ERR_INVALID;
+    q->phases(ns);
+    return NEB_OK;
+}
+
 NEB_API int neb_queue_submit(neb_queue* q, const neb_desc* desc, uint32_t n, uint8_t* arena, size_t arena_len,
                              int32_t* status) {
     return q ? q->submit(desc, n, arena, arena_len, status) : NEB_ERR_INVALID;

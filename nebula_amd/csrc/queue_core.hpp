@@ -51,7 +51,7 @@ struct QBatch {
     size_t used = 0;
     uint32_t key0 = NEB_KEYS_MIXED;  // the one key every packet uses so far, or NEB_KEYS_MIXED
     bool one_key = true;
-    Clock::time_point first{};
+    Clock::time_point first{}, sealed_at{}, launched_at{};
     int rc = NEB_OK;
 };
 
@@ -98,12 +98,21 @@ struct Queue {
     bool flush_req = false, quit = false;
     std::thread flusher, completer;
     uint64_t n_batches = 0, n_packets = 0, n_subs = 0, n_bytes = 0, n_zc = 0;
+    // phase times (ns, summed; neb_queue_phases): per batch fill (first submission -> sealed),
+    // drain (sealed -> launched: the last writers' copy-in and the flusher's wake-up) and device
+    // (launched -> done: the launch and the kernel); per submission copy-in, wait (copy-in done ->
+    // its batch done) and copy-out
+    uint64_t ns_fill = 0, ns_drain = 0, ns_device = 0, ns_copy_in = 0, ns_wait = 0, ns_copy_out = 0;
+    static uint64_t ns_between(Clock::time_point a, Clock::time_point b) {
+        return b > a ? (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count() : 0u;
+    }
 
     // seal the filling batch and move `cur` to the next one (caller holds mu)
     void seal_current() {
         Batch& x = b[cur];
         if (x.state != BState::kFilling) return;
         x.state = BState::kSealed;
+        x.sealed_at = Clock::now();
         cur = (cur + 1) % (uint32_t)b.size();
         fcv.notify_all();
     }
@@ -136,10 +145,14 @@ struct Queue {
             // one tunnel's packets run the single-key kernel, if that key is installed for this
             // algorithm (otherwise the mixed path reports NEB_STATUS_BAD_KEY per packet)
             if (hint != NEB_KEYS_MIXED && !dev.key_ok(hint)) hint = NEB_KEYS_MIXED;
+            const Clock::time_point tl = Clock::now();
             const int rc = dev.launch(next_launch, x.desc, n, x.arena, x.status, hint, x.tok);
             lk.lock();
             x.rc = rc;
             x.state = BState::kLaunched;
+            x.launched_at = tl;
+            ns_fill += ns_between(x.first, x.sealed_at);
+            ns_drain += ns_between(x.sealed_at, tl);
             n_batches++;
             n_packets += n;
             next_launch = (next_launch + 1) % (uint32_t)b.size();
@@ -162,6 +175,7 @@ struct Queue {
             lk.lock();
             if (wrc != NEB_OK && x.rc == NEB_OK) x.rc = wrc;
             x.state = BState::kDone;
+            ns_device += ns_between(x.launched_at, Clock::now());
             cv.notify_all();
             i = (i + 1) % (uint32_t)b.size();
         }
@@ -234,6 +248,7 @@ struct Queue {
             if (c.npk == q->cfg.max_packets) q->seal_current();
         }
         // copy the packets into the staging (outside the lock: submitters copy in parallel)
+        const Clock::time_point t_in = Clock::now();
         size_t off = off0;
         const uint64_t rebase = (uint64_t)(uintptr_t)arena - (uint64_t)(uintptr_t)x->arena;  // wraps
         for (uint32_t i = 0; i < cnt; i++) {
@@ -266,11 +281,13 @@ struct Queue {
             x->desc[pk0 + i] = s;
             x->status[pk0 + i] = -1;
         }
+        const Clock::time_point t_copied = Clock::now();
         {
             std::unique_lock<std::mutex> lk(q->mu);
             if (--x->writers == 0) q->fcv.notify_all();
             q->cv.wait(lk, [x] { return x->state == BState::kDone; });
         }
+        const Clock::time_point t_done = Clock::now();
         const int rc = x->rc;
         if (rc == NEB_OK && zc) {
             for (uint32_t i = 0; i < cnt; i++) status[p0 + i] = x->status[pk0 + i];
@@ -288,6 +305,9 @@ struct Queue {
         }
         {
             std::lock_guard<std::mutex> g(q->mu);
+            q->ns_copy_in += ns_between(t_in, t_copied);
+            q->ns_wait += ns_between(t_copied, t_done);
+            q->ns_copy_out += ns_between(t_done, Clock::now());
             if (--x->readers == 0) {
                 x->state = BState::kFree;
                 q->cv.notify_all();
@@ -311,6 +331,15 @@ struct Queue {
         s[1] = n_packets;
         s[2] = n_subs;
         s[3] = n_bytes;
+    }
+    void phases(uint64_t ns[6]) {
+        std::lock_guard<std::mutex> g(mu);
+        ns[0] = ns_fill;
+        ns[1] = ns_drain;
+        ns[2] = ns_device;
+        ns[3] = ns_copy_in;
+        ns[4] = ns_wait;
+        ns[5] = ns_copy_out;
     }
     uint64_t zero_copy_submissions() {
         std::lock_guard<std::mutex> g(mu);

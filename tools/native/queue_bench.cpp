@@ -145,15 +145,26 @@ int main(int argc, char** argv) {
             if (zc) neb_host_free(arena_p);
         });
     std::this_thread::sleep_for(std::chrono::milliseconds(400));
-    uint64_t s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+    uint64_t s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, o0[4] = {0, 0, 0, 0}, o1[4] = {0, 0, 0, 0};
+    uint64_t ph0[2][6] = {}, ph1[2][6] = {};
     go = true;
     pkts = 0;
-    if (sq) neb_queue_stats(sq, s0);
+    if (sq) {
+        neb_queue_stats(sq, s0);
+        neb_queue_stats(oq, o0);
+        neb_queue_phases(sq, ph0[0]);
+        neb_queue_phases(oq, ph0[1]);
+    }
     const auto t0 = Clock::now();
     std::this_thread::sleep_for(std::chrono::duration<double>(secs));
     const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
     const uint64_t n = pkts.load();
-    if (sq) neb_queue_stats(sq, s1);
+    if (sq) {
+        neb_queue_stats(sq, s1);
+        neb_queue_stats(oq, o1);
+        neb_queue_phases(sq, ph1[0]);
+        neb_queue_phases(oq, ph1[1]);
+    }
     stop = true;
     for (auto& x : th) x.join();
     std::vector<double> all;
@@ -171,6 +182,23 @@ int main(int argc, char** argv) {
                     "\"errors\": %d}\n",
                     zc ? "queue_native_zero_copy" : "queue_native", threads, flush, deadline, maxpk, depth, gibs, n / dt, p50, p99, (s1[0] - s0[0]) / dt,
                     (double)(s1[1] - s0[1]) / std::max<uint64_t>(1, s1[0] - s0[0]), errs.load());
+    if (!percall) {
+        // where the time goes (neb_queue_phases), mean µs: per device batch fill / drain / device, per
+        // submission copy-in / wait / copy-out; seal queue, then open queue
+        const char* nm[2] = {"seal", "open"};
+        for (int k = 0; k < 2; k++) {
+            const uint64_t* a = ph0[k];
+            const uint64_t* b = ph1[k];
+            const double nb = (double)std::max<uint64_t>(1, (k ? o1[0] - o0[0] : s1[0] - s0[0]));
+            const double ns = (double)std::max<uint64_t>(1, (k ? o1[2] - o0[2] : s1[2] - s0[2]));
+            std::printf("{\"bench\": \"queue_phases\", \"queue\": \"%s\", \"threads\": %d, \"zero_copy\": %s, "
+                        "\"batches\": %.0f, \"fill_us\": %.1f, \"drain_us\": %.1f, \"device_us\": %.1f, "
+                        "\"copy_in_us\": %.1f, \"wait_us\": %.1f, \"copy_out_us\": %.1f}\n",
+                        nm[k], threads, zc ? "true" : "false", nb, (b[0] - a[0]) / nb / 1e3, (b[1] - a[1]) / nb / 1e3,
+                        (b[2] - a[2]) / nb / 1e3, (b[3] - a[3]) / ns / 1e3, (b[4] - a[4]) / ns / 1e3,
+                        (b[5] - a[5]) / ns / 1e3);
+        }
+    }
     if (sq) neb_queue_destroy(sq);
     if (oq) neb_queue_destroy(oq);
     for (auto* k : keys) neb_cipher_destroy(k);

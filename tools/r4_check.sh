@@ -12,6 +12,13 @@ for t in 1 4 8 16 32 64; do
   timeout -k 5 60 ./queue_bench percall $t 1.5 >> $OUT/percall.jsonl 2>> $OUT/percall.err || exit $?
 done
 cat $OUT/percall.jsonl
+: > $OUT/queue.jsonl
+for m in queue queuezc; do
+  for t in 16 32 64; do
+    timeout -k 5 60 ./queue_bench $m $t 128 50 8192 1.5 >> $OUT/queue.jsonl 2>> $OUT/queue.err || exit $?
+  done
+done
+cat $OUT/queue.jsonl
 cd $R
 timeout -k 10 120 python tools/key_install_bench.py 4096 --single > $OUT/keys.json 2>&1 || exit $?
 cat $OUT/keys.json
