@@ -473,6 +473,29 @@ __device__ __forceinline__ uint4 gf_mul_pos(uint4 x, const uint4* ptab) {
     return gf_reduce(z);
 }
 
+// z ^= x · P unreduced (the 256-bit product of gf_mul_pos, before gf_reduce): several products
+// share one reduction (the GHASH pass's aggregated rounds).
+__device__ __forceinline__ void gf_acc_pos(uint4 x, const uint4* ptab, uint32_t z[8]) {
+    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t hi = xw[q], lo = xw[q] << 4;
+        const uint32_t ah[4] = {byte_hi_nibble<0>(hi), byte_hi_nibble<1>(hi), byte_hi_nibble<2>(hi),
+                                byte_hi_nibble<3>(hi)};
+        const uint32_t al[4] = {byte_hi_nibble<0>(lo), byte_hi_nibble<1>(lo), byte_hi_nibble<2>(lo),
+                                byte_hi_nibble<3>(lo)};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 e1 = lds_at<uint4>(ptab, (uint32_t)(6 - 2 * k) * 256u + ah[k]);
+            const uint4 e2 = lds_at<uint4>(ptab, (uint32_t)(7 - 2 * k) * 256u + al[k]);
+            z[q] = x3(z[q], e1.x, e2.x);
+            z[q + 1] = x3(z[q + 1], e1.y, e2.y);
+            z[q + 2] = x3(z[q + 2], e1.z, e2.z);
+            z[q + 3] = x3(z[q + 3], e1.w, e2.w);
+        }
+    }
+}
+
 // gf_mul_pos with the tables at byte offset `off` (per lane, a multiple of 256) from `base`
 __device__ __forceinline__ uint4 gf_mul_pos_off(uint4 x, const void* base, uint32_t off) {
     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
@@ -1351,27 +1374,48 @@ struct RkLane {  // per-lane round keys (VGPRs): the lanes of a CTR group hold t
 
 // One CTR group: packet p on lanes 4·(lane/4) .. +3. A packet's AES blocks are its m ciphertext
 // blocks (counters 2 .. m+1) and J0 (counter 1): block j = 4r + l in round r on lane l, J0 last.
-template <bool OPEN, class TL>
-__device__ __forceinline__ void gcm_ctr_group(const GcmArgs& args, uint32_t p, bool valid, const TL& T,
-                                              uint32_t lane, const uint4* sums) {
-    const uint32_t l = lane & 3u;
-    neb_desc d = {};
-    if (valid) d = args.desc[p];
-    const bool key_in = d.key_id < args.max_keys;
-    const uint32_t* rec = args.keys + (size_t)(key_in ? d.key_id : 0u) * kKeyRecDwords;
-    uint32_t st = NEB_STATUS_OK;
-    if (!key_in || rec[kRecAlg] != NEB_ALG_AESGCM) st = NEB_STATUS_BAD_KEY;
-    if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
-    const bool run = valid && st == NEB_STATUS_OK;
+// CtrPkt holds what a group loads before its rounds (ctr_fetch), so a wave's first group can be
+// fetched while the workgroup fills its T-tables.
+struct CtrPkt {
+    neb_desc d;
+    uint32_t p;
+    uint32_t st;
+    bool valid;
     RkLane rk;
+};
+__device__ __forceinline__ CtrPkt ctr_fetch(const GcmArgs& args, const uint32_t* sorted, uint32_t q, uint32_t npkt,
+                                            bool open) {
+    CtrPkt c;
+    c.valid = q < npkt;
+    c.p = c.valid ? sorted[q] : 0u;
+    c.d = neb_desc{};
+    if (c.valid) c.d = args.desc[c.p];
+    const bool key_in = c.d.key_id < args.max_keys;
+    const uint32_t* rec = args.keys + (size_t)(key_in ? c.d.key_id : 0u) * kKeyRecDwords;
+    c.st = NEB_STATUS_OK;
+    if (!key_in || rec[kRecAlg] != NEB_ALG_AESGCM) c.st = NEB_STATUS_BAD_KEY;
+    if (!open && c.st == NEB_STATUS_OK && c.d.counter >= kRejectAfterMessages) c.st = NEB_STATUS_EXHAUSTED;
+    const bool run = c.valid && c.st == NEB_STATUS_OK;
 #pragma unroll
     for (int i = 0; i < 15; i++) {
         const uint4 v = run ? ld_rec4(rec, kRecRoundKeys + 4u * i) : make_uint4(0, 0, 0, 0);
-        rk.k[4 * i] = v.x;
-        rk.k[4 * i + 1] = v.y;
-        rk.k[4 * i + 2] = v.z;
-        rk.k[4 * i + 3] = v.w;
+        c.rk.k[4 * i] = v.x;
+        c.rk.k[4 * i + 1] = v.y;
+        c.rk.k[4 * i + 2] = v.z;
+        c.rk.k[4 * i + 3] = v.w;
     }
+    return c;
+}
+
+template <bool OPEN, class TL>
+__device__ __forceinline__ void gcm_ctr_group(const GcmArgs& args, const CtrPkt& cp, const TL& T, uint32_t lane,
+                                              const uint4* sums) {
+    const uint32_t l = lane & 3u;
+    const neb_desc& d = cp.d;
+    const uint32_t p = cp.p, st = cp.st;
+    const bool valid = cp.valid;
+    const RkLane& rk = cp.rk;
+    const bool run = valid && st == NEB_STATUS_OK;
     const uint32_t hdr = args.hdr_from_dst ? d.flags & kCsHdrMask : 0u;
     const uint32_t m = (d.len + 15u) >> 4;
     const uint32_t R = run ? (m + 4u) >> 2 : 0u;  // m + 1 blocks over 4 lanes
@@ -1450,25 +1494,33 @@ __global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, c
     if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
     const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
     if (blockIdx.x >= ngroups) return;  // uniform over the workgroup
+    // the wave's first group is fetched (index, descriptor, key) before the T-table fill, so its
+    // chain of dependent loads runs under the fill instead of after it
+    uint32_t grp = blockIdx.x + wave * gridDim.x;
+    CtrPkt cp = ctr_fetch(args, sorted, grp * kPpw + (lane >> 2), npkt, OPEN);
     fill_ttab<2u * 256u * 32u, kCtrThreads>(lds.ttab, tid, ttab4_entry);
     __syncthreads();
     const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
     const uint32_t slots = gridDim.x * kCtrWaves;
-    for (uint32_t grp = blockIdx.x + wave * gridDim.x; grp < ngroups; grp += slots) {
-        const uint32_t q = grp * kPpw + (lane >> 2);
-        const bool valid = q < npkt;
-        const uint32_t p = valid ? sorted[q] : 0u;
-        gcm_ctr_group<OPEN>(args, p, valid, T, lane, sums);
+    for (; grp < ngroups; grp += slots) {
+        gcm_ctr_group<OPEN>(args, cp, T, lane, sums);
+        if (grp + slots < ngroups) cp = ctr_fetch(args, sorted, (grp + slots) * kPpw + (lane >> 2), npkt, OPEN);
     }
 }
 
 // The GHASH half of a packet group of the mixed-key split (lanes and padding as gcm_packet_group:
 // lane l owns padded blocks 2^lg·r + l + 1 of AAD || CT || lengths), reading the ciphertext (seal:
-// written by the CTR pass at dst; open: at src). Each round's block is loaded a round ahead.
-template <bool OPEN, class GH>
+// written by the CTR pass at dst; open: at src). Without the AES a round is a few hundred cycles,
+// shorter than a block's load from memory, so the rounds are aggregated U at a time:
+//   A <- A·H^(U·L) ⊕ X_0·H^((U-1)·L) ⊕ ... ⊕ X_(U-2)·H^L ⊕ X_(U-1)      (L = 2^lg lanes per packet)
+// — U independent products reduced once, only the first on the dependent chain, and the next U
+// blocks loaded while they run. pos + 128·k: the position tables of H^((k+1)·L), k < U. A packet
+// whose round count is not a multiple of U starts with zero rounds (a zero block leaves a Horner
+// sum from zero unchanged).
+template <bool OPEN, int U, class GH>
 __device__ __forceinline__ void ghash_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                    bool key_ok, const GH& gh, uint32_t lane, uint32_t lg,
-                                                   uint4* sums) {
+                                                   uint4* sums, const uint4* pos) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
@@ -1483,11 +1535,13 @@ __device__ __forceinline__ void ghash_packet_group(const GcmArgs& args, uint32_t
     sh.n = sh.na + sh.m + 1u;
     sh.R = run ? (sh.n + LPP - 1u) >> lg : 0u;
     sh.pad = (sh.R << lg) - sh.n;
+    const uint32_t M = (sh.R + U - 1u) / U;      // aggregated rounds
+    const int32_t front = (int32_t)(U * M - sh.R);  // leading zero rounds
     const uint8_t* ct = args.arena + (OPEN ? d.src_off : d.dst_off);
-    auto load = [&](uint32_t r) -> uint4 {  // round r's GHASH input block (big-endian words)
+    auto load = [&](int32_t r) -> uint4 {  // round r's GHASH input block (big-endian words)
         uint4 X = make_uint4(0, 0, 0, 0);
-        if (r >= sh.R) return X;
-        const LaneBlock b = lane_block(sh, r, l, lg);
+        if (r < 0 || (uint32_t)r >= sh.R) return X;
+        const LaneBlock b = lane_block(sh, (uint32_t)r, l, lg);
         if (b.is_ct) {
             const uint32_t off = 16u * (b.k - 1u);
             const uint8_t* q = ct + off;
@@ -1504,11 +1558,26 @@ __device__ __forceinline__ void ghash_packet_group(const GcmArgs& args, uint32_t
         return X;
     };
     uint4 A = make_uint4(0, 0, 0, 0);
-    uint4 X = load(0);
-    for (uint32_t r = 0; __any(r < sh.R); r++) {
-        const uint4 Xn = load(r + 1u);
-        if (r < sh.R) A = r == 0u ? X : xor4(gh.horner(A, lg), X);
-        X = Xn;
+    uint4 X[U];
+#pragma unroll
+    for (int i = 0; i < U; i++) X[i] = load(i - front);
+    for (uint32_t mr = 0; __any(mr < M); mr++) {
+        uint4 Xn[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) Xn[i] = load((int32_t)(U * (mr + 1u)) + i - front);
+        if (mr < M) {
+            if constexpr (U == 1) {
+                A = mr == 0u ? X[0] : xor4(gh.horner(A, lg), X[0]);
+            } else {
+                uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (mr) gf_acc_pos(A, pos + 128u * (U - 1), z);
+#pragma unroll
+                for (int i = 0; i < U - 1; i++) gf_acc_pos(X[i], pos + 128u * (U - 2 - i), z);
+                A = xor4(gf_reduce(z), X[U - 1]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++) X[i] = Xn[i];
     }
     const uint4 V = gh.final(A, lane, lg);  // every lane: the final shuffles across lanes
     if (l == LPP - 1u) {
@@ -1529,10 +1598,43 @@ constexpr int kGhThreads = kGhWaves * kWave;
 #ifndef NEB_GH_WPE
 #define NEB_GH_WPE 4  // launch bound: waves per SIMD (2 workgroups of 8 waves per CU; 5 spills)
 #endif
+constexpr int kGhMaxU = 3;
 struct GhLds {
-    uint4 shoup[kGhWaves][4][16];  // per wave: M_1..M_4 (full chunks), M_1, M_2, M_4, M_8 (tails)
-    uint4 pos[kGhWaves][8 * 16];   // per wave: position tables of H^(2^lg)
+    uint4 shoup[kGhWaves][4][16];          // per wave: M_1..M_4 (full chunks), M_1, M_2, M_4, M_8 (tails)
+    uint4 pos[kGhWaves][kGhMaxU][8 * 16];  // per wave: position tables of H^4, H^8, H^12 (tails: H^(2^lg))
 };
+
+// A chunk key's GHASH tables for the GHASH pass, copied from the record: lane L loads entry L of
+// the Shoup tables and entries L, L + 64 of each position table — front chunks M_1..M_4 and the
+// position tables of H^4 (the full table's first 8 positions), H^8, H^12; tails M_1, M_2, M_4, M_8
+// and those of H^(2^lg).
+template <bool FULL>
+__device__ __forceinline__ void stage_gh_tables(const uint32_t* rec, uint32_t lane, uint32_t lg, uint4* wtab,
+                                                uint4* wpos) {
+    const uint32_t t = lane >> 4, v = lane & 15u;
+    const uint4 sv = ld_rec4(rec, (FULL ? kRecShoup + 64u * t : rec_shoup_pow2(t)) + 4u * v);
+    if constexpr (FULL) {
+        const uint32_t src[kGhMaxU] = {kRecFull, kRecPos8, kRecPos12};
+        uint4 e[2 * kGhMaxU];
+#pragma unroll
+        for (int k = 0; k < kGhMaxU; k++) {
+            e[2 * k] = ld_rec4(rec, src[k] + 4u * lane);
+            e[2 * k + 1] = ld_rec4(rec, src[k] + 4u * (64u + lane));
+        }
+        wtab[lane] = sv;
+#pragma unroll
+        for (int k = 0; k < kGhMaxU; k++) {
+            wpos[128u * k + lane] = e[2 * k];
+            wpos[128u * k + 64u + lane] = e[2 * k + 1];
+        }
+    } else {
+        const uint32_t src = rec_pos_table(lg);
+        const uint4 e0 = ld_rec4(rec, src + 4u * lane), e1 = ld_rec4(rec, src + 4u * (64u + lane));
+        wtab[lane] = sv;
+        wpos[lane] = e0;
+        wpos[64u + lane] = e1;
+    }
+}
 
 // The scheduler's chunks (sched.hpp), owned and drawn as in gcm_chunk_kernel (workgroup w: chunks
 // w, w + G, ..., its waves through an LDS cursor one chunk ahead).
@@ -1549,7 +1651,7 @@ __global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmAr
     if (tid == 0) wg_cursor = kGhWaves;
     __syncthreads();
     uint4* wtab = &lds.shoup[wave][0][0];
-    uint4* wpos = &lds.pos[wave][0];
+    uint4* wpos = &lds.pos[wave][0][0];
     auto chunk_at = [&](uint32_t c) {
         return ca.chunks[c < nfront ? c : c < nfront + nlong ? ca.max_chunks - 1u - (c - nfront) : ca.max_chunks + (c - nfront - nlong)];
     };
@@ -1571,23 +1673,27 @@ __global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmAr
         const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
         const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
         const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
+        const uint32_t cls = __builtin_amdgcn_readfirstlane(ch.w & ((1u << kChunkLgShift) - 1u));
         const uint32_t* rec = args.keys + (size_t)(key < args.max_keys ? key : 0u) * kKeyRecDwords;
         const bool key_ok = key < args.max_keys && rec[kRecAlg] == NEB_ALG_AESGCM;
         if (full) {
-            stage_chunk_tables<true>(rec, ln, 2u, wtab, wpos);
+            stage_gh_tables<true>(rec, ln, 2u, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const GhChunk4 gh{wtab, wpos};
+            // aggregation by size class (rounds at 4 lanes: class 0 one, 1-2 up to 4, else 5+)
             for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
                 const uint32_t q = g0 + (ln >> 2);
                 const bool valid = q < count;
                 const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-                ghash_packet_group<OPEN>(args, p, valid, key, key_ok, gh, ln, 2u, sums);
+                if (cls >= 3u) ghash_packet_group<OPEN, 3>(args, p, valid, key, key_ok, gh, ln, 2u, sums, wpos);
+                else if (cls >= 1u) ghash_packet_group<OPEN, 2>(args, p, valid, key, key_ok, gh, ln, 2u, sums, wpos);
+                else ghash_packet_group<OPEN, 1>(args, p, valid, key, key_ok, gh, ln, 2u, sums, wpos);
             }
         } else {
             const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
-            stage_chunk_tables<false>(rec, ln, lg, wtab, wpos);
+            stage_gh_tables<false>(rec, ln, lg, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1595,7 +1701,7 @@ __global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmAr
             const bool valid = q < count;
             const uint32_t p = valid ? ca.sorted[start + q] : 0u;
             const GhChunkTree gh{wtab, wpos};
-            ghash_packet_group<OPEN>(args, p, valid, key, key_ok, gh, ln, lg, sums);
+            ghash_packet_group<OPEN, 1>(args, p, valid, key, key_ok, gh, ln, lg, sums, wpos);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
@@ -1624,6 +1730,7 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
     __shared__ uint4 basis8[32];  // x^i · H^8
     __shared__ uint4 basis16[32]; // x^i · H^16
     __shared__ uint4 basis23[2][32]; // x^i · H^2, x^i · H^3
+    __shared__ uint4 basis12[32];    // x^i · H^12
     __shared__ uint4 basis_h[128];  // x^i · H
     __shared__ uint4 part[2];
     // the S-box in LDS for the key schedule and H = E_K(0) on lane 0: its ~330 dependent lookups
@@ -1706,6 +1813,7 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         basis16[threadIdx.x] = gf_mul_xpow(hp[15], threadIdx.x);
         basis23[0][threadIdx.x] = gf_mul_xpow(hp[1], threadIdx.x);
         basis23[1][threadIdx.x] = gf_mul_xpow(hp[2], threadIdx.x);
+        basis12[threadIdx.x] = gf_mul_xpow(hp[11], threadIdx.x);
     }
     if (threadIdx.x == 0) rec[kRecAlg] = NEB_ALG_AESGCM;
     __syncthreads();
@@ -1742,6 +1850,14 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
         for (uint32_t j = 0; j < 4; j++)
             if ((v >> (3 - j)) & 1u) e = xor4(e, basis_h[4 * r + j]);
         uint32_t* o = rec + kRecPos1 + 4u * t;
+        o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
+    }
+    if (t < 128u) {  // and of H^12
+        const uint32_t r = t >> 4, v = t & 15u;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        for (uint32_t j = 0; j < 4; j++)
+            if ((v >> (3 - j)) & 1u) e = xor4(e, basis12[4 * r + j]);
+        uint32_t* o = rec + kRecPos12 + 4u * t;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
     {  // and of H^2, H^3

@@ -9,6 +9,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
+#include <deque>
 #include <cstring>
 #include <cstdlib>
 #include <mutex>
@@ -130,25 +131,29 @@ struct TxSpace {
 // Per-packet CipherState calls (neb_encrypt_danger / neb_decrypt_danger) and key installs share a
 // fixed pool of kPktSlots slots per engine: a stream and pinned, mapped staging the kernel reads
 // and writes in place ([desc 64 B | status 64 B | aad | payload + tag]). The box grants a process 4
-// hardware queues, so more streams only queue behind each other in the driver. A call takes a
-// ticket t and runs on slot t mod kPktSlots once that slot's turn reaches t / kPktSlots: FIFO per
-// slot, so a call waits only for the calls ahead of it, however many threads call. (Round 3 gave
-// every calling OS thread its own slot and stream, kept until the engine died: the count grew with
-// the threads cgo ever used, a thread alternating over more than 8 engines leaked one per call, and
-// at 64 threads p99 was 100x p50.)
+// hardware queues, so more streams only queue behind each other in the driver. A call takes a free
+// slot, or joins one FIFO of waiters and sleeps until a finishing call hands it its slot directly
+// (one wake-up per hand-off, nobody spins): the wait of a call is bounded by the calls ahead of
+// it, however many threads call. (Round 3 gave every calling OS thread its own slot and stream,
+// kept until the engine died: the count grew with the threads cgo ever used, a thread alternating
+// over more than 8 engines leaked one per call, and at 64 threads p99 was 100x p50.)
 constexpr uint32_t kPktSlots = 4;
 struct PktSlot {
     hipStream_t stream = nullptr;
     uint8_t* h = nullptr;
     size_t cap = 0;
-    std::atomic<uint64_t> turn{0};
-    std::mutex mu;
+};
+struct PktWaiter {
     std::condition_variable cv;
+    PktSlot* got = nullptr;
 };
 struct PktPool {
-    std::atomic<uint64_t> ticket{0};
-    std::atomic<uint64_t> calls{0}, waits{0};
+    std::mutex mu;
     PktSlot slot[kPktSlots];
+    PktSlot* free_[kPktSlots] = {};
+    uint32_t nfree = 0;
+    std::deque<PktWaiter*> waiters;
+    std::atomic<uint64_t> calls{0}, waits{0};
 };
 struct KeyUse {
     hipStream_t s;
@@ -235,27 +240,29 @@ static void set_error(const char* where, hipError_t err) {
 // Exclusive use of one slot of e's per-packet pool for the lifetime of the lease (PktPool).
 class PktLease {
   public:
-    explicit PktLease(PktPool& p) {
-        const uint64_t t = p.ticket.fetch_add(1, std::memory_order_relaxed);
-        s_ = &p.slot[t % kPktSlots];
-        want_ = t / kPktSlots;
+    explicit PktLease(PktPool& p) : p_(p) {
+        std::unique_lock<std::mutex> lk(p.mu);
         p.calls.fetch_add(1, std::memory_order_relaxed);
-        if (s_->turn.load(std::memory_order_acquire) == want_) return;
-        p.waits.fetch_add(1, std::memory_order_relaxed);
-        // a call holds its slot ≈ 30 µs: yield a few times before sleeping on the slot
-        for (int i = 0; i < 16; i++) {
-            std::this_thread::yield();
-            if (s_->turn.load(std::memory_order_acquire) == want_) return;
+        if (p.nfree) {
+            s_ = p.free_[--p.nfree];
+            return;
         }
-        std::unique_lock<std::mutex> g(s_->mu);
-        s_->cv.wait(g, [&] { return s_->turn.load(std::memory_order_acquire) == want_; });
+        p.waits.fetch_add(1, std::memory_order_relaxed);
+        PktWaiter w;
+        p.waiters.push_back(&w);
+        w.cv.wait(lk, [&] { return w.got != nullptr; });
+        s_ = w.got;
     }
     ~PktLease() {
-        {
-            std::lock_guard<std::mutex> g(s_->mu);  // no lost wake-up between a waiter's check and its sleep
-            s_->turn.store(want_ + 1, std::memory_order_release);
+        std::lock_guard<std::mutex> g(p_.mu);
+        if (p_.waiters.empty()) {
+            p_.free_[p_.nfree++] = s_;
+            return;
         }
-        s_->cv.notify_all();
+        PktWaiter* w = p_.waiters.front();  // FIFO: the longest waiter gets the slot
+        p_.waiters.pop_front();
+        w->got = s_;
+        w->cv.notify_one();
     }
     PktLease(const PktLease&) = delete;
     PktLease& operator=(const PktLease&) = delete;
@@ -278,8 +285,8 @@ class PktLease {
     }
 
   private:
+    PktPool& p_;
     PktSlot* s_ = nullptr;
-    uint64_t want_ = 0;
 };
 
 // After an asynchronous batch is enqueued on stream s: remember it for neb_cipher_destroy (the
@@ -368,9 +375,14 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
               hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) == hipSuccess &&
               hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) == hipSuccess &&
               hipStreamSynchronize(nullptr) == hipSuccess;  // the null-stream memset, before any stream reads keys
-    for (PktSlot& sl : e->pkt.slot)
+    for (PktSlot& sl : e->pkt.slot) {
         ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess &&
-             hipHostMalloc((void**)&sl.h, kStageMin, hipHostMallocDefault) == hipSuccess && (sl.cap = kStageMin);
+             hipHostMalloc((void**)&sl.h, kStageMin, hipHostMallocDefault) == hipSuccess;
+        if (ok) {
+            sl.cap = kStageMin;
+            e->pkt.free_[e->pkt.nfree++] = &sl;
+        }
+    }
     if (!ok) {
         set_error("engine allocation", hipGetLastError());
         neb_engine_destroy(e);
