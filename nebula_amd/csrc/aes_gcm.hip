@@ -24,6 +24,7 @@
 #include <hip/hip_ext.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <stdint.h>
 
 #include <type_traits>
@@ -1370,22 +1371,52 @@ struct RkLane {  // per-lane round keys (VGPRs): the lanes of a CTR group hold t
     __device__ __forceinline__ uint4 get(int r) const {
         return make_uint4(k[4 * r], k[4 * r + 1], k[4 * r + 2], k[4 * r + 3]);
     }
+    __device__ __forceinline__ void load(const uint32_t* rec, bool run, uint32_t) {
+#pragma unroll
+        for (int i = 0; i < 15; i++) {
+            const uint4 v = run ? ld_rec4(rec, kRecRoundKeys + 4u * i) : make_uint4(0, 0, 0, 0);
+            k[4 * i] = v.x;
+            k[4 * i + 1] = v.y;
+            k[4 * i + 2] = v.z;
+            k[4 * i + 3] = v.w;
+        }
+    }
+};
+// The same keys spread over the packet's quad of lanes: lane w holds word w of every round key (15
+// VGPRs instead of 60), and a round's key is broadcast across the quad by four DPP moves (+4 VALU
+// per AES round). A quad's lanes are active together (a packet's lanes share its round count).
+struct RkQuad {
+    uint32_t q[15];
+    static constexpr bool kUniform = false;
+    __device__ __forceinline__ uint4 get(int r) const {
+        return make_uint4((uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0x00, 0xF, 0xF, false),
+                          (uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0x55, 0xF, 0xF, false),
+                          (uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0xAA, 0xF, 0xF, false),
+                          (uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0xFF, 0xF, 0xF, false));
+    }
+    __device__ __forceinline__ void load(const uint32_t* rec, bool run, uint32_t lane) {
+        const uint32_t w = lane & 3u;
+#pragma unroll
+        for (int i = 0; i < 15; i++) q[i] = run ? rec[kRecRoundKeys + 4u * i + w] : 0u;
+    }
 };
 
 // One CTR group: packet p on lanes 4·(lane/4) .. +3. A packet's AES blocks are its m ciphertext
 // blocks (counters 2 .. m+1) and J0 (counter 1): block j = 4r + l in round r on lane l, J0 last.
 // CtrPkt holds what a group loads before its rounds (ctr_fetch), so a wave's first group can be
 // fetched while the workgroup fills its T-tables.
+template <class RK>
 struct CtrPkt {
     neb_desc d;
     uint32_t p;
     uint32_t st;
     bool valid;
-    RkLane rk;
+    RK rk;
 };
-__device__ __forceinline__ CtrPkt ctr_fetch(const GcmArgs& args, const uint32_t* sorted, uint32_t q, uint32_t npkt,
-                                            bool open) {
-    CtrPkt c;
+template <class RK>
+__device__ __forceinline__ CtrPkt<RK> ctr_fetch(const GcmArgs& args, const uint32_t* sorted, uint32_t q, uint32_t npkt,
+                                                bool open, uint32_t lane) {
+    CtrPkt<RK> c;
     c.valid = q < npkt;
     c.p = c.valid ? sorted[q] : 0u;
     c.d = neb_desc{};
@@ -1395,26 +1426,18 @@ __device__ __forceinline__ CtrPkt ctr_fetch(const GcmArgs& args, const uint32_t*
     c.st = NEB_STATUS_OK;
     if (!key_in || rec[kRecAlg] != NEB_ALG_AESGCM) c.st = NEB_STATUS_BAD_KEY;
     if (!open && c.st == NEB_STATUS_OK && c.d.counter >= kRejectAfterMessages) c.st = NEB_STATUS_EXHAUSTED;
-    const bool run = c.valid && c.st == NEB_STATUS_OK;
-#pragma unroll
-    for (int i = 0; i < 15; i++) {
-        const uint4 v = run ? ld_rec4(rec, kRecRoundKeys + 4u * i) : make_uint4(0, 0, 0, 0);
-        c.rk.k[4 * i] = v.x;
-        c.rk.k[4 * i + 1] = v.y;
-        c.rk.k[4 * i + 2] = v.z;
-        c.rk.k[4 * i + 3] = v.w;
-    }
+    c.rk.load(rec, c.valid && c.st == NEB_STATUS_OK, lane);
     return c;
 }
 
-template <bool OPEN, class TL>
-__device__ __forceinline__ void gcm_ctr_group(const GcmArgs& args, const CtrPkt& cp, const TL& T, uint32_t lane,
+template <bool OPEN, class TL, class RK>
+__device__ __forceinline__ void gcm_ctr_group(const GcmArgs& args, const CtrPkt<RK>& cp, const TL& T, uint32_t lane,
                                               const uint4* sums) {
     const uint32_t l = lane & 3u;
     const neb_desc& d = cp.d;
     const uint32_t p = cp.p, st = cp.st;
     const bool valid = cp.valid;
-    const RkLane& rk = cp.rk;
+    const RK& rk = cp.rk;
     const bool run = valid && st == NEB_STATUS_OK;
     const uint32_t hdr = args.hdr_from_dst ? d.flags & kCsHdrMask : 0u;
     const uint32_t m = (d.len + 15u) >> 4;
@@ -1485,9 +1508,11 @@ struct CtrLds {
 
 // Groups of 16 consecutive packets of the scheduler's order (sorted: bins by size class, then key,
 // so a group's packets are alike in size); group g on workgroup g mod G, as in gcm_single_kernel.
-template <bool OPEN>
+// QUAD: the round keys spread over each packet's quad (RkQuad), else whole in every lane (RkLane).
+template <bool OPEN, bool QUAD>
 __global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, const uint32_t* __restrict__ sorted,
                                                                  const uint4* __restrict__ sums) {
+    using RK = std::conditional_t<QUAD, RkQuad, RkLane>;
     __shared__ CtrLds lds;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint32_t npkt = args.npkt;
@@ -1497,14 +1522,14 @@ __global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, c
     // the wave's first group is fetched (index, descriptor, key) before the T-table fill, so its
     // chain of dependent loads runs under the fill instead of after it
     uint32_t grp = blockIdx.x + wave * gridDim.x;
-    CtrPkt cp = ctr_fetch(args, sorted, grp * kPpw + (lane >> 2), npkt, OPEN);
+    CtrPkt<RK> cp = ctr_fetch<RK>(args, sorted, grp * kPpw + (lane >> 2), npkt, OPEN, lane);
     fill_ttab<2u * 256u * 32u, kCtrThreads>(lds.ttab, tid, ttab4_entry);
     __syncthreads();
     const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
     const uint32_t slots = gridDim.x * kCtrWaves;
     for (; grp < ngroups; grp += slots) {
         gcm_ctr_group<OPEN>(args, cp, T, lane, sums);
-        if (grp + slots < ngroups) cp = ctr_fetch(args, sorted, (grp + slots) * kPpw + (lane >> 2), npkt, OPEN);
+        if (grp + slots < ngroups) cp = ctr_fetch<RK>(args, sorted, (grp + slots) * kPpw + (lane >> 2), npkt, OPEN, lane);
     }
 }
 
@@ -2063,9 +2088,17 @@ template <bool OPEN>
 static hipError_t launch_split(const neb::GcmArgs& a, const neb::ChunkArgs& ca, uint32_t max_chunks, uint4* d_sums,
                                int cu_count, hipStream_t s) {
     const uint32_t groups = (a.npkt + neb::kPpw - 1u) / neb::kPpw;
+    // NEB_CTR_RK=lane: every lane holds its packet's 60 round-key words (A/B against the quad form)
+    static const bool lane_rk = [] {
+        const char* v = std::getenv("NEB_CTR_RK");
+        return v && !std::strcmp(v, "lane");
+    }();
     auto ctr = [&]() {
-        return launch_grid(neb::gcm_ctr_kernel<OPEN>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves, cu_count, s,
-                           a, ca.sorted, (const uint4*)d_sums);
+        if (lane_rk)
+            return launch_grid(neb::gcm_ctr_kernel<OPEN, false>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves,
+                               cu_count, s, a, ca.sorted, (const uint4*)d_sums);
+        return launch_grid(neb::gcm_ctr_kernel<OPEN, true>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves,
+                           cu_count, s, a, ca.sorted, (const uint4*)d_sums);
     };
     auto gh = [&]() {
         return launch_grid(neb::gcm_ghash_kernel<OPEN>, neb::kGhThreads, max_chunks * (uint32_t)neb::kGhWaves, cu_count,
