@@ -1235,6 +1235,7 @@ __device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t
 
 struct ChunkArgs {
     const uint32_t* sorted;
+    const neb_desc* sdesc;  // descriptors in `sorted` order (the split passes)
     const uint4* chunks;
     uint32_t* counters;  // the scheduler's counters (sched.hpp kCnt*)
     uint32_t max_chunks, max_short;
@@ -1414,13 +1415,13 @@ struct CtrPkt {
     RK rk;
 };
 template <class RK>
-__device__ __forceinline__ CtrPkt<RK> ctr_fetch(const GcmArgs& args, const uint32_t* sorted, uint32_t q, uint32_t npkt,
-                                                bool open, uint32_t lane) {
+__device__ __forceinline__ CtrPkt<RK> ctr_fetch(const GcmArgs& args, const uint32_t* sorted, const neb_desc* sdesc,
+                                                uint32_t q, uint32_t npkt, bool open, uint32_t lane) {
     CtrPkt<RK> c;
     c.valid = q < npkt;
     c.p = c.valid ? sorted[q] : 0u;
     c.d = neb_desc{};
-    if (c.valid) c.d = args.desc[c.p];
+    if (c.valid) c.d = sdesc[q];
     const bool key_in = c.d.key_id < args.max_keys;
     const uint32_t* rec = args.keys + (size_t)(key_in ? c.d.key_id : 0u) * kKeyRecDwords;
     c.st = NEB_STATUS_OK;
@@ -1511,6 +1512,7 @@ struct CtrLds {
 // QUAD: the round keys spread over each packet's quad (RkQuad), else whole in every lane (RkLane).
 template <bool OPEN, bool QUAD>
 __global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, const uint32_t* __restrict__ sorted,
+                                                                 const neb_desc* __restrict__ sdesc,
                                                                  const uint4* __restrict__ sums) {
     using RK = std::conditional_t<QUAD, RkQuad, RkLane>;
     __shared__ CtrLds lds;
@@ -1522,14 +1524,15 @@ __global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, c
     // the wave's first group is fetched (index, descriptor, key) before the T-table fill, so its
     // chain of dependent loads runs under the fill instead of after it
     uint32_t grp = blockIdx.x + wave * gridDim.x;
-    CtrPkt<RK> cp = ctr_fetch<RK>(args, sorted, grp * kPpw + (lane >> 2), npkt, OPEN, lane);
+    CtrPkt<RK> cp = ctr_fetch<RK>(args, sorted, sdesc, grp * kPpw + (lane >> 2), npkt, OPEN, lane);
     fill_ttab<2u * 256u * 32u, kCtrThreads>(lds.ttab, tid, ttab4_entry);
     __syncthreads();
     const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
     const uint32_t slots = gridDim.x * kCtrWaves;
     for (; grp < ngroups; grp += slots) {
         gcm_ctr_group<OPEN>(args, cp, T, lane, sums);
-        if (grp + slots < ngroups) cp = ctr_fetch<RK>(args, sorted, (grp + slots) * kPpw + (lane >> 2), npkt, OPEN, lane);
+        if (grp + slots < ngroups)
+            cp = ctr_fetch<RK>(args, sorted, sdesc, (grp + slots) * kPpw + (lane >> 2), npkt, OPEN, lane);
     }
 }
 
@@ -1543,13 +1546,17 @@ __global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, c
 // whose round count is not a multiple of U starts with zero rounds (a zero block leaves a Horner
 // sum from zero unchanged).
 template <bool OPEN, int U, class GH>
-__device__ __forceinline__ void ghash_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
-                                                   bool key_ok, const GH& gh, uint32_t lane, uint32_t lg,
-                                                   uint4* sums, const uint4* pos) {
+__device__ __forceinline__ void ghash_packet_group(const GcmArgs& args, const ChunkArgs& ca, uint32_t q, bool valid,
+                                                   uint32_t expect_key, bool key_ok, const GH& gh, uint32_t lane,
+                                                   uint32_t lg, uint4* sums, const uint4* pos) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
+    uint32_t p = 0;
     neb_desc d = {};
-    if (valid) d = args.desc[p];
+    if (valid) {  // two independent loads: the index and the scheduler's copy of the descriptor
+        p = ca.sorted[q];
+        d = ca.sdesc[q];
+    }
     uint32_t st = NEB_STATUS_OK;
     if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
     if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
@@ -1711,10 +1718,9 @@ __global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmAr
             for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
                 const uint32_t q = g0 + (ln >> 2);
                 const bool valid = q < count;
-                const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-                if (cls >= 3u) ghash_packet_group<OPEN, 3>(args, p, valid, key, key_ok, gh, ln, 2u, sums, wpos);
-                else if (cls >= 1u) ghash_packet_group<OPEN, 2>(args, p, valid, key, key_ok, gh, ln, 2u, sums, wpos);
-                else ghash_packet_group<OPEN, 1>(args, p, valid, key, key_ok, gh, ln, 2u, sums, wpos);
+                if (cls >= 3u) ghash_packet_group<OPEN, 3>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
+                else if (cls >= 1u) ghash_packet_group<OPEN, 2>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
+                else ghash_packet_group<OPEN, 1>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
             }
         } else {
             const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
@@ -1724,9 +1730,8 @@ __global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmAr
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t q = ln >> lg;
             const bool valid = q < count;
-            const uint32_t p = valid ? ca.sorted[start + q] : 0u;
             const GhChunkTree gh{wtab, wpos};
-            ghash_packet_group<OPEN, 1>(args, p, valid, key, key_ok, gh, ln, lg, sums, wpos);
+            ghash_packet_group<OPEN, 1>(args, ca, start + q, valid, key, key_ok, gh, ln, lg, sums, wpos);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
@@ -2073,7 +2078,7 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
-    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks, max_short};
+    neb::ChunkArgs ca{d_sorted, nullptr, d_chunks, d_counters, max_chunks, max_short};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
     // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.
@@ -2096,9 +2101,9 @@ static hipError_t launch_split(const neb::GcmArgs& a, const neb::ChunkArgs& ca, 
     auto ctr = [&]() {
         if (lane_rk)
             return launch_grid(neb::gcm_ctr_kernel<OPEN, false>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves,
-                               cu_count, s, a, ca.sorted, (const uint4*)d_sums);
+                               cu_count, s, a, ca.sorted, ca.sdesc, (const uint4*)d_sums);
         return launch_grid(neb::gcm_ctr_kernel<OPEN, true>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves,
-                           cu_count, s, a, ca.sorted, (const uint4*)d_sums);
+                           cu_count, s, a, ca.sorted, ca.sdesc, (const uint4*)d_sums);
     };
     auto gh = [&]() {
         return launch_grid(neb::gcm_ghash_kernel<OPEN>, neb::kGhThreads, max_chunks * (uint32_t)neb::kGhWaves, cu_count,
@@ -2111,11 +2116,12 @@ static hipError_t launch_split(const neb::GcmArgs& a, const neb::ChunkArgs& ca, 
 
 extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
                                           uint8_t* d_arena, const uint32_t* d_keys, uint32_t max_keys,
-                                          int32_t* d_status, const uint32_t* d_sorted, const uint4* d_chunks,
-                                          uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
-                                          uint4* d_sums, int cu_count, hipStream_t s, int hdr_from_dst) {
+                                          int32_t* d_status, const uint32_t* d_sorted, const neb_desc* d_sdesc,
+                                          const uint4* d_chunks, uint32_t* d_counters, uint32_t max_chunks,
+                                          uint32_t max_short, uint4* d_sums, int cu_count, hipStream_t s,
+                                          int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
-    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks, max_short};
+    neb::ChunkArgs ca{d_sorted, d_sdesc, d_chunks, d_counters, max_chunks, max_short};
     return open ? launch_split<true>(a, ca, max_chunks, d_sums, cu_count, s)
                 : launch_split<false>(a, ca, max_chunks, d_sums, cu_count, s);
 }

@@ -42,9 +42,10 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             int cu_count, hipStream_t s, int hdr_from_dst);
 extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
                                           uint8_t* d_arena, const uint32_t* d_keys, uint32_t max_keys,
-                                          int32_t* d_status, const uint32_t* d_sorted, const uint4* d_chunks,
-                                          uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
-                                          uint4* d_sums, int cu_count, hipStream_t s, int hdr_from_dst);
+                                          int32_t* d_status, const uint32_t* d_sorted, const neb_desc* d_sdesc,
+                                          const uint4* d_chunks, uint32_t* d_counters, uint32_t max_chunks,
+                                          uint32_t max_short, uint4* d_sums, int cu_count, hipStream_t s,
+                                          int hdr_from_dst);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int hdr_from_dst);
 #ifndef NEB_TX_CSUM_SEAL
@@ -711,8 +712,8 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     const size_t b_counters = align_up((neb::kSchedCounters + (size_t)neb::kSubBins * nb) * 4u, 256);
     const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up(((size_t)mc + ms) * 16u, 256);
-    const size_t b_sums = (size_t)cap * 16u;
-    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_sums;
+    const size_t b_sums = (size_t)cap * 16u, b_sdesc = (size_t)cap * sizeof(neb_desc);
+    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_sums + b_sdesc;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
     if (sp.mem) hipFree(sp.mem);
@@ -735,6 +736,8 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     sp.ws.chunks = (uint4*)m;
     m += b_chunks;
     sp.ws.sums = (uint4*)m;
+    m += b_sums;
+    sp.ws.sdesc = (neb_desc*)m;
     sp.ws.max_chunks = mc;
     sp.ws.max_short = ms;
     sp.bytes = bytes;
@@ -771,8 +774,8 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         if (err == hipSuccess) {
             if (mixed_split())
                 err = neb_gcm_batch_split(open, d_desc, n, d_n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                          sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, sp.ws.sums,
-                                          e->cu_count, s, hdr_from_dst);
+                                          sp.ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
+                                          sp.ws.sums, e->cu_count, s, hdr_from_dst);
             else
                 err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                             sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,

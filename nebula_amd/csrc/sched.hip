@@ -104,11 +104,14 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     }
 }
 
-// pass 3: scatter packet indices into their bin's range, at the rank pass 1 drew
-__global__ void sched_scatter_kernel(uint32_t n, const uint32_t* dn, SchedWs ws) {
+// pass 3: scatter packet indices and descriptors into their bin's range, at the rank pass 1 drew
+__global__ void sched_scatter_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn, SchedWs ws) {
     if (dn) n = min(n, *dn);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        ws.sorted[ws.base[ws.binof[i]] + ws.binpos[i]] = i;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t j = ws.base[ws.binof[i]] + ws.binpos[i];
+        ws.sorted[j] = i;
+        ws.sdesc[j] = desc[i];
+    }
 }
 
 // Descriptors of a shard whose engine disagrees with engine 0 on some key slots (engine.cpp
@@ -141,6 +144,6 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     hipLaunchKernelGGL(neb::sched_hist_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp, *ws);
     hipLaunchKernelGGL(neb::sched_alloc_kernel, dim3((nb + neb::kAllocThreads - 1) / neb::kAllocThreads),
                        dim3(neb::kAllocThreads), 0, s, max_keys, *ws);
-    hipLaunchKernelGGL(neb::sched_scatter_kernel, dim3(gp), dim3(tpb), 0, s, n, d_n, *ws);
+    hipLaunchKernelGGL(neb::sched_scatter_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, *ws);
     return hipGetLastError();
 }
