@@ -758,9 +758,14 @@ static bool mixed_split() {
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
 // only known on the device, e.g. the segments of a TX batch). hdr_from_dst: the TX batch's
 // descriptors (tx.hip) read their first `flags` plaintext bytes from the destination.
+// host_arena: the arena is pinned host memory the kernels reach over PCIe (zero-copy batches, the
+// submission queue): mixed-key AES-GCM then runs the fused chunk kernel, which reads each packet
+// once — the split passes read the ciphertext twice and put two chains of PCIe-latency rounds
+// where the fused kernel has one.
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr,
-                               SchedSpace* sched = nullptr, int hdr_from_dst = 0, hipEvent_t stop = nullptr) {
+                               SchedSpace* sched = nullptr, int hdr_from_dst = 0, hipEvent_t stop = nullptr,
+                               bool host_arena = false) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
             return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
@@ -772,7 +777,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         if (err == hipSuccess && sp.last != s) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
         if (err == hipSuccess) {
-            if (mixed_split())
+            if (!host_arena && mixed_split())
                 err = neb_gcm_batch_split(open, d_desc, n, d_n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                           sp.ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
                                           sp.ws.sums, e->cu_count, s, hdr_from_dst);
@@ -947,7 +952,7 @@ int neb_launch_on(neb_engine* e, int alg, int open, const neb_desc* desc, uint32
     if (n == 0) return NEB_OK;
     DeviceGuard dg(e->device);
     hipError_t err = launch_batch(e, alg, open, desc, n, arena, status, key_hint, s, nullptr,
-                                  static_cast<SchedSpace*>(sched));
+                                  static_cast<SchedSpace*>(sched), 0, nullptr, true);
     if (err != hipSuccess) {
         set_error("queue batch launch", err);
         return NEB_ERR_HIP;
@@ -994,7 +999,8 @@ static int batch_host_zero_copy(neb_engine* e, int alg, int open, const neb_desc
         d_desc = e->zc_desc;
     }
     if (!status_mapped) d_status = e->zc_status;
-    HIP_TRY(launch_batch(e, alg, open, d_desc, n, arena, d_status, key_hint, e->stream));
+    HIP_TRY(launch_batch(e, alg, open, d_desc, n, arena, d_status, key_hint, e->stream, nullptr, nullptr, 0, nullptr,
+                         true));
     if (!status_mapped)
         HIP_TRY(hipMemcpyAsync(status, d_status, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1163,7 +1169,7 @@ int neb_rx_pipe_submit(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena
     HIP_TRY(hipMemcpyAsync(r.d_desc + c0, r.h_desc + c0, (size_t)cnt * sizeof(neb_desc), hipMemcpyHostToDevice,
                            sl.stream));
     HIP_TRY(launch_batch(e, alg, 1, r.d_desc + c0, cnt, arena, r.d_status + c0, key_hint, sl.stream, nullptr,
-                         sl.sched));
+                         sl.sched, 0, nullptr, true));
     HIP_TRY(hipMemcpyAsync(r.h_status + c0, r.d_status + c0, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost,
                            sl.stream));
     HIP_TRY(hipEventRecord(sl.ev, sl.stream));
