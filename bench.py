@@ -258,12 +258,14 @@ def main():
     if args.mode == "relay":
         return bench_relay(args, ctrl, rank, world, device)
     b = W.make_batch(*{
+        0: (L.ALG_AESGCM, 1024, 1),
         1: (L.ALG_AESGCM, 65536, 1),
         2: (L.ALG_AESGCM, 65536, 4096),
         3: (L.ALG_CHACHAPOLY, 65536, 4096),
-    }[cfg], seed=W.SEED ^ rank, name=f"C{cfg + 1}") if cfg in (1, 2, 3) else \
+    }[cfg], seed=W.SEED ^ rank, name=f"C{cfg + 1}") if cfg in (0, 1, 2, 3) else \
         W.shard(W.config(4), rank, world)
-    workload_name = {1: "C2 AES-256-GCM, 1 tunnel key, 65536 x 1300 B packets, device-resident",
+    workload_name = {0: "C1 AES-256-GCM, 1 tunnel key, 1024 x 1300 B packets, device-resident",
+                     1: "C2 AES-256-GCM, 1 tunnel key, 65536 x 1300 B packets, device-resident",
                      2: "C3 AES-256-GCM, 4096 tunnel keys, 65536 x 1300 B packets, device-resident",
                      3: "C4 ChaCha20-Poly1305, 4096 tunnel keys, 65536 x 1300 B packets, device-resident",
                      4: "C5 AES-256-GCM, 4096 tunnel keys, IMIX 90/576/1300 (7:4:1), 1 Mi packets sharded"}[cfg]
@@ -364,8 +366,14 @@ def main():
     value = total_payload / dt / GIB
     achieved = alg_bytes / (seal_ms * 1e-3) / 1e9  # GB/s, seal kernel
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
-    kern_tag = ("gcm_single_kernel<false, false>" if b.nkeys == 1 else "gcm_chunk_kernel<false>") if b.alg == 1 \
-        else "chacha_batch_kernel<false>"
+    fused = os.environ.get("NEB_MIXED_FUSED") == "1"
+    if b.alg != L.ALG_AESGCM:
+        kern_tag = "chacha_batch_kernel<false>"
+    elif b.nkeys == 1:
+        kern_tag = "gcm_single_tail_kernel<false>" if b.n <= 6144 else "gcm_single_kernel<false, false>"
+    else:
+        kern_tag = "gcm_chunk_kernel<false>" if fused else \
+            "sched passes + gcm_ctr_kernel<false, true> + gcm_ghash_kernel<false> (the whole seal call)"
     pmc = pmc_config(f"C{cfg + 1}")
     lens = b.desc["len"].astype(np.int64)
     out = {

@@ -1239,6 +1239,7 @@ struct ChunkArgs {
     const uint4* chunks;
     uint32_t* counters;  // the scheduler's counters (sched.hpp kCnt*)
     uint32_t max_chunks, max_short;
+    uint32_t umax;  // the GHASH pass's largest aggregation (1..3; NEB_GH_UMAX, A/B)
 };
 
 // Chunk order: the chunks of each kind come longest first (size class). Workgroup w owns chunks w,
@@ -1718,8 +1719,10 @@ __global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmAr
             for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
                 const uint32_t q = g0 + (ln >> 2);
                 const bool valid = q < count;
-                if (cls >= 3u) ghash_packet_group<OPEN, 3>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
-                else if (cls >= 1u) ghash_packet_group<OPEN, 2>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
+                if (cls >= 3u && ca.umax >= 3u)
+                    ghash_packet_group<OPEN, 3>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
+                else if (cls >= 1u && ca.umax >= 2u)
+                    ghash_packet_group<OPEN, 2>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
                 else ghash_packet_group<OPEN, 1>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
             }
         } else {
@@ -2078,7 +2081,7 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
-    neb::ChunkArgs ca{d_sorted, nullptr, d_chunks, d_counters, max_chunks, max_short};
+    neb::ChunkArgs ca{d_sorted, nullptr, d_chunks, d_counters, max_chunks, max_short, 1u};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
     // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.
@@ -2121,7 +2124,12 @@ extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint
                                           uint32_t max_short, uint4* d_sums, int cu_count, hipStream_t s,
                                           int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
-    neb::ChunkArgs ca{d_sorted, d_sdesc, d_chunks, d_counters, max_chunks, max_short};
+    static const uint32_t umax = [] {
+        const char* v = std::getenv("NEB_GH_UMAX");
+        const int u = v ? std::atoi(v) : 3;
+        return (uint32_t)(u < 1 ? 1 : u > 3 ? 3 : u);
+    }();
+    neb::ChunkArgs ca{d_sorted, d_sdesc, d_chunks, d_counters, max_chunks, max_short, umax};
     return open ? launch_split<true>(a, ca, max_chunks, d_sums, cu_count, s)
                 : launch_split<false>(a, ca, max_chunks, d_sums, cu_count, s);
 }
