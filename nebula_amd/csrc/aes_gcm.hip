@@ -904,14 +904,17 @@ __device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uin
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
+// sdesc (optional): the packet's descriptor in the scheduler's sorted copy (one contiguous read per
+// chunk instead of a gather behind the index load).
 template <bool OPEN, bool CS = false, class GH, class TL>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
-                                                 uint32_t lane, uint32_t lg, const uint4* cs_pow = nullptr) {
+                                                 uint32_t lane, uint32_t lg, const uint4* cs_pow = nullptr,
+                                                 const neb_desc* sdesc = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
-    if (valid) d = args.desc[p];
+    if (valid) d = sdesc ? *sdesc : args.desc[p];
     uint32_t st = NEB_STATUS_OK;
     if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
     if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
@@ -1321,7 +1324,8 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                 const uint32_t q = g0 + (ln >> 2);
                 const bool valid = q < count;
                 const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-                gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
+                gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u, nullptr,
+                                       ca.sdesc + start + q);
             }
         } else {
             const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
@@ -1333,7 +1337,8 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             const bool valid = q < count;
             const uint32_t p = valid ? ca.sorted[start + q] : 0u;
             const GhChunkTree gh{wtab, wpos};
-            gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg);
+            gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg, nullptr,
+                                   ca.sdesc + start + q);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
@@ -2077,11 +2082,11 @@ extern "C" NEB_API int neb_debug_wave_trace(void* out, uint32_t max) {
 
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
-                                            const uint32_t* d_sorted, const uint4* d_chunks,
+                                            const uint32_t* d_sorted, const neb_desc* d_sdesc, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
-    neb::ChunkArgs ca{d_sorted, nullptr, d_chunks, d_counters, max_chunks, max_short, 1u};
+    neb::ChunkArgs ca{d_sorted, d_sdesc, d_chunks, d_counters, max_chunks, max_short, 1u};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
     // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.

@@ -37,7 +37,7 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
                                            int hdr_from_dst, hipEvent_t stop);
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
-                                            const uint32_t* d_sorted, const uint4* d_chunks,
+                                            const uint32_t* d_sorted, const neb_desc* d_sdesc, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst);
 extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
@@ -783,7 +783,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
                                           sp.ws.sums, e->cu_count, s, hdr_from_dst);
             else
                 err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                            sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
+                                            sp.ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
                                             e->cu_count, s, hdr_from_dst);
         }
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);
