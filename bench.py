@@ -366,13 +366,13 @@ def main():
     value = total_payload / dt / GIB
     achieved = alg_bytes / (seal_ms * 1e-3) / 1e9  # GB/s, seal kernel
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
-    fused = os.environ.get("NEB_MIXED_FUSED") == "1"
+    fused = os.environ.get("NEB_MIXED_SPLIT") != "1"
     if b.alg != L.ALG_AESGCM:
         kern_tag = "chacha_batch_kernel<false>"
     elif b.nkeys == 1:
         kern_tag = "gcm_single_tail_kernel<false>" if b.n <= 6144 else "gcm_single_kernel<false, false>"
     else:
-        kern_tag = "gcm_chunk_kernel<false>" if fused else \
+        kern_tag = "sched passes + gcm_chunk_kernel<false> (the whole seal call)" if fused else \
             "sched passes + gcm_ctr_kernel<false, true> + gcm_ghash_kernel<false> (the whole seal call)"
     pmc = pmc_config(f"C{cfg + 1}")
     lens = b.desc["len"].astype(np.int64)

@@ -1325,7 +1325,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                 const bool valid = q < count;
                 const uint32_t p = valid ? ca.sorted[start + q] : 0u;
                 gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u, nullptr,
-                                       ca.sdesc + start + q);
+                                       ca.sdesc ? ca.sdesc + start + q : nullptr);
             }
         } else {
             const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
@@ -1338,7 +1338,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             const uint32_t p = valid ? ca.sorted[start + q] : 0u;
             const GhChunkTree gh{wtab, wpos};
             gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg, nullptr,
-                                   ca.sdesc + start + q);
+                                   ca.sdesc ? ca.sdesc + start + q : nullptr);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();

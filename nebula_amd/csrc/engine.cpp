@@ -748,11 +748,17 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     return hipSuccess;
 }
 
-// Mixed-key AES-GCM: the CTR + GHASH passes (aes_gcm.hip gcm_ctr_kernel / gcm_ghash_kernel), or with
-// NEB_MIXED_FUSED=1 (read per batch) round 3's fused chunk kernel, kept for A/B comparison.
+// Mixed-key AES-GCM runs the fused chunk kernel (aes_gcm.hip gcm_chunk_kernel); NEB_MIXED_SPLIT=1 (read
+// per batch) runs the two-pass form instead (gcm_ctr_kernel + gcm_ghash_kernel, DESIGN.md §3.2: measured
+// slower on C3 and C5). NEB_SCHED_SDESC=1: the fused kernel reads the scheduler's sorted descriptor
+// copy (the split passes always do).
 static bool mixed_split() {
-    const char* v = std::getenv("NEB_MIXED_FUSED");
-    return !(v && v[0] == '1');
+    const char* v = std::getenv("NEB_MIXED_SPLIT");
+    return v && v[0] == '1';
+}
+static bool sched_sdesc() {
+    const char* v = std::getenv("NEB_SCHED_SDESC");
+    return v && v[0] == '1';
 }
 
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
@@ -775,15 +781,18 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         std::lock_guard<std::mutex> g(sp.mu);
         hipError_t err = sched_reserve(e, sp, n, s);
         if (err == hipSuccess && sp.last != s) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
-        if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &sp.ws, s);
+        const bool split = !host_arena && mixed_split();
+        neb::SchedWs ws = sp.ws;
+        if (!split && !sched_sdesc()) ws.sdesc = nullptr;
+        if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &ws, s);
         if (err == hipSuccess) {
-            if (!host_arena && mixed_split())
+            if (split)
                 err = neb_gcm_batch_split(open, d_desc, n, d_n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                           sp.ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
                                           sp.ws.sums, e->cu_count, s, hdr_from_dst);
             else
                 err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                            sp.ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
+                                            ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
                                             e->cu_count, s, hdr_from_dst);
         }
         if (err == hipSuccess) err = hipEventRecord(sp.done, s);

@@ -110,7 +110,7 @@ __global__ void sched_scatter_kernel(const neb_desc* __restrict__ desc, uint32_t
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t j = ws.base[ws.binof[i]] + ws.binpos[i];
         ws.sorted[j] = i;
-        ws.sdesc[j] = desc[i];
+        if (ws.sdesc) ws.sdesc[j] = desc[i];
     }
 }
 

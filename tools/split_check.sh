@@ -6,17 +6,16 @@ OUT=$R/gpurun_out/split; mkdir -p $OUT
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -4 $OUT/pytest_gpu.log; [ $rc -gt 1 ] && exit $rc
-for v in split u1 lane fused; do
-  unset NEB_MIXED_FUSED NEB_CTR_RK NEB_GH_UMAX
-  [ $v = fused ] && export NEB_MIXED_FUSED=1
-  [ $v = lane ] && export NEB_CTR_RK=lane
-  [ $v = u1 ] && export NEB_GH_UMAX=1
+for v in ${VARIANTS:-fused sdesc split}; do
+  unset NEB_MIXED_SPLIT NEB_CTR_RK NEB_GH_UMAX NEB_SCHED_SDESC NEB_GH_OCC
+  [ $v = split ] && export NEB_MIXED_SPLIT=1
+  [ $v = sdesc ] && export NEB_SCHED_SDESC=1
   for c in 2 4; do
     timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_${v}_c$c.json 2> $OUT/bench_${v}_c$c.err || exit $?
     echo "$v C$((c+1)): $(grep -o '"value": [0-9.]*' $OUT/bench_${v}_c$c.json) $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_${v}_c$c.json)"
   done
 done
-unset NEB_MIXED_FUSED NEB_CTR_RK NEB_GH_UMAX
+unset NEB_MIXED_SPLIT NEB_CTR_RK NEB_GH_UMAX NEB_SCHED_SDESC NEB_GH_OCC
 cd /tmp && export TMPDIR=/tmp && cd $R
 for c in 2 4; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_c$c -o run -- python bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline > $OUT/trace_c$c.log 2>&1 || exit $?
