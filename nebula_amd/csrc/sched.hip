@@ -2,6 +2,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "sched.hpp"
@@ -18,6 +20,9 @@ __device__ __forceinline__ uint32_t size_class(const neb_desc& d, uint32_t lpp) 
 // pass 1: histogram of (size class, key) bins; keys outside the table go to key index max_keys.
 // The returning add also ranks the packet inside its bin, so pass 3 needs no atomics: the adds
 // execute at the memory side (MI355X_MICROARCH.md, global atomics), ≈55 µs per 1 Mi packets each.
+// SUB: sub-bins per bin for this batch (kSubBins for large batches, 1 for small ones: the contention
+// the sub-bins spread is a large batch's, and pass 2 reads SUB words per bin)
+template <uint32_t SUB>
 __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn,
                                   uint32_t max_keys, uint32_t lpp, SchedWs ws) {
     // the cursors are cleared here (the previous batch's crypto kernel has finished with them);
@@ -28,7 +33,7 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const neb_desc d = desc[i];
         const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
-        const uint32_t b = (size_class(d, lpp) * (max_keys + 1u) + key) * kSubBins + (blockIdx.x & (kSubBins - 1u));
+        const uint32_t b = (size_class(d, lpp) * (max_keys + 1u) + key) * SUB + (blockIdx.x & (SUB - 1u));
         ws.binof[i] = b;
         ws.binpos[i] = atomicAdd(&ws.hist[b], 1u);
     }
@@ -38,21 +43,22 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
 // aggregated per workgroup (block scans, then one atomic per counter and workgroup): one atomic per
 // bin put ~4096 returning atomics on a single word for a 4096-tunnel batch.
 constexpr int kAllocThreads = 256;
+template <uint32_t SUB>
 __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
     using Scan = hipcub::BlockScan<uint32_t, kAllocThreads>;
     __shared__ typename Scan::TempStorage tmp;
     __shared__ uint32_t wg_base[4];
     const uint32_t nb = sched_nbins(max_keys);
     const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
-    uint32_t sc[kSubBins], c = 0;
+    uint32_t sc[SUB], c = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < kSubBins; j++) {
-        sc[j] = b < nb ? ws.hist[b * kSubBins + j] : 0u;
+    for (uint32_t j = 0; j < SUB; j++) {
+        sc[j] = b < nb ? ws.hist[b * SUB + j] : 0u;
         c += sc[j];
     }
     if (c)  // clear for the next batch
 #pragma unroll
-        for (uint32_t j = 0; j < kSubBins; j++) ws.hist[b * kSubBins + j] = 0u;
+        for (uint32_t j = 0; j < SUB; j++) ws.hist[b * SUB + j] = 0u;
     const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
     const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
     const uint32_t lg = tail ? sched_tail_lg(tail, cls) : 2u;
@@ -85,8 +91,8 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t base = wg_base[0] + off_p;
     uint32_t sb = base;
 #pragma unroll
-    for (uint32_t j = 0; j < kSubBins; j++) {
-        ws.base[b * kSubBins + j] = sb;
+    for (uint32_t j = 0; j < SUB; j++) {
+        ws.base[b * SUB + j] = sb;
         sb += sc[j];
     }
     const uint32_t cf = wg_base[1] + off_f;
@@ -141,9 +147,19 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     const uint32_t nb = neb::sched_nbins(max_keys);
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
-    hipLaunchKernelGGL(neb::sched_hist_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp, *ws);
-    hipLaunchKernelGGL(neb::sched_alloc_kernel, dim3((nb + neb::kAllocThreads - 1) / neb::kAllocThreads),
-                       dim3(neb::kAllocThreads), 0, s, max_keys, *ws);
+    const dim3 ga((nb + neb::kAllocThreads - 1) / neb::kAllocThreads), ta(neb::kAllocThreads);
+    static const uint32_t from = [] {  // NEB_SUB_BINS_FROM=<packets> (read once): the A/B of the threshold
+        const char* v = std::getenv("NEB_SUB_BINS_FROM");
+        return v ? (uint32_t)std::strtoul(v, nullptr, 10) : neb::kSubBinsFrom;
+    }();
+    if (n >= from) {
+        hipLaunchKernelGGL(neb::sched_hist_kernel<neb::kSubBins>, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp,
+                           *ws);
+        hipLaunchKernelGGL(neb::sched_alloc_kernel<neb::kSubBins>, ga, ta, 0, s, max_keys, *ws);
+    } else {
+        hipLaunchKernelGGL(neb::sched_hist_kernel<1>, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp, *ws);
+        hipLaunchKernelGGL(neb::sched_alloc_kernel<1>, ga, ta, 0, s, max_keys, *ws);
+    }
     hipLaunchKernelGGL(neb::sched_scatter_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, *ws);
     return hipGetLastError();
 }

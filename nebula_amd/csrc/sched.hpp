@@ -52,6 +52,12 @@ constexpr uint32_t kSchedCounters = 4;
 #define NEB_SUB_BINS 8
 #endif
 constexpr uint32_t kSubBins = NEB_SUB_BINS;
+// batches of at least this many packets (the host's bound) count in kSubBins sub-bins, smaller ones in
+// one: C3's 64 Ki packets put ≈ 16 adds on each of 4096 bins, and pass 2 then reads 1/8 of the words
+#ifndef NEB_SUB_BINS_FROM
+#define NEB_SUB_BINS_FROM (1u << 18)
+#endif
+constexpr uint32_t kSubBinsFrom = NEB_SUB_BINS_FROM;
 static_assert(kSubBins == 1 || kSubBins == 2 || kSubBins == 4 || kSubBins == 8, "sub-bins: a power of two <= 8");
 
 struct SchedWs {          // device workspace, sized for n packets and nbins bins

@@ -7,7 +7,8 @@ cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -4 $OUT/pytest_gpu.log; [ $rc -gt 1 ] && exit $rc
 for v in ${VARIANTS:-fused sdesc split}; do
-  unset NEB_MIXED_SPLIT NEB_CTR_RK NEB_GH_UMAX NEB_SCHED_SDESC NEB_GH_OCC
+  unset NEB_MIXED_SPLIT NEB_CTR_RK NEB_GH_UMAX NEB_SCHED_SDESC NEB_GH_OCC NEB_SUB_BINS_FROM
+  [ $v = sub8 ] && export NEB_SUB_BINS_FROM=0
   [ $v = split ] && export NEB_MIXED_SPLIT=1
   [ $v = sdesc ] && export NEB_SCHED_SDESC=1
   for c in 2 4; do
