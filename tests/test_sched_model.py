@@ -18,9 +18,9 @@ import sched_model as M  # noqa: E402
 from nebula_amd import workload as W  # noqa: E402
 
 
-def _check(key_id, aad_len, length, max_keys):
+def _check(key_id, aad_len, length, max_keys, split_cls=M.SPLIT_TAIL_CLASS):
     n = len(key_id)
-    chunks = M.plan(key_id, aad_len, length, max_keys)
+    chunks = M.plan(key_id, aad_len, length, max_keys, split_cls)
     seen = np.concatenate([c.packets for c in chunks]) if chunks else np.zeros(0, np.int64)
     assert np.array_equal(np.sort(seen), np.arange(n)), "every packet in exactly one chunk"
     cls = M.size_class(aad_len, length)
@@ -56,15 +56,17 @@ def test_baseline_mixed_configs(idx):
     aad = np.full(n, 16, np.uint32)
     chunks, nblk = _check(kid, aad, lens, 4096)
     if idx == 2:
-        # C3: Poisson(16) packets per key; with the 8/16-lane tails 86.7% of the lane-rounds carry
-        # a block (DESIGN.md §3.2 "Wave utilisation")
+        # C3: Poisson(16) packets per key; with the 8/16-lane tails and the split 9-12 packet tails
+        # 89.4% of the lane-rounds carry a block (86.7% without the split)
         used = int(nblk.sum())
         spent = sum(M.lane_rounds(c, nblk) for c in chunks)
-        assert abs(used / spent - 0.867) < 0.005
+        assert abs(used / spent - 0.894) < 0.005
+        base, _ = _check(kid, aad, lens, 4096, split_cls=99)
+        assert abs(used / sum(M.lane_rounds(c, nblk) for c in base) - 0.867) < 0.005
         fronts = sum(c.kind == "front" for c in chunks)
         tails = len(chunks) - fronts
-        # ≈ 16 fronts and 7 tails per workgroup on 256 CUs (the wave timeline)
-        assert 15 <= fronts / 256 <= 16.5 and 6 <= tails / 256 <= 8
+        # ≈ 13 fronts and 13 tails per workgroup on 256 CUs (16 and 7 without the split)
+        assert 12 <= fronts / 256 <= 14 and 12 <= tails / 256 <= 14
 
 
 def test_random_batches():
@@ -79,13 +81,19 @@ def test_random_batches():
 
 
 def test_bin_tail_shapes():
-    """One bin of c packets, c = 1..40: c // 16 full groups, then a 9-15 packet tail as a partial
-    4-lane group, a 5-8 packet tail at 8 lanes, a 1-4 packet tail at 16 (1300-B packets)."""
+    """One bin of c packets, c = 1..40: c // 16 full groups, then a 13-15 packet tail as a partial
+    4-lane group, a 9-12 packet tail as 8 packets at 8 lanes and the rest at 16, a 5-8 packet tail
+    at 8 lanes, a 1-4 packet tail at 16 (1300-B packets)."""
     for c in range(1, 41):
         kid = np.zeros(c, np.uint32)
         chunks, _ = _check(kid, np.full(c, 16, np.uint32), np.full(c, 1300, np.uint32), 4)
         t = c % 16
         front = [len(x.packets) for x in chunks if x.kind == "front"]
         back = [(len(x.packets), x.lg) for x in chunks if x.kind != "front"]
-        assert sum(front) == c // 16 * 16 + (t if t >= 9 else 0)
-        assert back == ([] if t == 0 or t >= 9 else [(t, 4 if t <= 4 else 3)])
+        assert sum(front) == c // 16 * 16 + (t if t >= 13 else 0)
+        if t == 0 or t >= 13:
+            assert back == []
+        elif t >= 9:
+            assert back == [(8, 3), (t - 8, 4)]
+        else:
+            assert back == [(t, 4 if t <= 4 else 3)]

@@ -30,6 +30,9 @@ def tail_lg(count: int, cls: int) -> int:
     return min(fit, size)
 
 
+SPLIT_TAIL_CLASS = 4  # kSplitTailClass: a 9-12 packet tail = 8 packets at 8 lanes + the rest at 16
+
+
 def groups(cls: int) -> int:
     """sched_groups: groups of 16 packets per front chunk."""
     return 1 if cls >= 3 else 8 >> cls
@@ -61,7 +64,8 @@ class Chunk:
     lg: int            # lanes per packet = 2**lg
 
 
-def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: int) -> List[Chunk]:
+def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: int,
+         split_cls: int = SPLIT_TAIL_CLASS) -> List[Chunk]:
     """The chunks sched_alloc_kernel writes for one batch (every bin, its front chunks and tail)."""
     key = np.where(key_id < max_keys, key_id, max_keys).astype(np.int64)
     cls = size_class(aad_len, length)
@@ -79,11 +83,15 @@ def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: 
         cnt = int(e - s)
         nfull, tail = divmod(cnt, CHUNK_PKTS)
         lg = tail_lg(tail, c) if tail else 2
-        fpk = nfull * CHUNK_PKTS + (tail if tail and lg == 2 else 0)
+        split = lg == 2 and 9 <= tail <= 12 and c >= split_cls
+        fpk = nfull * CHUNK_PKTS + (tail if tail and lg == 2 and not split else 0)
         cpk = groups(c) * CHUNK_PKTS
         for j in range(0, fpk, cpk):
             out.append(Chunk("front", order[s + j:s + min(fpk, j + cpk)], k, c, 2))
-        if tail and lg != 2:
+        if split:
+            out.append(Chunk("long" if tail_long(c, 3) else "short", order[s + fpk:s + fpk + 8], k, c, 3))
+            out.append(Chunk("long" if tail_long(c, 4) else "short", order[s + fpk + 8:e], k, c, 4))
+        elif tail and lg != 2:
             out.append(Chunk("long" if tail_long(c, lg) else "short", order[s + fpk:e], k, c, lg))
     return out
 
