@@ -74,19 +74,11 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t fpk = nfull * kChunkPkts + (tail && lg == 2u && !split ? tail : 0u);
     const uint32_t cpk = sched_groups(cls) * kChunkPkts;  // packets per front chunk
     const uint32_t nfront = (fpk + cpk - 1u) / cpk;
-    // back chunks: one tail at 8 or 16 lanes, or a split tail's two (8 lanes, then 16)
-    uint4 bk[2];
-    uint32_t nback = 0;
-    if (split) {
-        bk[0] = make_uint4(fpk, 8u, key, cls | (3u << kChunkLgShift));
-        bk[1] = make_uint4(fpk + 8u, tail - 8u, key, cls | (4u << kChunkLgShift));
-        nback = 2;
-    } else if (tail && lg != 2u) {
-        bk[0] = make_uint4(fpk, tail, key, cls | (lg << kChunkLgShift));
-        nback = 1;
-    }
-    uint32_t nlong = 0;
-    for (uint32_t j = 0; j < nback; j++) nlong += sched_tail_long(cls, bk[j].w >> kChunkLgShift) ? 1u : 0u;
+    // back chunks: one tail at 8 or 16 lanes (lg0), or a split tail's two (8 lanes, then 16)
+    const uint32_t nback = split ? 2u : (tail && lg != 2u ? 1u : 0u);
+    const uint32_t lg0 = split ? 3u : lg, cnt0 = split ? 8u : tail;
+    const bool long0 = nback && sched_tail_long(cls, lg0), long1 = split && sched_tail_long(cls, 4u);
+    const uint32_t nlong = (long0 ? 1u : 0u) + (long1 ? 1u : 0u);
     const uint32_t nshort = nback - nlong;
     uint32_t off_p, off_f, off_l, off_s, tot_p, tot_f, tot_l, tot_s;
     Scan(tmp).ExclusiveSum(c, off_p, tot_p);
@@ -114,16 +106,22 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t cf = wg_base[1] + off_f;
     for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
         ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));
-    uint32_t tl = wg_base[2] + off_l, ts = wg_base[3] + off_s;
-    for (uint32_t j = 0; j < nback; j++) {
-        uint4 ch = bk[j];
-        ch.x += base;
-        if (sched_tail_long(cls, ch.w >> kChunkLgShift)) {
+    const uint32_t tl = wg_base[2] + off_l, ts = wg_base[3] + off_s;
+    if (nback) {
+        const uint4 ch = make_uint4(base + fpk, cnt0, key, cls | (lg0 << kChunkLgShift));
+        if (long0) {
             if (tl < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - tl] = ch;
-            tl++;
-        } else {
-            if (ts < ws.max_short) ws.chunks[ws.max_chunks + ts] = ch;
-            ts++;
+        } else if (ts < ws.max_short) {
+            ws.chunks[ws.max_chunks + ts] = ch;
+        }
+    }
+    if (split) {  // the second tail: after the first in its list
+        const uint4 ch = make_uint4(base + fpk + 8u, tail - 8u, key, cls | (4u << kChunkLgShift));
+        const uint32_t tl1 = tl + (long0 ? 1u : 0u), ts1 = ts + (long0 ? 0u : 1u);
+        if (long1) {
+            if (tl1 < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - tl1] = ch;
+        } else if (ts1 < ws.max_short) {
+            ws.chunks[ws.max_chunks + ts1] = ch;
         }
     }
 }
