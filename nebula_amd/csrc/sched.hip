@@ -43,11 +43,8 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
 // aggregated per workgroup (block scans, then one atomic per counter and workgroup): one atomic per
 // bin put ~4096 returning atomics on a single word for a 4096-tunnel batch.
 constexpr int kAllocThreads = 256;
-// split_cls: from this size class up, a 9-12 packet tail runs as 8 packets at 8 lanes plus the rest at
-// 16 lanes (about 3/4 of the rounds of a partial 4-lane group: C3 0.867 -> 0.894 of the lane-rounds
-// busy); 0xFFFFFFFF: never (NEB_SPLIT_TAILS=0)
 template <uint32_t SUB>
-__global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws, uint32_t split_cls) {
+__global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
     using Scan = hipcub::BlockScan<uint32_t, kAllocThreads>;
     __shared__ typename Scan::TempStorage tmp;
     __shared__ uint32_t wg_base[4];
@@ -70,16 +67,12 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     // one back chunk. The crypto kernels take the front chunks, then the back ones. Front <= n/16 +
     // bins, back <= bins and front + back <= n/16 + min(n, bins): the ranges never meet inside
     // max_chunks (sched_max_chunks).
-    const bool split = lg == 2u && tail >= 9u && tail <= 12u && cls >= split_cls;
-    const uint32_t fpk = nfull * kChunkPkts + (tail && lg == 2u && !split ? tail : 0u);
+    const uint32_t fpk = nfull * kChunkPkts + (tail && lg == 2u ? tail : 0u);
     const uint32_t cpk = sched_groups(cls) * kChunkPkts;  // packets per front chunk
     const uint32_t nfront = (fpk + cpk - 1u) / cpk;
-    // back chunks: one tail at 8 or 16 lanes (lg0), or a split tail's two (8 lanes, then 16)
-    const uint32_t nback = split ? 2u : (tail && lg != 2u ? 1u : 0u);
-    const uint32_t lg0 = split ? 3u : lg, cnt0 = split ? 8u : tail;
-    const bool long0 = nback && sched_tail_long(cls, lg0), long1 = split && sched_tail_long(cls, 4u);
-    const uint32_t nlong = (long0 ? 1u : 0u) + (long1 ? 1u : 0u);
-    const uint32_t nshort = nback - nlong;
+    const bool back = tail && lg != 2u;
+    const bool is_long = back && sched_tail_long(cls, lg);
+    const uint32_t nlong = is_long ? 1u : 0u, nshort = back && !is_long ? 1u : 0u;
     uint32_t off_p, off_f, off_l, off_s, tot_p, tot_f, tot_l, tot_s;
     Scan(tmp).ExclusiveSum(c, off_p, tot_p);
     __syncthreads();
@@ -106,22 +99,13 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     const uint32_t cf = wg_base[1] + off_f;
     for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
         ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));
-    const uint32_t tl = wg_base[2] + off_l, ts = wg_base[3] + off_s;
-    if (nback) {
-        const uint4 ch = make_uint4(base + fpk, cnt0, key, cls | (lg0 << kChunkLgShift));
-        if (long0) {
+    if (back) {
+        const uint4 ch = make_uint4(base + fpk, tail, key, cls | (lg << kChunkLgShift));
+        const uint32_t tl = wg_base[2] + off_l, ts = wg_base[3] + off_s;
+        if (is_long) {
             if (tl < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - tl] = ch;
         } else if (ts < ws.max_short) {
             ws.chunks[ws.max_chunks + ts] = ch;
-        }
-    }
-    if (split) {  // the second tail: after the first in its list
-        const uint4 ch = make_uint4(base + fpk + 8u, tail - 8u, key, cls | (4u << kChunkLgShift));
-        const uint32_t tl1 = tl + (long0 ? 1u : 0u), ts1 = ts + (long0 ? 0u : 1u);
-        if (long1) {
-            if (tl1 < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - tl1] = ch;
-        } else if (ts1 < ws.max_short) {
-            ws.chunks[ws.max_chunks + ts1] = ch;
         }
     }
 }
@@ -164,10 +148,6 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
     const dim3 ga((nb + neb::kAllocThreads - 1) / neb::kAllocThreads), ta(neb::kAllocThreads);
-    static const uint32_t split_cls = [] {  // NEB_SPLIT_TAILS=0: the A/B without split tails
-        const char* v = std::getenv("NEB_SPLIT_TAILS");
-        return v && v[0] == '0' ? 0xFFFFFFFFu : neb::kSplitTailClass;
-    }();
     static const uint32_t from = [] {  // NEB_SUB_BINS_FROM=<packets> (read once): the A/B of the threshold
         const char* v = std::getenv("NEB_SUB_BINS_FROM");
         return v ? (uint32_t)std::strtoul(v, nullptr, 10) : neb::kSubBinsFrom;
@@ -175,10 +155,10 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     if (n >= from) {
         hipLaunchKernelGGL(neb::sched_hist_kernel<neb::kSubBins>, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp,
                            *ws);
-        hipLaunchKernelGGL(neb::sched_alloc_kernel<neb::kSubBins>, ga, ta, 0, s, max_keys, *ws, split_cls);
+        hipLaunchKernelGGL(neb::sched_alloc_kernel<neb::kSubBins>, ga, ta, 0, s, max_keys, *ws);
     } else {
         hipLaunchKernelGGL(neb::sched_hist_kernel<1>, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp, *ws);
-        hipLaunchKernelGGL(neb::sched_alloc_kernel<1>, ga, ta, 0, s, max_keys, *ws, split_cls);
+        hipLaunchKernelGGL(neb::sched_alloc_kernel<1>, ga, ta, 0, s, max_keys, *ws);
     }
     hipLaunchKernelGGL(neb::sched_scatter_kernel, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, *ws);
     return hipGetLastError();

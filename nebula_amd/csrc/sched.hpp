@@ -33,9 +33,6 @@ __host__ __device__ inline uint32_t sched_tail_lg(uint32_t count, uint32_t cls) 
     const uint32_t size = cls == 0u ? 2u : (cls == 1u ? 3u : 4u);
     return fit < size ? fit : size;
 }
-// from this size class up (9-16 rounds at 4 lanes), a tail of 9-12 packets is split into 8 packets
-// at 8 lanes and the rest at 16 (R/2 + R/4 rounds instead of R); below it the split saves nothing
-constexpr uint32_t kSplitTailClass = 4;
 // groups of 16 packets per front chunk: about 8 rounds of work per chunk for the short classes
 __host__ __device__ inline uint32_t sched_groups(uint32_t cls) { return cls >= 3u ? 1u : 8u >> cls; }
 constexpr uint32_t kMaxChunkPkts = 8u * kChunkPkts;

@@ -30,7 +30,11 @@ def tail_lg(count: int, cls: int) -> int:
     return min(fit, size)
 
 
-SPLIT_TAIL_CLASS = 4  # kSplitTailClass: a 9-12 packet tail = 8 packets at 8 lanes + the rest at 16
+SPLIT_TAIL_CLASS = 99  # the product never splits a tail (sched.hip)
+# the round-4 experiment: from size class 4 a 9-12 packet tail = 8 packets at 8 lanes + the rest at
+# 16. More lane-rounds busy in this model (C3 0.867 -> 0.894), slower on the GPU (each extra chunk
+# pays its key staging and tree final: C3 469-472 -> 456-459 GiB/s, profiles/r4/split_tails.log)
+EXPERIMENT_SPLIT_CLASS = 4
 
 
 def groups(cls: int) -> int:
