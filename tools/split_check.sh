@@ -7,9 +7,9 @@ cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -4 $OUT/pytest_gpu.log; [ $rc -gt 1 ] && exit $rc
 setv() {
-  unset NEB_MIXED_SPLIT NEB_CTR_RK NEB_GH_UMAX NEB_SCHED_SDESC NEB_GH_OCC NEB_SUB_BINS_FROM NEB_SPLIT_TAILS
+  unset NEB_MIXED_SPLIT NEB_CTR_RK NEB_GH_UMAX NEB_SCHED_SDESC NEB_GH_OCC NEB_SUB_BINS_FROM NEB_SPLIT_TAILS NEB_PAIR_TAILS
   [ $1 = sub8 ] && export NEB_SUB_BINS_FROM=0
-  [ $1 = nosplit ] && export NEB_SPLIT_TAILS=0
+  [ $1 = pair0 ] && export NEB_PAIR_TAILS=0
   [ $1 = split ] && export NEB_MIXED_SPLIT=1
   [ $1 = sdesc ] && export NEB_SCHED_SDESC=1
   return 0
