@@ -1984,6 +1984,25 @@ static hipError_t launch_grid(K kern, int threads, uint32_t work_waves, int cu_c
     hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, args...);
     return hipGetLastError();
 }
+// the same with `stop` (optional) bound to the dispatch (hipExtLaunchKernel): the event completes
+// with the kernel, and no marker packet follows it on the stream
+template <class K, class... Extra>
+static hipError_t launch_grid_stop(K kern, int threads, uint32_t work_waves, int cu_count, hipStream_t s,
+                                   hipEvent_t stop, Extra... args) {
+    static const int per_cu = [&] {  // per instantiation: kernels of one signature share it (same bounds here)
+        int pc = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, threads, 0) != hipSuccess || pc < 1) pc = 1;
+        return pc;
+    }();
+    const uint32_t waves = (uint32_t)threads / 64u;
+    const uint32_t want = (work_waves + waves - 1) / waves;
+    const uint32_t cap = (uint32_t)(per_cu * cu_count);
+    const uint32_t grid = want < cap ? want : cap;
+    if (grid == 0) return stop ? hipEventRecord(stop, s) : hipSuccess;
+    if (stop) hipExtLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, nullptr, stop, 0, args...);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, args...);
+    return hipGetLastError();
+}
 
 // Waves of gcm_single_kernel's grid for a batch of at most n packets (a full pass is that many
 // groups of kPpw packets; the packets after the last full pass go to the tail kernel). The TX
@@ -2084,15 +2103,17 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const neb_desc* d_sdesc, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
-                                            int cu_count, hipStream_t s, int hdr_from_dst) {
+                                            int cu_count, hipStream_t s, int hdr_from_dst,
+                                            hipEvent_t stop) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
     neb::ChunkArgs ca{d_sorted, d_sdesc, d_chunks, d_counters, max_chunks, max_short, 1u};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
     // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.
     const uint32_t bound = max_chunks * (uint32_t)neb::kChunkWaves;
-    return open ? launch_grid(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, a, ca)
-                : launch_grid(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, a, ca);
+    // stop (optional): an event bound to the kernel's dispatch (no marker packet after it)
+    return open ? launch_grid_stop(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, stop, a, ca)
+                : launch_grid_stop(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, stop, a, ca);
 }
 
 // Mixed keys in two passes (gcm_ctr_kernel + gcm_ghash_kernel): seal CTR then GHASH, open GHASH then

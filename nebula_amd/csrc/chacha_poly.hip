@@ -16,6 +16,7 @@
 //    product across the lanes (the one-time key r is per packet).
 //  * Field arithmetic: 5 × 26-bit limbs, 64-bit partial products.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "../../include/nebula_aead.h"
@@ -406,7 +407,7 @@ extern "C" hipError_t neb_chacha_key_setup(const uint8_t* keys, const uint32_t* 
 }
 
 template <bool OPEN>
-static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStream_t s) {
+static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStream_t s, hipEvent_t stop) {
     auto kern = neb::chacha_batch_kernel<OPEN>;
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, neb::kChThreads, 0) != hipSuccess || per_cu < 1)
@@ -415,15 +416,17 @@ static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStrea
     uint32_t want = (groups + neb::kChWavesPerWG - 1) / neb::kChWavesPerWG;
     uint32_t cap = (uint32_t)(per_cu * cu_count);
     uint32_t grid = want < cap ? want : cap;
-    if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(neb::kChThreads), 0, s, a);
+    if (grid == 0) return stop ? hipEventRecord(stop, s) : hipSuccess;
+    // stop (optional): bound to the dispatch, so no marker packet follows the batch (hipExtLaunchKernel)
+    if (stop) hipExtLaunchKernelGGL(kern, dim3(grid), dim3(neb::kChThreads), 0, s, nullptr, stop, 0, a);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(neb::kChThreads), 0, s, a);
     return hipGetLastError();
 }
 
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                       int hdr_from_dst) {
+                                       int hdr_from_dst, hipEvent_t stop) {
     neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst};
-    return open ? launch_chacha<true>(a, cu_count, s) : launch_chacha<false>(a, cu_count, s);
+    return open ? launch_chacha<true>(a, cu_count, s, stop) : launch_chacha<false>(a, cu_count, s, stop);
 }

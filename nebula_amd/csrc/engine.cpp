@@ -39,7 +39,7 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const neb_desc* d_sdesc, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
-                                            int cu_count, hipStream_t s, int hdr_from_dst);
+                                            int cu_count, hipStream_t s, int hdr_from_dst, hipEvent_t stop);
 extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
                                           uint8_t* d_arena, const uint32_t* d_keys, uint32_t max_keys,
                                           int32_t* d_status, const uint32_t* d_sorted, const neb_desc* d_sdesc,
@@ -54,7 +54,7 @@ extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                       int hdr_from_dst);
+                                       int hdr_from_dst, hipEvent_t stop);
 
 // Device workspace of the mixed-key scheduler (sched.hpp). One per engine; a batch waits on the
 // previous user's event before reusing it, so batches on different streams never overlap in it.
@@ -756,6 +756,15 @@ static bool mixed_split() {
     const char* v = std::getenv("NEB_MIXED_SPLIT");
     return v && v[0] == '1';
 }
+// NEB_BIND_EVENTS=0 (read once): markers after each batch instead of events bound to its last
+// kernel's dispatch (the A/B of round 4's binding for mixed-key AES-GCM and ChaCha batches)
+static bool bind_events() {
+    static const bool on = [] {
+        const char* v = std::getenv("NEB_BIND_EVENTS");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
 static bool sched_sdesc() {
     const char* v = std::getenv("NEB_SCHED_SDESC");
     return v && v[0] == '1';
@@ -790,12 +799,12 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
                 err = neb_gcm_batch_split(open, d_desc, n, d_n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                           sp.ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
                                           sp.ws.sums, e->cu_count, s, hdr_from_dst);
-            else
+            else  // sp.done bound to the chunk kernel's dispatch: no marker packet between batches
                 err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                             ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
-                                            e->cu_count, s, hdr_from_dst);
+                                            e->cu_count, s, hdr_from_dst, bind_events() ? sp.done : nullptr);
         }
-        if (err == hipSuccess) err = hipEventRecord(sp.done, s);
+        if (err == hipSuccess && (split || !bind_events())) err = hipEventRecord(sp.done, s);
         if (err == hipSuccess) sp.last = s;
         if (err != hipSuccess) {
             // binning passes of this batch may already be queued on s: let them finish before the
@@ -806,7 +815,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         return err;
     }
     return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n, e->cu_count,
-                            s, hdr_from_dst);
+                            s, hdr_from_dst, stop);
 }
 
 // One packet through the device, on a slot of the engine's per-packet pool (PktPool): the packet is
@@ -902,20 +911,20 @@ static int batch_device(neb_engine* e, int alg, int open, const neb_desc* d_desc
     if (!d_desc || !d_arena || !d_status) return NEB_ERR_INVALID;
     DeviceGuard dg(e->device);
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream, as for any HIP launch
-    // a single-key AES-GCM batch binds its key-use event to its last kernel (no marker after it)
-    const bool bound = alg == NEB_ALG_AESGCM && key_hint != NEB_KEYS_MIXED;
-    hipEvent_t stop = bound ? use_event(e, key_hint, s) : nullptr;
+    // A batch binds its key-use event to its last kernel (no marker packet after it: each marker
+    // between two batches cost ≈ 5 µs, C3 +3.5-5%, profiles/r3_ab/use_events.log). A mixed-key
+    // AES-GCM batch runs through the engine's scheduler workspace, whose `done` event is bound to
+    // its chunk kernel the same way and orders every later user of the workspace after it;
+    // neb_cipher_destroy waits on that event, so it needs no key-use event of its own.
+    const bool sched = alg == NEB_ALG_AESGCM && key_hint == NEB_KEYS_MIXED;
+    const bool single_aes = alg == NEB_ALG_AESGCM && key_hint != NEB_KEYS_MIXED;  // bound since round 3
+    hipEvent_t stop = sched || !(single_aes || bind_events()) ? nullptr : use_event(e, key_hint, s);
     hipError_t err = launch_batch(e, alg, open, d_desc, n, d_arena, d_status, key_hint, s, nullptr, nullptr, 0, stop);
     if (err != hipSuccess) {
         set_error("batch launch", err);
         return NEB_ERR_HIP;
     }
-    if (bound && stop) return NEB_OK;
-    // A mixed-key AES-GCM batch ran through the engine's scheduler workspace, whose `done` event
-    // is recorded after it and orders every later user of the workspace after it:
-    // neb_cipher_destroy waits on that event, so the batch needs no marker of its own (each marker
-    // between two batches cost ≈ 5 µs, C3 +3.5-5%, profiles/r3_ab/use_events.log).
-    if (!(alg == NEB_ALG_AESGCM && key_hint == NEB_KEYS_MIXED)) note_use(e, key_hint, s);
+    if (!sched && !stop) note_use(e, key_hint, s);  // no event could be created: a marker
     return NEB_OK;
 }
 
