@@ -1190,6 +1190,61 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     }
 }
 
+// ---- one packet, its bytes in the kernel arguments (the per-packet CipherState calls) ---------
+// A per-packet call through the tail kernel spent ≈ 18.6 µs on the device for one packet, mostly
+// a chain of PCIe round trips to the caller's pinned staging: the descriptor, then each round's
+// payload block, then (open) the received tag. Here the host puts the descriptor, the AAD and the
+// payload (+ tag) into the kernel's argument block, which the runtime writes to device memory with
+// the dispatch, so the kernel reads nothing over PCIe; it writes the result and the status into
+// the caller's pinned staging (posted writes). One wave, 64 lanes per packet (2 rounds for 1300 B).
+constexpr uint32_t kOneBytes = 2048;  // AAD (padded to 16) + payload (+ tag): larger packets take the batch path
+struct OneArgs {
+    neb_desc d;           // offsets from `in`; dst_off reaches the host output (a wrapping 64-bit offset)
+    const uint32_t* keys;
+    uint32_t max_keys, key;
+    int32_t* status;      // host
+    uint32_t pad_[2];
+    uint8_t in[kOneBytes];  // 16-B aligned within the argument block
+};
+static_assert(offsetof(OneArgs, in) % 16 == 0, "the packet bytes are read as 16-B blocks");
+template <bool OPEN>
+__global__ __launch_bounds__(kWave) void gcm_one_kernel(OneArgs a) {
+    __shared__ TailLds lds;
+    const uint32_t lane = threadIdx.x;
+    // the argument block in place (a by-value struct indexed per lane would be copied to scratch)
+    // the block's address as an opaque integer: derived from the constant-address kernarg pointer,
+    // the output address (base + dst_off) would let the compiler treat the result stores as stores
+    // to constant memory and drop them
+    uint64_t kb = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kb));
+    const uint8_t* ka = reinterpret_cast<const uint8_t*>(kb);
+    const uint32_t key = a.key;
+    const uint32_t* srec = a.keys + (size_t)(key < a.max_keys ? key : 0u) * kKeyRecDwords;
+    // T-tables, 16 entries per lane at a time (loads before stores, as fill_ttab)
+    for (uint32_t j0 = 0; j0 < 256u * 32u; j0 += 16u * kWave) {
+        uint2 v[16];
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) v[j] = ttab_entry(j0 + j * kWave + lane);
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) lds.ttab[j0 + j * kWave + lane] = v[j];
+    }
+    for (uint32_t tdx = lane; tdx < 16u * kTailLg; tdx += kWave)  // M[v] of H^(2^j), j < kTailLg
+        lds.shoup[tdx] = ld_rec4(srec, rec_shoup_pow2(tdx >> 4) + 4u * (tdx & 15u));
+    for (uint32_t tdx = lane; tdx < 128u; tdx += kWave) lds.pos[tdx] = ld_rec4(srec, kRecPos64 + 4u * tdx);
+    uint32_t rks[60];
+    load_round_keys(srec, rks);
+    __syncthreads();
+    const TLook T{lds.ttab, ttab_lane_base(lane)};
+    const GhShoup gh{lds.shoup, lds.pos};
+    const bool key_ok = key < a.max_keys && __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
+    uint8_t* base = const_cast<uint8_t*>(ka + offsetof(OneArgs, in));
+    GcmArgs ga{nullptr, 1u, base, a.keys, a.max_keys, key, a.status, nullptr, 0u, 0u};
+    // the host passed the output's address in dst_off: rebase it on the argument block (wrapping)
+    neb_desc d = a.d;
+    d.dst_off = a.d.dst_off - (uint64_t)(uintptr_t)base;
+    gcm_packet_group<OPEN>(ga, 0u, true, key, key_ok, RkRegs{rks}, gh, T, lane, kTailLg, nullptr, &d);
+}
+
 // ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------
 
 
@@ -2098,6 +2153,37 @@ extern "C" NEB_API int neb_debug_wave_trace(void* out, uint32_t max) {
     return (int)n;
 }
 #endif
+
+// One packet (the per-packet path): aad[aad_len] and in[in_len] (payload, + tag when opening) go
+// in the kernel arguments; the kernel writes len payload bytes (+ the tag when sealing) to `out`
+// and the status to *status (pinned host memory, or device memory). hipErrorInvalidValue when the
+// packet does not fit kOneBytes (the caller takes the batch path).
+extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in, uint32_t in_len,
+                                  uint32_t len, uint64_t counter, uint8_t* out, int32_t* status, const uint32_t* d_keys,
+                                  uint32_t max_keys, uint32_t key, hipStream_t s) {
+    const uint32_t pay = (aad_len + 15u) & ~15u;
+    if ((uint64_t)pay + in_len > neb::kOneBytes) return hipErrorInvalidValue;
+    neb::OneArgs a;
+    std::memset(&a, 0, offsetof(neb::OneArgs, in));
+    if (aad_len) std::memcpy(a.in, aad, aad_len);
+    if (in_len) std::memcpy(a.in + pay, in, in_len);
+    a.d.aad_off = 0;
+    a.d.src_off = pay;
+    a.d.len = len;
+    a.d.aad_len = aad_len;
+    a.d.counter = counter;
+    a.d.key_id = key;
+    a.keys = d_keys;
+    a.max_keys = max_keys;
+    a.key = key;
+    a.status = status;
+    a.d.dst_off = (uint64_t)(uintptr_t)out;  // the output's address: the kernel rebases it on its argument block
+    if (open)
+        hipLaunchKernelGGL(neb::gcm_one_kernel<true>, dim3(1), dim3(neb::kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL(neb::gcm_one_kernel<false>, dim3(1), dim3(neb::kWave), 0, s, a);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,

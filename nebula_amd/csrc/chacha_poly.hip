@@ -16,6 +16,8 @@
 //    product across the lanes (the one-time key r is per packet).
 //  * Field arithmetic: 5 × 26-bit limbs, 64-bit partial products.
 #include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstring>
 #include <hip/hip_ext.h>
 #include <stdint.h>
 
@@ -238,25 +240,22 @@ struct ChachaArgs {
 // Payload and AAD blocks loaded one round ahead of their use (1) or in their round (0). Off: a
 // round ahead measured 2-3% slower on C4 (110.0 vs 107.1 µs per seal launch, rocprof A/B,
 // profiles/r2_s3/ab_chacha_prefetch): the kernel is bound by VALU issue, not by load latency.
-template <bool OPEN>
-__global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs args) {
+// One wave's group of 4 packets (16 lanes each): packets 4·grp .. 4·grp + 3 of the batch, the
+// descriptor of packet p from desc_of(p).
+template <bool OPEN, class DF>
+__device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t grp, uint32_t npkt, DF&& desc_of) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
     const uint32_t l = lane & 15u;
     const uint32_t w = l & 3u;      // column within the quad
     const uint32_t j = l >> 2;      // quad within the packet
     const uint32_t q = lane >> 4;   // packet slot within the wave
     const uint32_t pbase = lane & ~15u;  // first lane of this packet
-    uint32_t npkt = args.npkt;
-    if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
-    const uint32_t ngroups = (npkt + 3u) >> 2;
     constexpr uint32_t kConst[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
-
-    for (uint32_t grp = blockIdx.x * kChWavesPerWG + wave; grp < ngroups; grp += gridDim.x * kChWavesPerWG) {
+    {
         const uint32_t p = grp * 4u + q;
         const bool valid = p < npkt;
         neb_desc d = {};
-        if (valid) d = args.desc[p];
+        if (valid) d = desc_of(p);
         uint32_t st = NEB_STATUS_OK;
         if (args.key_hint != NEB_KEYS_MIXED && d.key_id != args.key_hint) st = NEB_STATUS_BAD_KEY;
         const uint32_t* rec = args.keys + (size_t)d.key_id * kKeyRecDwords;
@@ -278,7 +277,7 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 32));
         if (rmax == 0u) {
             if (valid && l == 15u) args.status[p] = (int32_t)st;
-            continue;
+            return;
         }
 
         // state column w: a = constant, b = key word w, c = key word 4+w, d = counter / nonce
@@ -349,7 +348,7 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
         }
         if (!run) {
             if (valid && l == 15u) args.status[p] = (int32_t)st;
-            continue;
+            return;
         }
         // lane l's last block is e_l = ((t - l - 1) mod 16) + 1 blocks from the end
         const uint32_t e = ((t - l - 1u) & 15u) + 1u;
@@ -378,6 +377,42 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
         }
         if (l == 15u) args.status[p] = (int32_t)st;
     }
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs args) {
+    const uint32_t wave = threadIdx.x >> 6;
+    uint32_t npkt = args.npkt;
+    if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
+    const uint32_t ngroups = (npkt + 3u) >> 2;
+    for (uint32_t grp = blockIdx.x * kChWavesPerWG + wave; grp < ngroups; grp += gridDim.x * kChWavesPerWG)
+        chacha_group<OPEN>(args, grp, npkt, [&](uint32_t p) { return args.desc[p]; });
+}
+
+// One packet, its bytes in the kernel arguments (the per-packet path; aes_gcm.hip gcm_one_kernel
+// has the why): lanes 0-15 of one wave.
+constexpr uint32_t kChOneBytes = 2048;
+struct ChOneArgs {
+    neb_desc d;  // offsets from `in`; dst_off = the output's address (rebased in the kernel)
+    const uint32_t* keys;
+    uint32_t max_keys, key;
+    int32_t* status;
+    uint32_t pad_[2];
+    uint8_t in[kChOneBytes];
+};
+static_assert(offsetof(ChOneArgs, in) % 16 == 0, "the packet bytes are read as 16-B blocks");
+template <bool OPEN>
+__global__ __launch_bounds__(kWave) void chacha_one_kernel(ChOneArgs a) {
+    // the block's address as an opaque integer: derived from the constant-address kernarg pointer,
+    // the output address (base + dst_off) would let the compiler treat the result stores as stores
+    // to constant memory and drop them
+    uint64_t kb = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(ChOneArgs, in);
+    asm volatile("" : "+s"(kb));
+    uint8_t* base = reinterpret_cast<uint8_t*>(kb);
+    neb_desc d = a.d;
+    d.dst_off = a.d.dst_off - (uint64_t)(uintptr_t)base;
+    const ChachaArgs ca{nullptr, 1u, base, a.keys, a.max_keys, a.key, a.status, nullptr, 0u};
+    chacha_group<OPEN>(ca, 0u, 1u, [&](uint32_t) { return d; });
 }
 
 // Key install of a batch of keys, one workgroup per key: the record is cleared (it may have held
@@ -420,6 +455,34 @@ static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStrea
     // stop (optional): bound to the dispatch, so no marker packet follows the batch (hipExtLaunchKernel)
     if (stop) hipExtLaunchKernelGGL(kern, dim3(grid), dim3(neb::kChThreads), 0, s, nullptr, stop, 0, a);
     else hipLaunchKernelGGL(kern, dim3(grid), dim3(neb::kChThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// One packet (the per-packet path), as neb_gcm_one.
+extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in,
+                                     uint32_t in_len, uint32_t len, uint64_t counter, uint8_t* out, int32_t* status,
+                                     const uint32_t* d_keys, uint32_t max_keys, uint32_t key, hipStream_t s) {
+    const uint32_t pay = (aad_len + 15u) & ~15u;
+    if ((uint64_t)pay + in_len > neb::kChOneBytes) return hipErrorInvalidValue;
+    neb::ChOneArgs a;
+    std::memset(&a, 0, offsetof(neb::ChOneArgs, in));
+    if (aad_len) std::memcpy(a.in, aad, aad_len);
+    if (in_len) std::memcpy(a.in + pay, in, in_len);
+    a.d.aad_off = 0;
+    a.d.src_off = pay;
+    a.d.dst_off = (uint64_t)(uintptr_t)out;
+    a.d.len = len;
+    a.d.aad_len = aad_len;
+    a.d.counter = counter;
+    a.d.key_id = key;
+    a.keys = d_keys;
+    a.max_keys = max_keys;
+    a.key = key;
+    a.status = status;
+    if (open)
+        hipLaunchKernelGGL(neb::chacha_one_kernel<true>, dim3(1), dim3(neb::kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL(neb::chacha_one_kernel<false>, dim3(1), dim3(neb::kWave), 0, s, a);
     return hipGetLastError();
 }
 

@@ -35,6 +35,12 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
                                            int hdr_from_dst, hipEvent_t stop);
+extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in, uint32_t in_len,
+                                  uint32_t len, uint64_t counter, uint8_t* out, int32_t* status, const uint32_t* d_keys,
+                                  uint32_t max_keys, uint32_t key, hipStream_t s);
+extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in,
+                                     uint32_t in_len, uint32_t len, uint64_t counter, uint8_t* out, int32_t* status,
+                                     const uint32_t* d_keys, uint32_t max_keys, uint32_t key, hipStream_t s);
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const neb_desc* d_sdesc, const uint4* d_chunks,
@@ -832,6 +838,35 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
     PktLease sl(e->pkt);
     if (!sl.reserve(total)) return NEB_ERR_HIP;
     uint8_t* h = sl->h;
+    // The packet's bytes travel in the kernel's arguments and only the result comes back through
+    // the slot (aes_gcm.hip gcm_one_kernel, chacha_poly.hip chacha_one_kernel); NEB_ONE_KERNEL=0
+    // for the A/B
+    static const bool one = [] {
+        const char* v = std::getenv("NEB_ONE_KERNEL");
+        return !(v && v[0] == '0');
+    }();
+    if (one) {
+        *(int32_t*)(h + o_status) = -1;
+        auto* fn = c->alg == NEB_ALG_AESGCM ? neb_gcm_one : neb_chacha_one;
+        hipError_t err = fn(open, ad, (uint32_t)ad_len, in, (uint32_t)in_len, (uint32_t)pay_len, n, h + o_pay,
+                            (int32_t*)(h + o_status), e->d_keys, e->max_keys, c->key_id, sl->stream);
+        if (err == hipSuccess) {
+            err = hipStreamSynchronize(sl->stream);
+            if (err != hipSuccess) {
+                set_error("one_packet", err);
+                return NEB_ERR_HIP;
+            }
+            std::memcpy(st_out, h + o_status, 4);
+            const size_t out_len = open ? pay_len : pay_len + 16;
+            if (out_len) std::memcpy(dst, h + o_pay, out_len);
+            return NEB_OK;
+        }
+        if (err != hipErrorInvalidValue) {  // (too large for the arguments: the batch path below)
+            set_error("one_packet", err);
+            return NEB_ERR_HIP;
+        }
+        (void)hipGetLastError();
+    }
     neb_desc d{};
     d.src_off = o_pay - o_aad;
     d.dst_off = o_pay - o_aad;

@@ -38,6 +38,60 @@ __device__ __forceinline__ bool rx_bit(const uint64_t* bits, uint64_t mask, uint
     return (bits[p >> 6] >> (p & 63)) & 1u;
 }
 
+__device__ __forceinline__ uint32_t rx_hash(uint32_t w, uint64_t c, uint32_t lg) {
+    uint64_t h = (c ^ ((uint64_t)w << 40) ^ w) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    return (uint32_t)(h >> (64 - lg));
+}
+
+// The slot of packet i's (window, counter) key: claimed by the first to arrive at it, found by
+// comparing the owner's key (exact, no hash comparison); the table has at least 4n slots. An
+// entry whose generation is not this batch's is empty.
+__device__ __forceinline__ uint32_t rx_slot(const RxDevWs& ws, uint32_t i, uint32_t w, uint64_t c, bool insert) {
+    const uint32_t tmask = (1u << ws.tab_lg) - 1u;
+    const uint64_t mine = ((uint64_t)ws.gen << 32) | (i + 1u);
+    uint32_t h = rx_hash(w, c, ws.tab_lg);
+    for (;;) {
+        uint64_t o = ws.tab_owner[h];
+        if (insert) {
+            while ((uint32_t)(o >> 32) != ws.gen) {  // empty: claim it
+                const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(ws.tab_owner + h), o, mine);
+                if (seen == o) return h;
+                o = seen;
+            }
+        }
+        // (a lookup always finds its own key before an empty slot)
+        const uint32_t oi = (uint32_t)o - 1u;
+        if (o == mine || (ws.keyw[oi] == w && ws.ctr[oi] == c)) return h;
+        h = (h + 1u) & tmask;
+    }
+}
+
+
+// The first-occurrence table's insert, in the keys kernel: as rx_slot, but an owner's key comes
+// from its descriptor (keyw / ctr of other workgroups are being written in the same launch).
+__device__ __forceinline__ uint32_t rx_slot_insert(const RxDevWs& ws, const RxDevWin& win,
+                                                   const neb_desc* __restrict__ desc, uint32_t i, uint32_t w,
+                                                   uint64_t c) {
+    const uint32_t tmask = (1u << ws.tab_lg) - 1u;
+    const uint64_t mine = ((uint64_t)ws.gen << 32) | (i + 1u);
+    uint32_t h = rx_hash(w, c, ws.tab_lg);
+    for (;;) {
+        uint64_t o = ws.tab_owner[h];  // may be stale: the CAS returns the slot's real owner
+        while ((uint32_t)(o >> 32) != ws.gen) {  // empty: claim it
+            const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(ws.tab_owner + h), o, mine);
+            if (seen == o) return h;
+            o = seen;
+        }
+        if (o == mine) return h;
+        const uint32_t oi = (uint32_t)o - 1u;
+        const uint32_t ok = desc[oi].key_id;
+        const uint32_t ow = ok < win.count && win.present[ok] ? ok : win.count;
+        if (ow == w && desc[oi].counter == c) return h;
+        h = (h + 1u) & tmask;
+    }
+}
+
 // ---- the stable sort of the packets by window (LSD radix, arrival order kept) ----------------
 // At most kRxSortBlocks workgroups of 256 x items packets each, so every workgroup of a pass can
 // read all the workgroups' digit counts itself (no scan launch) and the next pass's counts are
@@ -64,7 +118,11 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
         const size_t wi = (size_t)b * so.per_blk + x;
         if (wi < win.count) ws.wflag[wi] = 0;
     }
-    if (b == 0 && t == 0) *ws.nsub = 0;
+    if (b == 0 && t == 0) {
+        *ws.nsub = 0;
+        *ws.ticket = 0;
+        *ws.err = 0;
+    }
     if (b >= so.nblk) return;
     for (uint32_t p = 1; p < so.passes; p++) ws.sort_hist[((size_t)p * kRxSortBlocks + b) * 256 + t] = 0;
     __syncthreads();
@@ -101,6 +159,14 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
             ws.ctr[e] = ctr[r];
             differs |= w != w0;
             atomicAdd(&hist[(w >> so.shift[0]) & mask], 1u);
+            if (w < win.count) {
+                // the (window, counter) key into the first-occurrence table, and a counter near the
+                // wrap marks its window for the host (the scan-admit reads both after this launch)
+                const uint32_t h = rx_slot_insert(ws, win, desc, e, w, ctr[r]);
+                atomicMax(reinterpret_cast<unsigned long long*>(ws.tab_min + h),
+                          ((unsigned long long)ws.gen << 32) | (0xFFFFFFFFu - e));
+                if (ctr[r] >= kRxRiskyCounter) atomicMax(ws.wrisky + w, ws.gen);
+            }
         }
     }
     if (differs) s_mixed = 1u;
@@ -213,35 +279,6 @@ __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p
     }
 }
 
-__device__ __forceinline__ uint32_t rx_hash(uint32_t w, uint64_t c, uint32_t lg) {
-    uint64_t h = (c ^ ((uint64_t)w << 40) ^ w) * 0x9E3779B97F4A7C15ull;
-    h ^= h >> 29;
-    return (uint32_t)(h >> (64 - lg));
-}
-
-// The slot of packet i's (window, counter) key: claimed by the first to arrive at it, found by
-// comparing the owner's key (exact, no hash comparison); the table has at least 4n slots. An
-// entry whose generation is not this batch's is empty.
-__device__ __forceinline__ uint32_t rx_slot(const RxDevWs& ws, uint32_t i, uint32_t w, uint64_t c, bool insert) {
-    const uint32_t tmask = (1u << ws.tab_lg) - 1u;
-    const uint64_t mine = ((uint64_t)ws.gen << 32) | (i + 1u);
-    uint32_t h = rx_hash(w, c, ws.tab_lg);
-    for (;;) {
-        uint64_t o = ws.tab_owner[h];
-        if (insert) {
-            while ((uint32_t)(o >> 32) != ws.gen) {  // empty: claim it
-                const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(ws.tab_owner + h), o, mine);
-                if (seen == o) return h;
-                o = seen;
-            }
-        }
-        // (a lookup always finds its own key before an empty slot)
-        const uint32_t oi = (uint32_t)o - 1u;
-        if (o == mine || (ws.keyw[oi] == w && ws.ctr[oi] == c)) return h;
-        h = (h + 1u) & tmask;
-    }
-}
-
 // (head, max) pairs of the segmented max scan: a head starts a new run
 struct RxSeg {
     uint32_t f;
@@ -249,42 +286,75 @@ struct RxSeg {
 };
 __device__ __forceinline__ RxSeg rx_seg(RxSeg a, RxSeg b) { return {a.f | b.f, b.f ? b.v : max(a.v, b.v)}; }
 
-// Run order (sorted by window, arrival order kept), kRxBlock elements per workgroup: the counters
-// in run order, touched / risky windows, every packet's key into the first-occurrence table, and
-// the segmented inclusive max of the counters within the workgroup (blk_max / blk_fh let the
-// admission finish the scan across workgroups).
-__global__ __launch_bounds__(kRxThreads) void rx_scan_kernel(uint32_t n, RxDevWin win, RxDevWs ws) {
+// R2 granules (cdna_hip_programming.md Guideline 16): {gen:32 | value:32}, one aligned 8-B
+// agent-scope atomic store each, read back by agent-scope atomic loads until the tag matches
+__device__ __forceinline__ void rx_pub(uint64_t* g, uint32_t gen, uint32_t v) {
+    __hip_atomic_store(g, ((uint64_t)gen << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t rx_peek(const uint64_t* g) {
+    return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr uint32_t kRxSpinLimit = 1u << 20;  // ≈ 0.1 s of polling: then the batch fails (need_host bit 1)
+
+// Scan and admission in one launch, kRxBlock run positions per workgroup, in the order the
+// workgroups start (a ticket), so every block a workgroup waits for has started and waits only
+// for blocks before it. Per workgroup:
+//  1. its counters into run order, touched / risky flags of its runs' heads, and the segmented
+//     inclusive max of the counters within the block; then its first head and the max at its last
+//     position are published (rx_pub, tagged with the batch generation);
+//  2. one wave looks back over the blocks before it, as far as (and including) the first that holds
+//     a run head, and takes the max of their published values: the max over the part of the run
+//     that continues into this block from before it;
+//  3. which packets the sequential receive would decrypt, if every tag verified (safe windows):
+//     c > the run's max so far, or inside the window, not received before and the first
+//     occurrence of its (window, counter) (the table the keys kernel filled); compacted into
+//     sub_map / sub_desc with one atomic per workgroup (order is immaterial to the open); the run's
+//     last packet sets its window's final current and the range of counters that leave it.
+// A window with a counter near the wrap (wrisky, from the keys kernel) or a current near it is
+// decided on the host.
+__global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_desc* __restrict__ desc, uint32_t n,
+                                                                     RxDevWin win, RxDevWs ws,
+                                                                     int32_t* __restrict__ status) {
     __shared__ uint64_t s_v[kRxThreads / 64];
     __shared__ uint32_t s_f[kRxThreads / 64];
-    __shared__ uint32_t s_fh;
+    __shared__ uint64_t s_incl[kRxBlock];
+    __shared__ uint64_t s_pre;
+    __shared__ uint32_t s_fh, s_b, s_base;
+    __shared__ uint32_t s_cnt[kRxThreads / 64];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint32_t b0 = blockIdx.x * kRxBlock, k0 = b0 + t * kRxItems;
-    if (t == 0) s_fh = kRxBlock;
+    if (t == 0) {
+        s_b = atomicAdd(ws.ticket, 1u);
+        s_fh = kRxBlock;
+    }
+    __syncthreads();
+    const uint32_t b = s_b, b0 = b * kRxBlock, k0 = b0 + t * kRxItems;
+    const uint32_t gen = ws.gen;
     uint64_t c[kRxItems];
-    uint32_t hd[kRxItems];
+    uint32_t hd[kRxItems], wj[kRxItems], ij[kRxItems];
     RxSeg agg{0u, 0ull};
 #pragma unroll
     for (uint32_t j = 0; j < kRxItems; j++) {
         const uint32_t k = k0 + j;
         c[j] = 0;
         hd[j] = 0;
+        wj[j] = win.count;
+        ij[j] = 0;
         if (k >= n) continue;
         const uint32_t w = ws.run_w[k];
         const uint32_t i = ws.run_i[k];
+        wj[j] = w;
+        ij[j] = i;
         c[j] = ws.ctr[i];
         ws.run_c[k] = c[j];
         hd[j] = k == 0u || ws.run_w[k - 1u] != w;
         agg = rx_seg(agg, {hd[j], c[j]});
-        if (w >= win.count) continue;
-        // flag words are written by the run's head and by risky packets only (one window's whole
-        // batch on one address would serialise)
-        uint32_t fl = c[j] >= kRxRiskyCounter ? kRxRisky : 0u;
-        if (hd[j]) fl |= kRxTouched | (win.cur[w] >= kRxRiskyCounter ? kRxRisky : 0u);
-        if (fl) atomicOr(&ws.wflag[w], fl);
-        atomicMax(reinterpret_cast<unsigned long long*>(ws.tab_min + rx_slot(ws, i, w, c[j], true)),
-                  ((unsigned long long)ws.gen << 32) | (0xFFFFFFFFu - i));
+        // flag words are written by the run's head only (one window's whole batch on one address
+        // would serialise)
+        if (w < win.count && hd[j]) {
+            const bool risky = ws.wrisky[w] == gen || win.cur[w] >= kRxRiskyCounter;
+            atomicOr(&ws.wflag[w], kRxTouched | (risky ? kRxRisky : 0u));
+        }
     }
-    __syncthreads();  // s_fh
 #pragma unroll
     for (uint32_t j = 0; j < kRxItems; j++)
         if (hd[j]) {
@@ -309,63 +379,85 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_kernel(uint32_t n, RxDevWi
     RxSeg wp{0u, 0ull};
     for (uint32_t q = 0; q < wv; q++) wp = rx_seg(wp, {s_f[q], s_v[q]});
     RxSeg run = rx_seg(wp, ex);
+    const uint32_t fh = s_fh;
 #pragma unroll
     for (uint32_t j = 0; j < kRxItems; j++) {
         const uint32_t k = k0 + j;
         run = rx_seg(run, {hd[j], c[j]});
-        if (k < n) ws.incl[k] = run.v;
-        if (k + 1u == n || k == b0 + kRxBlock - 1u) {  // the workgroup's last element
-            ws.blk_max[blockIdx.x] = run.v;
-            ws.blk_fh[blockIdx.x] = s_fh;
+        s_incl[t * kRxItems + j] = run.v;
+        if (k + 1u == n || k == b0 + kRxBlock - 1u) {  // the block's last position: publish
+            rx_pub(ws.blk_pub + 3u * b, gen, fh);
+            rx_pub(ws.blk_pub + 3u * b + 1u, gen, (uint32_t)run.v);
+            rx_pub(ws.blk_pub + 3u * b + 2u, gen, (uint32_t)(run.v >> 32));
         }
     }
-}
-
-// Which packets the sequential receive would decrypt, if every tag verified (safe windows),
-// compacted into sub_map / sub_desc (one atomic per workgroup; order is immaterial to the open);
-// the run's last packet sets its window's final current and the range of counters that leave it.
-__global__ __launch_bounds__(kRxThreads) void rx_admit_kernel(const neb_desc* __restrict__ desc, uint32_t n,
-                                                                RxDevWin win, RxDevWs ws,
-                                                                int32_t* __restrict__ status) {
-    __shared__ uint64_t s_pre;
-    __shared__ uint32_t s_cnt[kRxThreads / 64];
-    __shared__ uint32_t s_base;
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint32_t b = blockIdx.x, b0 = b * kRxBlock, k0 = b0 + t * kRxItems;
-    const uint32_t fh = ws.blk_fh[b];
-    // the max over the run that continues into this workgroup: back over earlier workgroups to
-    // (and including) the first one holding a run head
+    // the max over the run that continues into this block: back over earlier blocks to (and
+    // including) the first one holding a run head, 64 at a time, each lane polling one block's
+    // granules until they carry this batch's generation
     if (wv == 0) {
         uint64_t pre = 0;
+        bool timed_out = false;
         if (fh > 0u)
-            for (int64_t base = (int64_t)b - 1; base >= 0; base -= 64) {
+            for (int64_t base = (int64_t)b - 1; base >= 0 && !timed_out; base -= 64) {
                 const int64_t bb = base - (int64_t)lane;
                 const bool valid = bb >= 0;
-                const bool has = valid && ws.blk_fh[bb] < kRxBlock;
+                uint32_t g_fh = kRxBlock;
+                uint64_t g_max = 0;
+                bool got = !valid;
+                uint32_t spins = 0;
+                for (;;) {
+                    if (!got) {
+                        const uint64_t* g = ws.blk_pub + 3u * (uint64_t)bb;
+                        const uint64_t a0 = rx_peek(g), a1 = rx_peek(g + 1), a2 = rx_peek(g + 2);
+                        if ((uint32_t)(a0 >> 32) == gen && (uint32_t)(a1 >> 32) == gen && (uint32_t)(a2 >> 32) == gen) {
+                            got = true;
+                            g_fh = (uint32_t)a0;
+                            g_max = (uint64_t)(uint32_t)a1 | ((uint64_t)(uint32_t)a2 << 32);
+                        }
+                    }
+                    // done once the blocks up to the nearest one with a head (or all 64) are in
+                    const uint64_t in = __ballot(got), heads = __ballot(got && g_fh < kRxBlock);
+                    const uint64_t need = heads ? ((heads & (~heads + 1u)) << 1) - 1u : ~0ull;  // lanes <= first head
+                    if ((in & need) == need) break;
+                    if (++spins > kRxSpinLimit) {
+                        timed_out = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (timed_out) break;
+                const bool has = valid && g_fh < kRxBlock;
                 const uint64_t stop = __ballot(has);
                 const uint32_t last = stop ? (uint32_t)__builtin_ctzll(stop) : 63u;
-                uint64_t m = (valid && lane <= last) ? ws.blk_max[bb] : 0ull;
+                uint64_t m = (valid && lane <= last) ? g_max : 0ull;
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) m = max(m, (uint64_t)__shfl_xor(m, o));
                 pre = max(pre, m);
                 if (stop) break;
             }
-        if (lane == 0) s_pre = pre;
+        if (lane == 0) {
+            s_pre = pre;
+            if (timed_out) {
+                atomicOr(ws.err, 1u);
+                s_fh = 0xFFFFFFFFu;  // admit nothing here
+            }
+        }
     }
     __syncthreads();
     const uint64_t pre = s_pre;
+    const bool failed = s_fh == 0xFFFFFFFFu;
     auto incl_at = [&](uint32_t k) -> uint64_t {  // the run's inclusive max at k (k >= b0 - 1)
         if (k < b0) return pre;
-        const uint64_t v = ws.incl[k];
+        const uint64_t v = s_incl[k - b0];
         return k - b0 >= fh ? v : max(pre, v);
     };
-    uint32_t okm = 0, ids[kRxItems];
+    uint32_t okm = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kRxItems; j++) {
         const uint32_t k = k0 + j;
         if (k >= n) continue;
-        const uint32_t w = ws.run_w[k];
-        const uint32_t i = ws.run_i[k];
+        const uint32_t w = wj[j];
+        const uint32_t i = ij[j];
         ws.verdict[i] = NEB_STATUS_OK;
         ws.adm[i] = 0;
         if (w >= win.count) {
@@ -380,18 +472,17 @@ __global__ __launch_bounds__(kRxThreads) void rx_admit_kernel(const neb_desc* __
             ws.exit_hi[w] = cur >= len ? cur - len : 0u;          // lo > hi: none left
             ws.recv[w] = 0;
         }
-        if (ws.wflag[w] & kRxRisky) continue;  // decided on the host
-        const bool head = k == 0u || ws.run_w[k - 1u] != w;
+        if (failed || ws.wrisky[w] == gen || cur0 >= kRxRiskyCounter) continue;  // decided on the host
+        const bool head = hd[j] != 0u;
         const uint64_t prev = head ? cur0 : max(cur0, incl_at(k - 1u));
-        const uint64_t c = ws.run_c[k];
+        const uint64_t cc = c[j];
         const uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
-        bool ok = c > prev;  // above every earlier counter of the run: its first occurrence too
-        if (!ok && rx_in_window(c, prev, win.length)) {
-            ok = !(c <= cur0 && rx_bit(bits, win.length - 1u, c));
+        bool ok = cc > prev;  // above every earlier counter of the run: its first occurrence too
+        if (!ok && rx_in_window(cc, prev, win.length)) {
+            ok = !(cc <= cur0 && rx_bit(bits, win.length - 1u, cc));
             // the first occurrence of (window, counter)
-            ok = ok && ws.tab_min[rx_slot(ws, i, w, c, false)] == (((uint64_t)ws.gen << 32) | (0xFFFFFFFFu - i));
+            ok = ok && ws.tab_min[rx_slot(ws, i, w, cc, false)] == (((uint64_t)gen << 32) | (0xFFFFFFFFu - i));
         }
-        ids[j] = i;
         if (ok) {
             ws.adm[i] = 1;
             okm |= 1u << j;
@@ -401,13 +492,13 @@ __global__ __launch_bounds__(kRxThreads) void rx_admit_kernel(const neb_desc* __
     }
     // workgroup prefix of the admitted counts
     const uint32_t take = (uint32_t)__popc(okm);
-    uint32_t x = take;
+    uint32_t xx = take;
 #pragma unroll
     for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
+        const uint32_t y = __shfl_up(xx, o);
+        if (lane >= o) xx += y;
     }
-    if (lane == 63u) s_cnt[wv] = x;
+    if (lane == 63u) s_cnt[wv] = xx;
     __syncthreads();
     if (t == 0) {
         uint32_t tot = 0;
@@ -415,13 +506,13 @@ __global__ __launch_bounds__(kRxThreads) void rx_admit_kernel(const neb_desc* __
         s_base = tot ? atomicAdd(ws.nsub, tot) : 0u;
     }
     __syncthreads();
-    uint32_t j0 = s_base + x - take;
+    uint32_t j0 = s_base + xx - take;
     for (uint32_t q = 0; q < wv; q++) j0 += s_cnt[q];
 #pragma unroll
     for (uint32_t j = 0; j < kRxItems; j++)
         if (okm >> j & 1u) {
-            ws.sub_map[j0] = ids[j];
-            ws.sub_desc[j0++] = desc[ids[j]];
+            ws.sub_map[j0] = ij[j];
+            ws.sub_desc[j0++] = desc[ij[j]];
         }
 }
 
@@ -561,7 +652,11 @@ __global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
     const uint32_t w = wl < win.count ? (uint32_t)wl : 0u;
     const uint32_t fl = wl < win.count ? ws.wflag[w] : 0u;
     const bool fast = rx_fast(fl);
-    if ((fl & kRxTouched) && (fl & (kRxRisky | kRxSlow)) && sub == 0) *ws.need_host = 1u;  // a plain store
+    // plain stores into the pinned host word: bit 0 a window for the host, bit 1 a lookback timeout
+    // (every writer reads the same err, so racing writers agree on bit 1)
+    const uint32_t errb = *ws.err ? 2u : 0u;
+    if ((fl & kRxTouched) && (fl & (kRxRisky | kRxSlow)) && sub == 0) *ws.need_host = 1u | errb;
+    if (errb && t == 0) *ws.need_host = errb | 1u;
     uint64_t r = 0;
     uint64_t cur = 0, lo = 1, hi = 0;
     if ((fl & kRxTouched) && !fast) {  // the settle may have set bits of a window finished on the host
@@ -642,8 +737,7 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
                                sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i);
     }
     const dim3 blocks((n + neb::kRxBlock - 1) / neb::kRxBlock);
-    hipLaunchKernelGGL(neb::rx_scan_kernel, blocks, dim3(neb::kRxThreads), 0, s, n, *win, *ws);
-    hipLaunchKernelGGL(neb::rx_admit_kernel, blocks, dim3(neb::kRxThreads), 0, s, d_desc, n, *win, *ws, d_status);
+    hipLaunchKernelGGL(neb::rx_scan_admit_kernel, blocks, dim3(neb::kRxThreads), 0, s, d_desc, n, *win, *ws, d_status);
     return hipGetLastError();
 }
 

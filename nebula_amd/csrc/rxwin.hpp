@@ -48,10 +48,13 @@ struct RxDevWs {
     // run order (sorted by window, arrival order kept)
     uint32_t* run_w;
     uint32_t* run_i;
-    uint64_t* run_c;
-    uint64_t* incl;     // segmented inclusive max of the counters within each block of kRxBlock
-    uint64_t* blk_max;  // per block: incl at its last element
-    uint32_t* blk_fh;   // per block: position of its first run head (kRxBlock: none)
+    uint64_t* run_c;  // the counters in run order (read by the host's exact pass)
+    // per block of kRxBlock run positions, published inside rx_scan_admit_kernel for the blocks
+    // after it: 3 granules {gen:32 | value:32} = the position of its first run head (kRxBlock:
+    // none), then the low and high words of the segmented max at its last element
+    uint64_t* blk_pub;
+    uint32_t* ticket;  // the scan-admit blocks' order of start (zeroed by the keys kernel)
+    uint32_t* err;     // nonzero: a scan-admit lookback timed out (zeroed by the keys kernel)
     // first occurrences: an open-addressing table keyed by (window, counter), 2^tab_lg >= 4n slots,
     // tagged with the batch generation (an entry of an older batch is empty, so the table is
     // never cleared between batches); a slot's owner (gen:32 | arrival index + 1) names its key
@@ -66,13 +69,15 @@ struct RxDevWs {
     int32_t* sub_status;
     uint32_t* nsub;
     // per window
+    uint32_t* wrisky;  // the generation of the last batch with a counter >= kRxRiskyCounter in it
     uint32_t* wflag;
     uint64_t* curnew;
     uint64_t* exit_lo;
     uint64_t* exit_hi;
     uint64_t* recv;
     uint64_t* scratch;  // count x words
-    uint32_t* need_host;  // pinned host word: set to 1 when a touched window is risky or slow
+    uint32_t* need_host;  // pinned host word: bit 0 when a touched window is risky or slow, bit 1 on
+                          // a lookback timeout (an internal error: the batch fails)
     // the generation of the last batch whose packets named more than one window (written by the
     // keys kernel); any other value lets the sort passes write the identity order (one window)
     uint32_t* mixed;
@@ -100,10 +105,10 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
     w.run_w = (uint32_t*)take((size_t)n * 4);
     w.run_i = (uint32_t*)take((size_t)n * 4);
     w.run_c = (uint64_t*)take((size_t)n * 8);
-    w.incl = (uint64_t*)take((size_t)n * 8);
     const size_t nblk = ((size_t)n + kRxBlock - 1) / kRxBlock;
-    w.blk_max = (uint64_t*)take(nblk * 8);
-    w.blk_fh = (uint32_t*)take(nblk * 4);
+    w.blk_pub = (uint64_t*)take(nblk * 3 * 8);
+    w.ticket = (uint32_t*)take(4);
+    w.err = (uint32_t*)take(4);
     w.tab_lg = 1;
     while ((1ull << w.tab_lg) < 4ull * n) w.tab_lg++;  // at most a quarter full
     w.tab_owner = (uint64_t*)take((size_t)8 << w.tab_lg);
@@ -112,6 +117,7 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
     w.sub_desc = (neb_desc*)take((size_t)n * sizeof(neb_desc));
     w.sub_status = (int32_t*)take((size_t)n * 4);
     w.nsub = (uint32_t*)take(4);
+    w.wrisky = (uint32_t*)take((size_t)count * 4);
     w.wflag = (uint32_t*)take((size_t)count * 4);
     w.curnew = (uint64_t*)take((size_t)count * 8);
     w.exit_lo = (uint64_t*)take((size_t)count * 8);

@@ -30,12 +30,35 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
     if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i < kSchedCounters; i += blockDim.x) ws.counters[i] = 0;
     if (dn) n = min(n, *dn);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const neb_desc d = desc[i];
-        const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
-        const uint32_t b = (size_class(d, lpp) * (max_keys + 1u) + key) * SUB + (blockIdx.x & (SUB - 1u));
-        ws.binof[i] = b;
-        ws.binpos[i] = atomicAdd(&ws.hist[b], 1u);
+    // Neighbouring lanes in the same bin (a batch already grouped by key, e.g. a receive batch in
+    // its windows' order) add their count once: the run's first lane adds the run's length and
+    // hands each lane its rank (one returning atomic per run instead of one per packet on the
+    // same word). Every lane of a wave runs every pass (the shuffles), valid lanes are a prefix.
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t upto = lane == 63u ? ~0ull : (2ull << lane) - 1u;  // lanes <= this one
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
+        const bool valid = i < n;
+        uint32_t b = 0xFFFFFFFFu;
+        if (valid) {
+            const neb_desc d = desc[i];
+            const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
+            b = (size_class(d, lpp) * (max_keys + 1u) + key) * SUB + (blockIdx.x & (SUB - 1u));
+        }
+        const uint32_t pb = (uint32_t)__shfl_up((int)b, 1);
+        const bool head = valid && (lane == 0u || pb != b);
+        const uint64_t hm = __ballot(head);
+        const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+        const uint32_t hl = 63u - (uint32_t)__builtin_clzll((hm & upto) | 1ull);  // this lane's run head
+        const uint64_t after = hm & ~upto;
+        const uint32_t next = after ? (uint32_t)__builtin_ctzll(after) : nvalid;  // the next run's head
+        uint32_t base = 0;
+        if (head) base = atomicAdd(&ws.hist[b], next - lane);
+        base = (uint32_t)__shfl((int)base, (int)hl);
+        if (valid) {
+            ws.binof[i] = b;
+            ws.binpos[i] = base + (lane - hl);
+        }
     }
 }
 

@@ -538,9 +538,12 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
         d->ws_n = n;
     }
     // a new generation per batch empties the first-occurrence table; cleared for real at wrap
-    if (++d->ws.gen == 0) {
+    if (++d->ws.gen == 0) {  // (every generation-tagged word: the table, the block granules, wrisky)
+        const size_t nblk = ((size_t)d->ws_n + neb::kRxBlock - 1) / neb::kRxBlock;
         RX_HIP(hipMemsetAsync(d->ws.tab_owner, 0, (size_t)8 << d->ws.tab_lg, s));
         RX_HIP(hipMemsetAsync(d->ws.tab_min, 0, (size_t)8 << d->ws.tab_lg, s));
+        RX_HIP(hipMemsetAsync(d->ws.blk_pub, 0, nblk * 3 * 8, s));
+        RX_HIP(hipMemsetAsync(d->ws.wrisky, 0, (size_t)v.count * 4, s));
         d->ws.gen = 1;
     }
     *d->h_host = 0;
@@ -569,7 +572,9 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
         std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, open %.1f, finish %.1f us, wait %.1f us\n", n, us(t0, t1),
                      us(t1, t2), us(t2, t3), us(t3, now()));
     // the finish flags, in pinned host memory, whether any window needs the sequential finish
-    if (__atomic_load_n(d->h_host, __ATOMIC_ACQUIRE) == 0) return NEB_OK;
+    const uint32_t need = __atomic_load_n(d->h_host, __ATOMIC_ACQUIRE);
+    if (need == 0) return NEB_OK;
+    if (need & 2u) return NEB_ERR_HIP;  // rx_scan_admit_kernel's lookback timed out (an internal error)
     std::vector<uint32_t> flag;
     if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
     RX_HIP(hipStreamSynchronize(s));

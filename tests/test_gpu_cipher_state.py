@@ -357,3 +357,32 @@ def test_entry_points_restore_current_device():
             c.destroy()
         assert torch.cuda.current_device() == 0
     assert torch.cuda.current_device() == 0
+
+
+def test_one_packet_kernel_size_boundary(engine, oracle_mod):
+    """AES-GCM per-packet calls carry the packet in the kernel's arguments up to 2048 bytes of
+    AAD (padded to 16) + payload (+ tag when opening) (aes_gcm.hip gcm_one_kernel); larger ones take
+    the batch path. Both sides of the boundary, with 0-, 16- and 1348-byte AADs (the relay's
+    GMAC), seal and open against the oracle, a tampered tag refused with the plaintext zeroed."""
+    from nebula_amd import _lib as L
+    from nebula_amd.noiseutil import CipherAESGCM
+
+    rng = np.random.default_rng(5)
+    key = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    cs = CipherAESGCM.Cipher(engine, key)
+    try:
+        for ad_len in (0, 16, 1348):
+            room = 2048 - ((ad_len + 15) // 16) * 16
+            for pt_len in sorted({0, 1, 15, 16, 17, room - 17, room - 16, room - 15, room - 1, room, room + 1, 4000}):
+                n = (ad_len << 20) | pt_len
+                ad = bytes(rng.integers(0, 256, ad_len, dtype=np.uint8))
+                pt = bytes(rng.integers(0, 256, pt_len, dtype=np.uint8))
+                ct = cs.EncryptDanger(None, ad, pt, n).bytes()
+                assert ct == oracle_mod.seal(L.ALG_AESGCM, key, oracle_mod.nonce(L.ALG_AESGCM, n), ad, pt), (ad_len, pt_len)
+                assert cs.DecryptDanger(None, ad, ct, n).bytes() == pt, (ad_len, pt_len)
+                bad = bytearray(ct)
+                bad[-1] ^= 1
+                with pytest.raises(N.ErrOpen):
+                    cs.DecryptDanger(None, ad, bytes(bad), n)
+    finally:
+        cs.destroy()
