@@ -62,6 +62,25 @@ extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
                                        int hdr_from_dst, hipEvent_t stop);
 
+// The stream a workspace's `done` event was last recorded on. A batch on that same stream is
+// ordered after it already and skips the cross-stream wait (a barrier packet that cost ≈ 5 µs between
+// kernels). The handle alone does not name a stream: one destroyed with work still pending is
+// released when the work ends, and a stream created meanwhile may get its address; so the identity
+// is the handle together with HIP's per-stream id.
+struct StreamTag {
+    hipStream_t h = nullptr;
+    unsigned long long id = ~0ull;
+    static unsigned long long id_of(hipStream_t s) {
+        unsigned long long v = ~0ull;
+        return hipStreamGetId(s, &v) == hipSuccess ? v : ~0ull;
+    }
+    bool same(hipStream_t s) const { return id != ~0ull && h == s && id_of(s) == id; }
+    void set(hipStream_t s) {
+        h = s;
+        id = id_of(s);
+    }
+};
+
 // Device workspace of the mixed-key scheduler (sched.hpp). One per engine; a batch waits on the
 // previous user's event before reusing it, so batches on different streams never overlap in it.
 struct SchedSpace {
@@ -70,9 +89,7 @@ struct SchedSpace {
     uint32_t n_cap = 0;
     neb::SchedWs ws{};
     hipEvent_t done = nullptr;
-    // the stream `done` was last recorded on: a batch on that same stream is ordered after it
-    // already, and skips the cross-stream wait (a barrier packet that cost ≈ 5 µs between kernels)
-    hipStream_t last = nullptr;
+    StreamTag last;  // the stream `done` was last recorded on
     bool dirty = true;  // the bin counts need a clear (new buffer, or a batch that failed to launch)
     std::mutex mu;
 };
@@ -129,7 +146,7 @@ struct TxSpace {
     uint32_t n_cap = 0, tun_cap = 0, wire_cap = 0;
     neb::TxWs ws{};
     hipEvent_t done = nullptr;
-    hipStream_t last = nullptr;  // the stream `done` was last recorded on (SchedSpace::last)
+    StreamTag last;  // the stream `done` was last recorded on
     uint8_t* d_io = nullptr;  // neb_tx_seal_batch_host staging
     size_t io_cap = 0;
     std::mutex mu;
@@ -718,8 +735,9 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     const size_t b_counters = align_up((neb::kSchedCounters + (size_t)neb::kSubBins * nb) * 4u, 256);
     const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up(((size_t)mc + ms) * 16u, 256);
-    const size_t b_sums = (size_t)cap * 16u, b_sdesc = (size_t)cap * sizeof(neb_desc);
-    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_sums + b_sdesc;
+    const size_t b_sums = (size_t)cap * 16u, b_sdesc = align_up((size_t)cap * sizeof(neb_desc), 256);
+    const size_t b_sort = align_up(neb::sched_sort_tmp_bytes(cap, e->max_keys), 256);  // 0: no sorted binning
+    const size_t bytes = b_counters + b_base + 4 * b_idx + b_chunks + b_sums + b_sdesc + b_sort;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
     if (sp.mem) hipFree(sp.mem);
@@ -744,6 +762,11 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     sp.ws.sums = (uint4*)m;
     m += b_sums;
     sp.ws.sdesc = (neb_desc*)m;
+    m += b_sdesc;
+    sp.ws.vals = (uint32_t*)m;
+    m += b_idx;
+    sp.ws.sort_tmp = b_sort ? m : nullptr;
+    sp.ws.sort_tmp_bytes = b_sort;
     sp.ws.max_chunks = mc;
     sp.ws.max_short = ms;
     sp.bytes = bytes;
@@ -795,7 +818,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
         hipError_t err = sched_reserve(e, sp, n, s);
-        if (err == hipSuccess && sp.last != s) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
+        if (err == hipSuccess && !sp.last.same(s)) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
         const bool split = !host_arena && mixed_split();
         neb::SchedWs ws = sp.ws;
         if (!split && !sched_sdesc()) ws.sdesc = nullptr;
@@ -811,7 +834,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
                                             e->cu_count, s, hdr_from_dst, bind_events() ? sp.done : nullptr);
         }
         if (err == hipSuccess && (split || !bind_events())) err = hipEventRecord(sp.done, s);
-        if (err == hipSuccess) sp.last = s;
+        if (err == hipSuccess) sp.last.set(s);
         if (err != hipSuccess) {
             // binning passes of this batch may already be queued on s: let them finish before the
             // next batch clears the counters (sched_reserve's dirty path waits on sp.done only)
@@ -1274,7 +1297,7 @@ static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, c
                   uint32_t max_wires, uint32_t* d_nwires, int32_t* d_pk_status, uint32_t key_hint, hipStream_t s) {
     TxSpace& tx = e->tx;
     HIP_TRY(tx_reserve(e, npk, ntun, max_wires));
-    if (tx.last != s) HIP_TRY(hipStreamWaitEvent(s, tx.done, 0));
+    if (!tx.last.same(s)) HIP_TRY(hipStreamWaitEvent(s, tx.done, 0));
     HIP_TRY(neb_tx_plan(d_pk, npk, d_in, d_tun, ntun, e->d_keys, e->max_keys, alg, &tx.ws, out_cap, max_wires,
                         d_pk_status, d_nwires, s));
     // one tunnel key with AES-GCM: the seal sums the payload into the L4 checksums itself, so the
@@ -1287,7 +1310,7 @@ static int tx_run(neb_engine* e, int alg, neb_tx_tunnel* d_tun, uint32_t ntun, c
                          cs ? 2 : (int)neb::kTxSealFromInput));
     HIP_TRY(neb_tx_finish(d_tun, npk, ntun, &tx.ws, s));
     HIP_TRY(hipEventRecord(tx.done, s));
-    tx.last = s;
+    tx.last.set(s);
     return NEB_OK;
 }
 

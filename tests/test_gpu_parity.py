@@ -118,6 +118,34 @@ def test_mixed_key_density_vs_oracle(engine, oracle_mod, alg, n, nkeys, sizes, r
     assert np.array_equal(got_o, ref_o)
 
 
+# every binning path of the mixed-key scheduler (sched.hip), forced by its per-batch knobs: the radix
+# sort (large batches), the one-launch histogram with one or kSubBins words per bin, three launches
+BINNING = {"sorted": {"NEB_SCHED_SORT_FROM": "0"},
+           "fused": {"NEB_SCHED_SORT_FROM": "4000000000"},
+           "fused_subbins": {"NEB_SCHED_SORT_FROM": "4000000000", "NEB_SUB_BINS_FROM": "0"},
+           "three_launches": {"NEB_SCHED_SORT_FROM": "4000000000", "NEB_SCHED_FUSED": "0", "NEB_SUB_BINS_FROM": "0"}}
+
+
+@pytest.mark.parametrize("path", sorted(BINNING))
+@pytest.mark.parametrize("n,nkeys,sizes,ratio", [
+    (4096, 256, (1300,), (1,)),
+    (6000, 24, (0, 1, 16, 17, 48, 49, 112, 113, 240, 241, 496, 497, 1008, 1009, 2032, 2033), (1,) * 16),
+])
+def test_binning_paths_vs_oracle(engine, oracle_mod, monkeypatch, path, n, nkeys, sizes, ratio):
+    for k, v in BINNING[path].items():
+        monkeypatch.setenv(k, v)
+    b = W.make_batch(L.ALG_AESGCM, n, nkeys, sizes=sizes, ratio=ratio, seed=n ^ nkeys ^ 0x5EED, name="binning")
+    ref, st_ref = oracle_seal(oracle_mod, b)
+    for rep in range(2):  # twice: each path leaves its counters and bins clear for the next batch
+        got, st = run_device(engine, b, seal=True)
+        assert (st == 0).all() and (st_ref == 0).all()
+        assert np.array_equal(got, ref)
+    ref_o, _ = oracle_open(oracle_mod, b, ref)
+    got_o, st_o = run_device(engine, b, seal=False, arena=ref)
+    assert (st_o == 0).all()
+    assert np.array_equal(got_o, ref_o)
+
+
 def _edge_batch(alg, lens, alens, nkeys=3, seed=99):
     rng = np.random.default_rng(seed)
     n = len(lens)
