@@ -12,6 +12,7 @@
 #include <deque>
 #include <cstring>
 #include <cstdlib>
+#include <dlfcn.h>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -66,18 +67,25 @@ extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_
 // ordered after it already and skips the cross-stream wait (a barrier packet that cost ≈ 5 µs between
 // kernels). The handle alone does not name a stream: one destroyed with work still pending is
 // released when the work ends, and a stream created meanwhile may get its address; so the identity
-// is the handle together with HIP's per-stream id.
+// is the handle together with HIP's per-stream id (hipStreamGetId, HIP >= 7.1, looked up at run time:
+// a process may run an older HIP runtime, as PyTorch's wheel does). Without it the handle alone is
+// the identity, and a caller must not destroy a stream while the engine's batches on it are pending
+// (streams).
 struct StreamTag {
+    using GetId = hipError_t (*)(hipStream_t, unsigned long long*);
     hipStream_t h = nullptr;
-    unsigned long long id = ~0ull;
+    unsigned long long id = 0;
+    bool valid = false;
     static unsigned long long id_of(hipStream_t s) {
-        unsigned long long v = ~0ull;
-        return hipStreamGetId(s, &v) == hipSuccess ? v : ~0ull;
+        static const GetId get = (GetId)dlsym(RTLD_DEFAULT, "hipStreamGetId");
+        unsigned long long v = 0;
+        return get && get(s, &v) == hipSuccess ? v : 0ull;
     }
-    bool same(hipStream_t s) const { return id != ~0ull && h == s && id_of(s) == id; }
+    bool same(hipStream_t s) const { return valid && h == s && id_of(s) == id; }
     void set(hipStream_t s) {
         h = s;
         id = id_of(s);
+        valid = true;
     }
 };
 
@@ -736,8 +744,7 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up(((size_t)mc + ms) * 16u, 256);
     const size_t b_sums = (size_t)cap * 16u, b_sdesc = align_up((size_t)cap * sizeof(neb_desc), 256);
-    const size_t b_sort = align_up(neb::sched_sort_tmp_bytes(cap, e->max_keys), 256);  // 0: no sorted binning
-    const size_t bytes = b_counters + b_base + 4 * b_idx + b_chunks + b_sums + b_sdesc + b_sort;
+    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_sums + b_sdesc;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
     if (sp.mem) hipFree(sp.mem);
@@ -762,11 +769,6 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     sp.ws.sums = (uint4*)m;
     m += b_sums;
     sp.ws.sdesc = (neb_desc*)m;
-    m += b_sdesc;
-    sp.ws.vals = (uint32_t*)m;
-    m += b_idx;
-    sp.ws.sort_tmp = b_sort ? m : nullptr;
-    sp.ws.sort_tmp_bytes = b_sort;
     sp.ws.max_chunks = mc;
     sp.ws.max_short = ms;
     sp.bytes = bytes;

@@ -107,10 +107,26 @@ struct RxSort {
 // Per packet: its window (or count: none) and counter, and the first pass's digit counts per
 // workgroup (packet e = b * per_blk + j * 256 + t). Also clears the window flags, the admitted
 // count and the later passes' digit counts (the grid covers the packets and the windows).
+// Workgroups from kgrid on insert the packets' (window, counter) keys into the first-occurrence table,
+// one packet per thread, and mark a window whose counter is near the wrap for the host (the
+// scan-admit reads both). Nothing else in the launch reads the table, so the inserts run beside the
+// keys work instead of after it: inside the keys workgroups' loop (4 packets per thread on 64
+// workgroups) they cost 33-35 µs on C3, as a launch of their own 14 after the keys' 8.
 __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict__ desc, RxDevWin win, RxDevWs ws,
-                                                      RxSort so) {
+                                                      RxSort so, uint32_t kgrid) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t s_mixed;
+    if (blockIdx.x >= kgrid) {
+        const uint32_t e = (blockIdx.x - kgrid) * 256u + threadIdx.x;
+        if (e >= so.n) return;
+        const uint32_t k = desc[e].key_id;
+        if (k >= win.count || !win.present[k]) return;
+        const uint64_t c = desc[e].counter;
+        const uint32_t h = rx_slot_insert(ws, win, desc, e, k, c);
+        atomicMax(reinterpret_cast<unsigned long long*>(ws.tab_min + h), ((unsigned long long)ws.gen << 32) | (0xFFFFFFFFu - e));
+        if (c >= kRxRiskyCounter) atomicMax(ws.wrisky + k, ws.gen);
+        return;
+    }
     const uint32_t t = threadIdx.x, b = blockIdx.x;
     hist[t] = 0;
     if (t == 0) s_mixed = 0;
@@ -159,14 +175,6 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
             ws.ctr[e] = ctr[r];
             differs |= w != w0;
             atomicAdd(&hist[(w >> so.shift[0]) & mask], 1u);
-            if (w < win.count) {
-                // the (window, counter) key into the first-occurrence table, and a counter near the
-                // wrap marks its window for the host (the scan-admit reads both after this launch)
-                const uint32_t h = rx_slot_insert(ws, win, desc, e, w, ctr[r]);
-                atomicMax(reinterpret_cast<unsigned long long*>(ws.tab_min + h),
-                          ((unsigned long long)ws.gen << 32) | (0xFFFFFFFFu - e));
-                if (ctr[r] >= kRxRiskyCounter) atomicMax(ws.wrisky + w, ws.gen);
-            }
         }
     }
     if (differs) s_mixed = 1u;
@@ -721,7 +729,7 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
         sh += so.bits[p];
     }
     const uint32_t kgrid = std::max<uint32_t>(so.nblk, (win->count + so.per_blk - 1) / so.per_blk);
-    hipLaunchKernelGGL(neb::rx_keys_kernel, dim3(kgrid), dim3(256), 0, s, d_desc, *win, *ws, so);
+    hipLaunchKernelGGL(neb::rx_keys_kernel, dim3(kgrid + (n + 255u) / 256u), dim3(256), 0, s, d_desc, *win, *ws, so, kgrid);
     // pass p writes the run arrays when (passes - 1 - p) is even, so the last pass ends there
     for (uint32_t p = 0; p < so.passes; p++) {
         const bool to_run = ((so.passes - 1 - p) & 1u) == 0;

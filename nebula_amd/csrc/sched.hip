@@ -5,7 +5,6 @@
 #include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
-#include <hipcub/device/device_radix_sort.hpp>
 
 #include "sched.hpp"
 
@@ -23,24 +22,28 @@ __device__ __forceinline__ uint32_t size_class(const neb_desc& d, uint32_t lpp) 
 // execute at the memory side (MI355X_MICROARCH.md, global atomics), ≈55 µs per 1 Mi packets each.
 // SUB: sub-bins per bin for this batch (kSubBins for large batches, 1 for small ones: the contention
 // the sub-bins spread is a large batch's, and pass 2 reads SUB words per bin)
-// blk / nblk: this workgroup's index among the nblk that run the pass
 template <uint32_t SUB>
-__device__ __forceinline__ void sched_hist_body(const neb_desc* __restrict__ desc, uint32_t n, uint32_t max_keys,
-                                                uint32_t lpp, const SchedWs& ws, uint32_t blk, uint32_t nblk) {
+__global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn,
+                                  uint32_t max_keys, uint32_t lpp, SchedWs ws) {
+    // the cursors are cleared here (the previous batch's crypto kernel has finished with them);
+    // the bin counts were cleared by the previous batch's pass 2 as it read them
+    if (blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < kSchedCounters; i += blockDim.x) ws.counters[i] = 0;
+    if (dn) n = min(n, *dn);
     // Neighbouring lanes in the same bin (a batch already grouped by key, e.g. a receive batch in
     // its windows' order) add their count once: the run's first lane adds the run's length and
     // hands each lane its rank (one returning atomic per run instead of one per packet on the
     // same word). Every lane of a wave runs every pass (the shuffles), valid lanes are a prefix.
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t upto = lane == 63u ? ~0ull : (2ull << lane) - 1u;  // lanes <= this one
-    for (uint32_t i0 = blk * blockDim.x; i0 < n; i0 += nblk * blockDim.x) {
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {
         const uint32_t i = i0 + threadIdx.x;
         const bool valid = i < n;
         uint32_t b = 0xFFFFFFFFu;
         if (valid) {
             const neb_desc d = desc[i];
             const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
-            b = (size_class(d, lpp) * (max_keys + 1u) + key) * SUB + (blk & (SUB - 1u));
+            b = (size_class(d, lpp) * (max_keys + 1u) + key) * SUB + (blockIdx.x & (SUB - 1u));
         }
         const uint32_t pb = (uint32_t)__shfl_up((int)b, 1);
         const bool head = valid && (lane == 0u || pb != b);
@@ -58,40 +61,23 @@ __device__ __forceinline__ void sched_hist_body(const neb_desc* __restrict__ des
         }
     }
 }
-template <uint32_t SUB>
-__global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn,
-                                  uint32_t max_keys, uint32_t lpp, SchedWs ws) {
-    // the cursors are cleared here (the previous batch's crypto kernel has finished with them);
-    // the bin counts were cleared by the previous batch's pass 2 as it read them
-    if (blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i < kSchedCursors; i += blockDim.x) ws.counters[i] = 0;
-    if (dn) n = min(n, *dn);
-    sched_hist_body<SUB>(desc, n, max_keys, lpp, ws, blockIdx.x, gridDim.x);
-}
 
 // pass 2: every non-empty bin reserves its range of `sorted` and its chunks. The reservations are
 // aggregated per workgroup (block scans, then one atomic per counter and workgroup): one atomic per
 // bin put ~4096 returning atomics on a single word for a 4096-tunnel batch.
 constexpr int kAllocThreads = 256;
-// SORTED (the sorted binning, SUB = 1): the packets are in bin order already; hist[b] holds the end
-// of bin b's range in `sorted` and base[b] its start (sched_bounds_kernel), so no range is reserved.
-template <uint32_t SUB, bool SORTED = false>
-__device__ __forceinline__ void sched_alloc_body(uint32_t max_keys, const SchedWs& ws, uint32_t blk) {
+template <uint32_t SUB>
+__global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
     using Scan = hipcub::BlockScan<uint32_t, kAllocThreads>;
     __shared__ typename Scan::TempStorage tmp;
     __shared__ uint32_t wg_base[4];
     const uint32_t nb = sched_nbins(max_keys);
-    const uint32_t b = blk * kAllocThreads + threadIdx.x;  // the workgroups cover the bins exactly once
-    uint32_t sc[SUB], c = 0, start = 0;
+    const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
+    uint32_t sc[SUB], c = 0;
 #pragma unroll
     for (uint32_t j = 0; j < SUB; j++) {
         sc[j] = b < nb ? ws.hist[b * SUB + j] : 0u;
         c += sc[j];
-    }
-    if constexpr (SORTED) {
-        static_assert(SUB == 1, "the sorted binning counts in one word per bin");
-        if (c) start = ws.base[b];
-        c = c ? c - start : 0u;
     }
     if (c)  // clear for the next batch
 #pragma unroll
@@ -119,21 +105,20 @@ __device__ __forceinline__ void sched_alloc_body(uint32_t max_keys, const SchedW
     __syncthreads();
     Scan(tmp).ExclusiveSum(nshort, off_s, tot_s);
     if (threadIdx.x == 0) {
-        wg_base[0] = !SORTED && tot_p ? atomicAdd(&ws.counters[kCntPackets], tot_p) : 0u;
+        wg_base[0] = tot_p ? atomicAdd(&ws.counters[kCntPackets], tot_p) : 0u;
         wg_base[1] = tot_f ? atomicAdd(&ws.counters[kCntFrontChunks], tot_f) : 0u;
         wg_base[2] = tot_l ? atomicAdd(&ws.counters[kCntBackChunks], tot_l) : 0u;
         wg_base[3] = tot_s ? atomicAdd(&ws.counters[kCntShortChunks], tot_s) : 0u;
     }
     __syncthreads();
     if (c == 0u) return;
-    const uint32_t base = SORTED ? start : wg_base[0] + off_p;
+    const uint32_t base = wg_base[0] + off_p;
     uint32_t sb = base;
-    if constexpr (!SORTED)
 #pragma unroll
-        for (uint32_t j = 0; j < SUB; j++) {
-            ws.base[b * SUB + j] = sb;
-            sb += sc[j];
-        }
+    for (uint32_t j = 0; j < SUB; j++) {
+        ws.base[b * SUB + j] = sb;
+        sb += sc[j];
+    }
     const uint32_t cf = wg_base[1] + off_f;
     for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
         ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));
@@ -147,113 +132,15 @@ __device__ __forceinline__ void sched_alloc_body(uint32_t max_keys, const SchedW
         }
     }
 }
-template <uint32_t SUB, bool SORTED = false>
-__global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
-    sched_alloc_body<SUB, SORTED>(max_keys, ws, blockIdx.x);
-}
-
-// ---- sorted binning (batches of >= kSchedSortFrom packets) ----
-// 1. each packet's bin number and index (and the cursors cleared);
-// 2. a radix sort of (bin, index) over the bin number's bits (hipcub / rocPRIM onesweep: per-
-//    workgroup LDS histograms and a decoupled look-back, no per-packet global atomic);
-// 3. each bin's range in the sorted order from the run boundaries (hist[b] = end, base[b] = start);
-// 4. the allocation pass (SORTED) cuts the ranges into chunks as before.
-__global__ void sched_sortkey_kernel(const neb_desc* __restrict__ desc, uint32_t n, uint32_t max_keys, uint32_t lpp,
-                                     SchedWs ws) {
-    if (blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i < kSchedCursors; i += blockDim.x) ws.counters[i] = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const neb_desc d = desc[i];
-        const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
-        ws.binof[i] = size_class(d, lpp) * (max_keys + 1u) + key;
-        ws.vals[i] = i;
-    }
-}
-__global__ void sched_bounds_kernel(const uint32_t* __restrict__ skey, uint32_t n, SchedWs ws) {
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        const uint32_t b = skey[j];
-        if (j == 0u || skey[j - 1u] != b) ws.base[b] = j;
-        if (j + 1u == n || skey[j + 1u] != b) ws.hist[b] = j + 1u;
-    }
-}
-static uint32_t sched_bin_bits(uint32_t max_keys) {
-    const uint32_t nb = sched_nbins(max_keys);
-    uint32_t bits = 1;
-    while ((1u << bits) < nb) bits++;
-    return bits;
-}
 
 // pass 3: scatter packet indices and descriptors into their bin's range, at the rank pass 1 drew
-__device__ __forceinline__ void sched_scatter_body(const neb_desc* __restrict__ desc, uint32_t n, const SchedWs& ws,
-                                                   uint32_t blk, uint32_t nblk) {
-    for (uint32_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
+__global__ void sched_scatter_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn, SchedWs ws) {
+    if (dn) n = min(n, *dn);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t j = ws.base[ws.binof[i]] + ws.binpos[i];
         ws.sorted[j] = i;
         if (ws.sdesc) ws.sdesc[j] = desc[i];
     }
-}
-__global__ void sched_scatter_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn, SchedWs ws) {
-    if (dn) n = min(n, *dn);
-    sched_scatter_body(desc, n, ws, blockIdx.x, gridDim.x);
-}
-
-// The three passes in one launch. A workgroup's role comes from a ticket (an atomic on the
-// workgroup's first wave), not from blockIdx: tickets [0, H) count, [H, H + A) allocate, the rest
-// scatter. A workgroup waits only for workgroups with smaller tickets, which have all started (they
-// drew theirs) and wait for nothing later, so the launch cannot deadlock however the hardware
-// places or orders its workgroups. Each hand-off is a release by every producing workgroup (its
-// waves' stores drained, a barrier, one agent-scope release and a counter add) and one acquire on
-// the consuming workgroup after its poll (MI355X_MICROARCH.md, valid hand-off forms). Against three
-// launches this drops two kernel boundaries and the ramp of two small grids.
-constexpr uint32_t kSchedSpinLimit = 1u << 24;  // polls (≈ 1 s): a bound for a broken invariant, never reached
-__device__ __forceinline__ void sched_signal(uint32_t* ctr) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-__device__ __forceinline__ void sched_wait(uint32_t* ctr, uint32_t target) {
-    if (threadIdx.x == 0) {
-        for (uint32_t k = 0; k < kSchedSpinLimit; k++) {
-            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-            __builtin_amdgcn_s_sleep(4);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
-template <uint32_t SUB>
-__global__ __launch_bounds__(kAllocThreads) void sched_fused_kernel(const neb_desc* __restrict__ desc, uint32_t n,
-                                                                    const uint32_t* dn, uint32_t max_keys, uint32_t lpp,
-                                                                    SchedWs ws, uint32_t H, uint32_t A) {
-    __shared__ uint32_t s_ticket;
-    if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(&ws.counters[kCntTicket], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t t = s_ticket;
-    if (dn) n = min(n, *dn);
-    if (t < H) {
-        // the cursors are cleared by the first counting workgroup (the previous batch's crypto
-        // kernel has finished with them; the allocation adds to them only after every count)
-        if (t == 0u && threadIdx.x < kSchedCursors)
-            __hip_atomic_store(&ws.counters[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sched_hist_body<SUB>(desc, n, max_keys, lpp, ws, t, H);
-        sched_signal(&ws.counters[kCntHistDone]);
-    } else if (t < H + A) {
-        sched_wait(&ws.counters[kCntHistDone], H);
-        sched_alloc_body<SUB>(max_keys, ws, t - H);
-        sched_signal(&ws.counters[kCntAllocDone]);
-    } else {
-        sched_wait(&ws.counters[kCntAllocDone], A);
-        sched_scatter_body(desc, n, ws, t - H - A, gridDim.x - H - A);
-    }
-    // the last workgroup out clears the tickets and hand-off counters for the next batch
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(&ws.counters[kCntExit], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u)
-        for (uint32_t i = kCntTicket; i <= kCntExit; i++)
-            __hip_atomic_store(&ws.counters[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Descriptors of a shard whose engine disagrees with engine 0 on some key slots (engine.cpp
@@ -278,52 +165,16 @@ extern "C" hipError_t neb_fence_keys(const neb_desc* in, neb_desc* out, uint32_t
     return hipGetLastError();
 }
 
-size_t neb::sched_sort_tmp_bytes(uint32_t n, uint32_t max_keys) {
-    size_t bytes = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0,
-                                           (int)sched_bin_bits(max_keys)) != hipSuccess)
-        return 0;
-    return bytes;
-}
-
 extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
                                       uint32_t lpp, const neb::SchedWs* ws, hipStream_t s) {
     const uint32_t nb = neb::sched_nbins(max_keys);
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
     const dim3 ga((nb + neb::kAllocThreads - 1) / neb::kAllocThreads), ta(neb::kAllocThreads);
-    const char* bv = std::getenv("NEB_SUB_BINS_FROM");  // <packets> (read per batch): the A/B of the threshold
+    // NEB_SUB_BINS_FROM=<packets> (read per batch): the A/B of the threshold, and the tests' coverage
+    // of both counting layouts
+    const char* bv = std::getenv("NEB_SUB_BINS_FROM");
     const uint32_t from = bv ? (uint32_t)std::strtoul(bv, nullptr, 10) : neb::kSubBinsFrom;
-    // NEB_SCHED_SORT_FROM=<packets> and NEB_SCHED_FUSED=0 (read per batch): the A/Bs and the tests'
-    // coverage of every binning path
-    const char* sv = std::getenv("NEB_SCHED_SORT_FROM");
-    const uint32_t sort_from = sv ? (uint32_t)std::strtoul(sv, nullptr, 10) : neb::kSchedSortFrom;
-    // the sorted binning needs the packet count on the host (d_n: a count known only on the device)
-    if (!d_n && n >= sort_from && ws->sort_tmp && ws->vals) {
-        const uint32_t g = (n + tpb - 1) / tpb < 2048u ? (n + tpb - 1) / tpb : 2048u;
-        hipLaunchKernelGGL(neb::sched_sortkey_kernel, dim3(g), dim3(tpb), 0, s, d_desc, n, max_keys, lpp, *ws);
-        size_t tb = ws->sort_tmp_bytes;
-        hipError_t err = hipcub::DeviceRadixSort::SortPairs(ws->sort_tmp, tb, ws->binof, ws->binpos, ws->vals, ws->sorted,
-                                                            n, 0, (int)neb::sched_bin_bits(max_keys), s);
-        if (err != hipSuccess) return err;
-        hipLaunchKernelGGL(neb::sched_bounds_kernel, dim3(g), dim3(tpb), 0, s, ws->binpos, n, *ws);
-        hipLaunchKernelGGL((neb::sched_alloc_kernel<1, true>), ga, ta, 0, s, max_keys, *ws);
-        return hipGetLastError();
-    }
-    const char* fv = std::getenv("NEB_SCHED_FUSED");
-    const bool fused = !(fv && fv[0] == '0');
-    if (fused) {
-        // counting: up to 4096 workgroups; scattering: up to 1024 (grid-stride), behind the counts
-        const uint32_t H = gp, A = ga.x, S = gp < 1024u ? gp : 1024u;
-        if (n >= from)
-            hipLaunchKernelGGL(neb::sched_fused_kernel<neb::kSubBins>, dim3(H + A + S), ta, 0, s, d_desc, n, d_n, max_keys,
-                               lpp, *ws, H, A);
-        else
-            hipLaunchKernelGGL(neb::sched_fused_kernel<1>, dim3(H + A + S), ta, 0, s, d_desc, n, d_n, max_keys, lpp, *ws, H,
-                               A);
-        return hipGetLastError();
-    }
     if (n >= from) {
         hipLaunchKernelGGL(neb::sched_hist_kernel<neb::kSubBins>, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp,
                            *ws);

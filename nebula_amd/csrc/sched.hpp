@@ -42,14 +42,7 @@ constexpr uint32_t kCntPackets = 0;      // cursor into sorted[]
 constexpr uint32_t kCntFrontChunks = 1;  // chunks of groups at 4 lanes per packet, chunks[0, F)
 constexpr uint32_t kCntBackChunks = 2;   // long tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
 constexpr uint32_t kCntShortChunks = 3;  // short tails, chunks[max_chunks + j] (sched_tail_long)
-constexpr uint32_t kSchedCursors = 4;    // the slots above: cleared by every batch's binning
-// the one-launch binning (sched.hip sched_fused_kernel): workgroup tickets and the hand-offs between
-// its three phases; the last workgroup out clears them for the next batch
-constexpr uint32_t kCntTicket = 4;
-constexpr uint32_t kCntHistDone = 5;   // histogram workgroups finished
-constexpr uint32_t kCntAllocDone = 6;  // allocation workgroups finished
-constexpr uint32_t kCntExit = 7;       // workgroups finished
-constexpr uint32_t kSchedCounters = 8;
+constexpr uint32_t kSchedCounters = 4;
 
 // Each bin counts its packets in kSubBins sub-bins (sub-bin = the counting workgroup's index mod
 // kSubBins), so the returning atomics of one bin's packets spread over kSubBins words: a 4096-key
@@ -78,9 +71,6 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
                           // a group's descriptors one contiguous read instead of a gather behind the index
     uint4* chunks;        // [max_chunks + max_short] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
     uint4* sums;          // [n] the open's GHASH values between the split passes (aes_gcm.hip gcm_ctr_kernel)
-    uint32_t* vals;       // [n] the radix sort's input values (packet indices; the sorted binning)
-    void* sort_tmp;       // the radix sort's temporary storage (sort_tmp_bytes, sized for n_cap packets)
-    size_t sort_tmp_bytes;
     uint32_t max_chunks;  // fronts from 0 up, long tails from max_chunks - 1 down
     uint32_t max_short;   // short tails from max_chunks up
 };
@@ -101,22 +91,10 @@ __host__ __device__ inline uint32_t sched_max_short(uint32_t n, uint32_t max_key
 // ahead of "short" (1300 B at 16 lanes: 6 rounds; everything shorter).
 __host__ __device__ inline bool sched_tail_long(uint32_t cls, uint32_t lg) { return cls >= lg + 2u; }
 
-// Batches of at least kSchedSortFrom packets are binned by a radix sort of their bin numbers instead
-// of the histogram's returning atomics (sched.hip, sorted binning): a scattered 4-B atomic leaves L2
-// as a memory-side request of its own, ≈ 20 G of them per second chip-wide, so 1 Mi packets' ranks
-// cost ≈ 50 µs whatever the contention (47 µs measured for C5's histogram pass).
-#ifndef NEB_SCHED_SORT_FROM
-#define NEB_SCHED_SORT_FROM (1u << 18)
-#endif
-constexpr uint32_t kSchedSortFrom = NEB_SCHED_SORT_FROM;
-// temporary storage of the sorted binning for up to n packets (0 on failure)
-size_t sched_sort_tmp_bytes(uint32_t n, uint32_t max_keys);
-
 }  // namespace neb
 
-// Host launcher (sched.hip): the three binning passes on stream s, in one launch (sched_fused_kernel)
-// or, with NEB_SCHED_FUSED=0 (read once, the A/B), as three. The workspace's counters and bin counts
-// must be zero before the first batch (pass 1 clears the cursors and pass 2 the bin counts it reads,
-// so a batch leaves them zero for the next).
+// Host launcher (sched.hip): the three binning passes on stream s. The workspace's counters and
+// bin counts must be zero before the first batch (pass 1 clears the cursors and pass 2 the bin
+// counts it reads, so a batch leaves them zero for the next).
 extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
                                       uint32_t lpp, const neb::SchedWs* ws, hipStream_t s);

@@ -118,12 +118,9 @@ def test_mixed_key_density_vs_oracle(engine, oracle_mod, alg, n, nkeys, sizes, r
     assert np.array_equal(got_o, ref_o)
 
 
-# every binning path of the mixed-key scheduler (sched.hip), forced by its per-batch knobs: the radix
-# sort (large batches), the one-launch histogram with one or kSubBins words per bin, three launches
-BINNING = {"sorted": {"NEB_SCHED_SORT_FROM": "0"},
-           "fused": {"NEB_SCHED_SORT_FROM": "4000000000"},
-           "fused_subbins": {"NEB_SCHED_SORT_FROM": "4000000000", "NEB_SUB_BINS_FROM": "0"},
-           "three_launches": {"NEB_SCHED_SORT_FROM": "4000000000", "NEB_SCHED_FUSED": "0", "NEB_SUB_BINS_FROM": "0"}}
+# both counting layouts of the mixed-key scheduler (sched.hip), forced by its per-batch knob: one
+# count word per bin, or kSubBins
+BINNING = {"one_word": {"NEB_SUB_BINS_FROM": "4000000000"}, "subbins": {"NEB_SUB_BINS_FROM": "0"}}
 
 
 @pytest.mark.parametrize("path", sorted(BINNING))
