@@ -192,8 +192,9 @@ def cpu_baseline(b, target_s: float = 4.0):
         "sample": f"{n} packets of the same batch ({payload / 1e6:.1f} MB payload), seal x{iters} + open x{iters} "
                   f"({tt:.1f} s) on {best} pinned threads, the best of a sweep up to all {threads} CPUs of this "
                   f"process's affinity ('sweep'), and x{iters1} on 1 thread ({tt1:.1f} s); OpenSSL EVP "
-                  f"{'AES-256-GCM' if b.alg == 1 else 'ChaCha20-Poly1305'} (AES-NI/VAES + PCLMUL class, as Go's "
-                  f"crypto/cipher), {model}",
+                  + ("AES-256-GCM (AES-NI/VAES + PCLMUL class, as Go's crypto/cipher)" if b.alg == 1 else
+                     "ChaCha20-Poly1305 (AVX2 / AVX-512 SIMD class, as golang.org/x/crypto/chacha20poly1305)")
+                  + f", {model}",
     }
 
 

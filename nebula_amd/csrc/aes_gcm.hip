@@ -1207,10 +1207,16 @@ struct OneArgs {
     uint8_t in[kOneBytes];  // 16-B aligned within the argument block
 };
 static_assert(offsetof(OneArgs, in) % 16 == 0, "the packet bytes are read as 16-B blocks");
+// The 64 KiB T-table image is filled by NEB_ONE_FILL_WAVES waves (the packet's one wave alone spent
+// most of the kernel on it); the others leave after the fill.
+#ifndef NEB_ONE_FILL_WAVES
+#define NEB_ONE_FILL_WAVES 4
+#endif
+constexpr uint32_t kOneFillThreads = NEB_ONE_FILL_WAVES * kWave;
 template <bool OPEN>
-__global__ __launch_bounds__(kWave) void gcm_one_kernel(OneArgs a) {
+__global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     __shared__ TailLds lds;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1u);
     // the argument block in place (a by-value struct indexed per lane would be copied to scratch)
     // the block's address as an opaque integer: derived from the constant-address kernarg pointer,
     // the output address (base + dst_off) would let the compiler treat the result stores as stores
@@ -1220,20 +1226,21 @@ __global__ __launch_bounds__(kWave) void gcm_one_kernel(OneArgs a) {
     const uint8_t* ka = reinterpret_cast<const uint8_t*>(kb);
     const uint32_t key = a.key;
     const uint32_t* srec = a.keys + (size_t)(key < a.max_keys ? key : 0u) * kKeyRecDwords;
-    // T-tables, 16 entries per lane at a time (loads before stores, as fill_ttab)
-    for (uint32_t j0 = 0; j0 < 256u * 32u; j0 += 16u * kWave) {
+    // T-tables, 16 entries per thread at a time (loads before stores, as fill_ttab)
+    for (uint32_t j0 = 0; j0 < 256u * 32u; j0 += 16u * kOneFillThreads) {
         uint2 v[16];
 #pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) v[j] = ttab_entry(j0 + j * kWave + lane);
+        for (uint32_t j = 0; j < 16u; j++) v[j] = ttab_entry(j0 + j * kOneFillThreads + tid);
 #pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) lds.ttab[j0 + j * kWave + lane] = v[j];
+        for (uint32_t j = 0; j < 16u; j++) lds.ttab[j0 + j * kOneFillThreads + tid] = v[j];
     }
-    for (uint32_t tdx = lane; tdx < 16u * kTailLg; tdx += kWave)  // M[v] of H^(2^j), j < kTailLg
+    for (uint32_t tdx = tid; tdx < 16u * kTailLg; tdx += kOneFillThreads)  // M[v] of H^(2^j), j < kTailLg
         lds.shoup[tdx] = ld_rec4(srec, rec_shoup_pow2(tdx >> 4) + 4u * (tdx & 15u));
-    for (uint32_t tdx = lane; tdx < 128u; tdx += kWave) lds.pos[tdx] = ld_rec4(srec, kRecPos64 + 4u * tdx);
+    for (uint32_t tdx = tid; tdx < 128u; tdx += kOneFillThreads) lds.pos[tdx] = ld_rec4(srec, kRecPos64 + 4u * tdx);
+    __syncthreads();
+    if (tid >= kWave) return;  // the packet is one wave's
     uint32_t rks[60];
     load_round_keys(srec, rks);
-    __syncthreads();
     const TLook T{lds.ttab, ttab_lane_base(lane)};
     const GhShoup gh{lds.shoup, lds.pos};
     const bool key_ok = key < a.max_keys && __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
@@ -2179,9 +2186,9 @@ extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len
     a.status = status;
     a.d.dst_off = (uint64_t)(uintptr_t)out;  // the output's address: the kernel rebases it on its argument block
     if (open)
-        hipLaunchKernelGGL(neb::gcm_one_kernel<true>, dim3(1), dim3(neb::kWave), 0, s, a);
+        hipLaunchKernelGGL(neb::gcm_one_kernel<true>, dim3(1), dim3(neb::kOneFillThreads), 0, s, a);
     else
-        hipLaunchKernelGGL(neb::gcm_one_kernel<false>, dim3(1), dim3(neb::kWave), 0, s, a);
+        hipLaunchKernelGGL(neb::gcm_one_kernel<false>, dim3(1), dim3(neb::kOneFillThreads), 0, s, a);
     return hipGetLastError();
 }
 
