@@ -127,6 +127,8 @@ BINNING = {"one_word": {"NEB_SUB_BINS_FROM": "4000000000"}, "subbins": {"NEB_SUB
 @pytest.mark.parametrize("n,nkeys,sizes,ratio", [
     (4096, 256, (1300,), (1,)),
     (6000, 24, (0, 1, 16, 17, 48, 49, 112, 113, 240, 241, 496, 497, 1008, 1009, 2032, 2033), (1,) * 16),
+    # IMIX over 1000 keys, 21 sub-bin workgroups' worth
+    (21000, 1000, (90, 576, 1300), (7, 4, 1)),
 ])
 def test_binning_paths_vs_oracle(engine, oracle_mod, monkeypatch, path, n, nkeys, sizes, ratio):
     for k, v in BINNING[path].items():
