@@ -119,6 +119,9 @@ NEB_API int neb_engine_stats(const neb_engine* e, uint64_t stats[4]);
 NEB_API const char* neb_strerror(int rc);
 /* Detail of the last NEB_ERR_HIP / NEB_ERR_NO_DEVICE on the calling thread (HIP error string). */
 NEB_API const char* neb_last_error(void);
+/* The first 16 hex digits of the SHA-256 of the library's sources (nebula_amd/Makefile SRC then
+ * HDR, concatenated) it was built from: a test compares it with the sources beside it. */
+NEB_API const char* neb_build_id(void);
 
 /* ---- key install: noise.CipherFunc.Cipher(k) ----------------------------------------------- */
 

@@ -355,6 +355,11 @@ extern "C" {
 
 NEB_API const char* neb_last_error(void) { return g_last_error; }
 
+#ifndef NEB_BUILD_ID
+#define NEB_BUILD_ID "unknown"
+#endif
+NEB_API const char* neb_build_id(void) { return NEB_BUILD_ID; }
+
 NEB_API const char* neb_strerror(int rc) {
     switch (rc) {
         case NEB_OK: return "ok";

@@ -31,6 +31,21 @@ def test_library_exports_every_declared_symbol():
     assert set(syms) == set(L.SIGNATURES), set(syms) ^ set(L.SIGNATURES)
 
 
+def test_library_is_built_from_these_sources():
+    """neb_build_id() is the SHA-256 of the sources the library was compiled from (nebula_amd/Makefile:
+    SRC then HDR, concatenated): equal to the hash of the sources in this tree, so the .so a test
+    run loads (here, or the prebuilt one shipped to a GPU box) is HEAD's code, not a stale build."""
+    import hashlib
+
+    nd = os.path.join(ROOT, "nebula_amd")
+    mk = open(os.path.join(nd, "Makefile")).read()
+    files = []
+    for var in ("SRC", "HDR"):
+        files += re.search(rf"^{var} := (.*)$", mk, re.M).group(1).split()
+    h = hashlib.sha256(b"".join(open(os.path.join(nd, f), "rb").read() for f in files)).hexdigest()[:16]
+    assert L.lib().neb_build_id().decode() == h
+
+
 def test_library_has_no_unresolved_symbols():
     """Binding every symbol at load time (RTLD_NOW) fails on a reference the build left undefined,
     which a lazy load only reports at the first call into it."""
