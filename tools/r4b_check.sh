@@ -3,6 +3,8 @@
 # the mixed-key binning (new = one launch, old = NEB_SCHED_FUSED=0: three launches) on C3 / C5 and on
 # the device receive (C2 / C3), kernel traces of both, and the per-packet sweep.
 # Stops at the first abnormal exit.
+# (Historical: the one-launch binning and NEB_SCHED_FUSED were removed after this A/B; the script
+# records how profiles/r4b/binning1-2 were made.)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r4b; mkdir -p $OUT
 cd $R

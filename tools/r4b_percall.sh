@@ -2,6 +2,7 @@
 # Per-packet A/B: the T-table fill of gcm_one_kernel by 1 / 4 (product) / 8 waves
 # (build_var/one1, one8 via LD_LIBRARY_PATH; queue_bench's RUNPATH yields to it), queue_bench percall
 # at 1-64 threads, alternating, then kernel + HIP traces of the product at 4 threads.
+# (build_var/one1 and one8: tools/build_variant.sh one1 -DNEB_ONE_FILL_WAVES=1, one8 ... =8.)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r4b_pc; mkdir -p $OUT
 cd $R/tools/native || exit 1

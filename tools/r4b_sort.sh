@@ -2,6 +2,8 @@
 # The sorted binning of large mixed-key batches: the GPU suite (log kept), then C5 (and C3 as a
 # control) with the sort (default) against the histogram (NEB_SCHED_SORT_FROM=4000000000),
 # alternating, and kernel traces of both on C5. Stops at the first abnormal exit.
+# (Historical: the sorted binning and NEB_SCHED_SORT_FROM were removed after this A/B; the script
+# records how profiles/r4b/sort was made.)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r4b_sort; mkdir -p $OUT
 cd $R

@@ -2,6 +2,8 @@
 # Sort tile size A/B on C5: prod (4 packets per thread), build_var/items8, build_var/items16 (via
 # NEB_LIB_PATH) and the histogram (NEB_SCHED_SORT_FROM=4000000000), alternating; the binning and
 # full-size parity tests on prod first; a kernel trace of prod. Stops at the first abnormal exit.
+# (Historical: the sorted binning and its NEB_SORT_ITEMS builds were removed after this A/B; the
+# script records how profiles/r4b/sort/ab_items.log was made.)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r4b_sort2; mkdir -p $OUT
 cd $R
