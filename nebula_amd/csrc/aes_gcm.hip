@@ -1011,6 +1011,9 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         // shuffle max of the round counts first was 4-7% slower in the chunk kernel)
         for (uint32_t r = 0; __any(r < sh.R); r++) tround(r);
     };
+#if NEB_ONE_TRACE
+    const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // counter caching needs every block counter of every packet in the wave below 2^8 / 2^16
     if (__all(sh.m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
     else if (__all(sh.m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
@@ -1021,7 +1024,16 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
             cs_fk |= (uint32_t)__shfl_xor((int)cs_fk, (int)sft);
         }
     }
+#if NEB_ONE_TRACE
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t tp1 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
+#if NEB_ONE_TRACE
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t tp2 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) printf("  rounds %u  final %u (x10 ns, R=%u)\n", (unsigned)(tp1 - tp0), (unsigned)(tp2 - tp1), sh.R);
+#endif
     if constexpr (CS) {
         if (run && cs_on && l == LPP - 1u) V = xor4(V, gcm_csum_fix(d, sh.n, sh.na, cs_acc, cs_fk, args.arena, cs_pow));
     }
@@ -1221,11 +1233,18 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     // the block's address as an opaque integer: derived from the constant-address kernarg pointer,
     // the output address (base + dst_off) would let the compiler treat the result stores as stores
     // to constant memory and drop them
+#if NEB_ONE_TRACE  // phase stamps (100 MHz) printed by lane 0: an A/B build only
+    const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint64_t kb = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(kb));
     const uint8_t* ka = reinterpret_cast<const uint8_t*>(kb);
     const uint32_t key = a.key;
     const uint32_t* srec = a.keys + (size_t)(key < a.max_keys ? key : 0u) * kKeyRecDwords;
+    // The packet's bytes (the argument block's 2 KiB, in device memory) are touched by the fill's
+    // threads first, so the rounds' block loads after the fill hit the caches (0.4 µs of 12).
+    uint4 warm = make_uint4(0, 0, 0, 0);
+    if (tid < kOneBytes / 16u) warm = *reinterpret_cast<const uint4*>(ka + offsetof(OneArgs, in) + 16u * tid);
     // T-tables, 16 entries per thread at a time (loads before stores, as fill_ttab)
     for (uint32_t j0 = 0; j0 < 256u * 32u; j0 += 16u * kOneFillThreads) {
         uint2 v[16];
@@ -1237,8 +1256,12 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     for (uint32_t tdx = tid; tdx < 16u * kTailLg; tdx += kOneFillThreads)  // M[v] of H^(2^j), j < kTailLg
         lds.shoup[tdx] = ld_rec4(srec, rec_shoup_pow2(tdx >> 4) + 4u * (tdx & 15u));
     for (uint32_t tdx = tid; tdx < 128u; tdx += kOneFillThreads) lds.pos[tdx] = ld_rec4(srec, kRecPos64 + 4u * tdx);
+    asm volatile("" ::"v"(warm.x), "v"(warm.y), "v"(warm.z), "v"(warm.w));  // the loads complete
     __syncthreads();
     if (tid >= kWave) return;  // the packet is one wave's
+#if NEB_ONE_TRACE
+    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint32_t rks[60];
     load_round_keys(srec, rks);
     const TLook T{lds.ttab, ttab_lane_base(lane)};
@@ -1249,7 +1272,17 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     // the host passed the output's address in dst_off: rebase it on the argument block (wrapping)
     neb_desc d = a.d;
     d.dst_off = a.d.dst_off - (uint64_t)(uintptr_t)base;
+#if NEB_ONE_TRACE
+    const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();
+#endif
     gcm_packet_group<OPEN>(ga, 0u, true, key, key_ok, RkRegs{rks}, gh, T, lane, kTailLg, nullptr, &d);
+#if NEB_ONE_TRACE
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t ts3 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0)
+        printf("one %d: fill %u  keys %u  packet %u  (x10 ns)\n", (int)OPEN, (unsigned)(ts1 - ts0), (unsigned)(ts2 - ts1),
+               (unsigned)(ts3 - ts2));
+#endif
 }
 
 // ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------

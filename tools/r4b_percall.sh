@@ -9,7 +9,7 @@ cd $R/tools/native || exit 1
 timeout -k 10 300 python -u -m pytest $R/tests/test_gpu_cipher_state.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest_cs.log 2>&1
 rc=$?; tail -2 $OUT/pytest_cs.log; [ $rc -ne 0 ] && exit $rc
 for r in 1 2; do
-  for v in prod one1 one8; do
+  for v in ${VARIANTS:-prod one1 one8}; do
     : > $OUT/pc_${v}_$r.jsonl
     for t in 1 4 16 64; do
       if [ $v = prod ]; then
