@@ -807,14 +807,36 @@ __device__ __forceinline__ uint4 tree_final(uint4 A, uint32_t lane, uint32_t lg,
     return shfl4(V, lane & ~((1u << lg) - 1u));
 }
 
-// The single-key tail kernel (64 lanes per packet): Shoup tables of H^(2^i), i < lg, in order, and
-// the position tables of H^(2^lg) for the Horner step.
-struct GhShoup {
-    const uint4* base;
-    const uint4* pos;
+// 64 lanes per packet (the tail and per-packet kernels): lane l = 16a + b needs A_l·H^(64-l) =
+// A_l·H^(16-b)·H^(16(3-a)). Each lane multiplies by its own M_(16-b) (the record's Shoup tables
+// of H^1..H^16, m16), the 16 lanes of a quarter XOR their products (S_a), quarters 0 and 2 multiply
+// by H^16 and then quarters 0 and 1 by H^32, and the quarters XOR: 3 dependent multiplies instead
+// of the tree's 7 (GhShoup, kept for other lane counts). NEB_TAIL_TREE=1 keeps the tree (A/B).
+#ifndef NEB_TAIL_TREE
+#define NEB_TAIL_TREE 0
+#endif
+struct GhShoup64 {
+    const uint4* m16;    // M_1..M_16, 256 B each
+    const uint4* shoup;  // M of H^(2^j), j < 6 (GhShoup's): M_32 is j = 5
+    const uint4* pos;    // position tables of H^64 (the Horner stride)
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
-        return tree_final(A, lane, lg, base, [](uint32_t i) { return i * 256u; });
+#if NEB_TAIL_TREE
+        return tree_final(A, lane, lg, shoup, [](uint32_t i) { return i * 256u; });
+#else
+        const uint32_t b = lane & 15u, a = (lane >> 4) & 3u;
+        uint4 V = gf_mul_shoup(A, (15u - b) * 256u, m16);
+        V = xor4(V, shfl_xor4(V, 8));
+        V = xor4(V, shfl_xor4(V, 4));
+        V = xor4(V, shfl_xor4(V, 2));
+        V = xor4(V, shfl_xor4(V, 1));
+        const uint4 W = gf_mul_shoup(V, 15u * 256u, m16);     // S_a·H^16
+        V = (a & 1u) ? V : W;                                 // quarters 0, 2
+        const uint4 Y = gf_mul_shoup(V, 5u * 256u, shoup);    // ·H^32
+        V = a < 2u ? Y : V;                                   // quarters 0, 1
+        V = xor4(V, shfl_xor4(V, 16));
+        return xor4(V, shfl_xor4(V, 32));
+#endif
     }
 };
 
@@ -1151,8 +1173,8 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
 // The tail pass: the packets after gcm_single_kernel's full passes over args.tail_slots waves (the
 // groups that would otherwise run alone after everything else: 65 565 packets = 4098 groups of 16
 // on 4096 waves), 2^kTailLg lanes per packet: the two-table AES (64 KiB), Horner stride
-// H^(2^kTailLg) on its position tables, the final tree on the Shoup tables of H .. H^(2^(kTailLg-1))
-// (GhShoup). A tail is small and runs on few waves, so its time is one packet's latency: at 64
+// H^(2^kTailLg) on its position tables, the 3-deep final on the Shoup tables of H .. H^16 and H^32
+// (GhShoup64). A tail is small and runs on few waves, so its time is one packet's latency: at 64
 // lanes a 1300-B packet takes 2 rounds instead of 6 at 16 (bench.py --mode tx: 1457 vs 1456
 // superpackets, 0.243 vs 0.207 ms before it).
 constexpr uint32_t kTailLg = 6, kTailPpw = kWave >> kTailLg;
@@ -1168,7 +1190,9 @@ struct TailLds {
     uint2 ttab[256 * 32];       // 64 KiB T-table pairs, 32 copies
     uint4 shoup[kTailLg * 16];  // 1.5 KiB
     uint4 pos[8 * 16];          // 2 KiB
+    uint4 m16[16 * 16];         // 4 KiB: M_1..M_16 (GhShoup64)
 };
+static_assert(kTailLg == 6, "GhShoup64: 64 lanes per packet");
 template <bool OPEN>
 __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(GcmArgs args) {
     __shared__ TailLds lds;
@@ -1190,11 +1214,12 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
         lds.shoup[tid] = ld_rec4(srec, rec_shoup_pow2(j) + 4u * v);
     }
     if (tid < 128u) lds.pos[tid] = ld_rec4(srec, kRecPos64 + 4u * tid);
+    if (tid < 256u) lds.m16[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
     const TLook T{lds.ttab, ttab_lane_base(lane)};
-    const GhShoup gh{lds.shoup, lds.pos};
+    const GhShoup64 gh{lds.m16, lds.shoup, lds.pos};
     const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
     for (uint32_t t = blockIdx.x * kTailWaves + wave; t < tgroups; t += gridDim.x * kTailWaves) {
         const uint32_t p = p0 + kTailPpw * t + (lane >> kTailLg);
@@ -1256,6 +1281,7 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     for (uint32_t tdx = tid; tdx < 16u * kTailLg; tdx += kOneFillThreads)  // M[v] of H^(2^j), j < kTailLg
         lds.shoup[tdx] = ld_rec4(srec, rec_shoup_pow2(tdx >> 4) + 4u * (tdx & 15u));
     for (uint32_t tdx = tid; tdx < 128u; tdx += kOneFillThreads) lds.pos[tdx] = ld_rec4(srec, kRecPos64 + 4u * tdx);
+    for (uint32_t tdx = tid; tdx < 256u; tdx += kOneFillThreads) lds.m16[tdx] = ld_rec4(srec, kRecShoup + 4u * tdx);
     asm volatile("" ::"v"(warm.x), "v"(warm.y), "v"(warm.z), "v"(warm.w));  // the loads complete
     __syncthreads();
     if (tid >= kWave) return;  // the packet is one wave's
@@ -1265,7 +1291,7 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     uint32_t rks[60];
     load_round_keys(srec, rks);
     const TLook T{lds.ttab, ttab_lane_base(lane)};
-    const GhShoup gh{lds.shoup, lds.pos};
+    const GhShoup64 gh{lds.m16, lds.shoup, lds.pos};
     const bool key_ok = key < a.max_keys && __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
     uint8_t* base = const_cast<uint8_t*>(ka + offsetof(OneArgs, in));
     GcmArgs ga{nullptr, 1u, base, a.keys, a.max_keys, key, a.status, nullptr, 0u, 0u};
