@@ -11,7 +11,8 @@ timing is bracketed by a barrier + device sync on both sides and the max over ra
 
 Printed (rank 0, one JSON line): value = (payload sealed + payload opened, all ranks) / time.
 roofline: the seal kernel's algorithmic bytes (2p+32 per packet) / its mean launch time, from HIP
-events recorded on the kernel's stream inside the timed region; traffic = PMC-measured HBM bytes
+events bound to that kernel's own dispatch inside the timed region (neb_time_next_kernel: start and
+stop of the dominant kernel, no marker packets); traffic = PMC-measured HBM bytes
 per launch of this config's seal kernel from profiles/pmc_configs.json, else null.
 cpu_baseline: rank 0, N = 1 only, the OpenSSL-EVP port of the per-packet loop (oracle/) on a
 bounded sample of the same batch: the best of a thread sweep up to every CPU of this process's
@@ -331,32 +332,40 @@ def main():
         db.seal()
         db.open()
     torch.cuda.synchronize()
-    # Kernel durations come from HIP events on the launch stream inside the timed region. A timing
-    # event is a queue marker the GPU processes between the kernels, so events bracket the seal and
-    # open kernels of every EV_EVERY-th step only: the other steps run back-to-back as in
-    # deployment. The events skip the system-scope cache writeback (TimingEvent); a bracket still
-    # holds its marker's own cost, so kernel_ms is an upper bound on the launch duration.
+    # Kernel durations come from HIP events inside the timed region, on the launch stream. On every
+    # EV_EVERY-th step the seal's and the open's dominant kernel (the single-key kernel, the mixed-key
+    # chunk kernel, the ChaCha kernel) carry a start and a stop event bound to their own dispatch
+    # (neb_time_next_kernel -> hipExtLaunchKernel): the kernel's own duration, with no marker packet
+    # in the stream. Without a HIP handle (torch's events as the fallback) the events bracket the
+    # calls as markers instead, and kernel_ms is then an upper bound.
     timed = [i for i in range(args.steps) if i % EV_EVERY == 0]
-    ev = {i: (TimingEvent(), TimingEvent(), TimingEvent()) for i in timed}
+    ev = {i: tuple(TimingEvent() for _ in range(4)) for i in timed}
+    bound = all(x.torch_ev is None for e in ev.values() for x in e)
+    arm = L.lib().neb_time_next_kernel
     barrier()
     torch.cuda.synchronize()
     ts = time.perf_counter()
     for i in range(args.steps):
         e = ev.get(i)
-        if e:
+        if e and bound:
+            arm(e[0].h, e[1].h)
+        elif e:
             e[0].record(stream)
         db.seal()
-        if e:
+        if e and bound:
+            arm(e[2].h, e[3].h)
+        elif e:
             e[1].record(stream)
-        db.open()
-        if e:
             e[2].record(stream)
+        db.open()
+        if e and not bound:
+            e[3].record(stream)
     torch.cuda.synchronize()
     barrier()
     te = time.perf_counter()
     dt = te - ts
-    seal_ms = float(np.mean([a.elapsed_time(m) for a, m, _ in ev.values()]))
-    open_ms = float(np.mean([m.elapsed_time(z) for _, m, z in ev.values()]))
+    seal_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev.values()]))
+    open_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev.values()]))
     st = db.status_host()
     assert (st == 0).all(), "open failed inside the timed region"
     dt = ctrl.max(dt)
@@ -373,8 +382,10 @@ def main():
     elif b.nkeys == 1:
         kern_tag = "gcm_single_tail_kernel<false>" if b.n <= 6144 else "gcm_single_kernel<false, false>"
     else:
-        kern_tag = "sched passes + gcm_chunk_kernel<false> (the whole seal call)" if fused else \
-            "sched passes + gcm_ctr_kernel<false, true> + gcm_ghash_kernel<false> (the whole seal call)"
+        kern_tag = "gcm_chunk_kernel<false> (the binning passes before it excluded)" if fused else \
+            "gcm_ctr_kernel<false, true> (the split passes' first)"
+    if not bound:
+        kern_tag += "; event brackets around the whole seal call (an upper bound)"
     pmc = pmc_config(f"C{cfg + 1}")
     lens = b.desc["len"].astype(np.int64)
     out = {
@@ -402,9 +413,9 @@ def main():
             "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
             "binding": {k: pmc[k] for k in ("lds_busy", "valu_busy", "mean_ns", "source") if k in pmc} if pmc else None,
             "kernel": kern_tag,
-            # the seal call between HIP events on its stream: for mixed keys that is the binning
-            # passes (sched.hip) plus the chunk kernel, so `achieved` is a lower bound there
+            # the seal's dominant kernel between start / stop events bound to its dispatch
             "kernel_ms": round(seal_ms, 4), "open_kernel_ms": round(open_ms, 4),
+            "kernel_timing": "dispatch-bound events" if bound else "marker events around the call",
             "algorithmic_bytes_per_launch": int(alg_bytes),
         },
     }

@@ -122,6 +122,11 @@ NEB_API const char* neb_last_error(void);
 /* The first 16 hex digits of the SHA-256 of the library's sources (nebula_amd/Makefile SRC then
  * HDR, concatenated) it was built from: a test compares it with the sources beside it. */
 NEB_API const char* neb_build_id(void);
+/* Measurement: the next device batch this thread launches binds its dominant kernel's begin and end
+ * to these two HIP events (hipEvent_t, created with timing enabled) instead of recording markers
+ * around it — the single-key kernel, the mixed-key chunk kernel or the ChaCha kernel (a small batch:
+ * its one kernel). NULL, NULL disarms. */
+NEB_API int neb_time_next_kernel(void* start, void* stop);
 
 /* ---- key install: noise.CipherFunc.Cipher(k) ----------------------------------------------- */
 

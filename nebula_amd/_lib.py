@@ -63,6 +63,7 @@ SIGNATURES = {
     "neb_strerror": (C.c_char_p, [_i]),
     "neb_last_error": (C.c_char_p, []),
     "neb_build_id": (C.c_char_p, []),
+    "neb_time_next_kernel": (_i, [_vp, _vp]),
     "neb_cipher_create": (_i, [_vp, _i, _u8p, C.POINTER(_vp)]),
     "neb_cipher_create_batch": (_i, [_vp, _i, _u8p, _u32, _vp]),
     "neb_cipher_create_multi": (_i, [_vp, _u32, _i, _u8p, _vp]),

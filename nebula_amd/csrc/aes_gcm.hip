@@ -33,6 +33,7 @@
 #include "device_common.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
+#include "timing.hpp"
 
 namespace neb {
 
@@ -2120,9 +2121,7 @@ static hipError_t launch_grid_stop(K kern, int threads, uint32_t work_waves, int
     const uint32_t cap = (uint32_t)(per_cu * cu_count);
     const uint32_t grid = want < cap ? want : cap;
     if (grid == 0) return stop ? hipEventRecord(stop, s) : hipSuccess;
-    if (stop) hipExtLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, nullptr, stop, 0, args...);
-    else hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, s, args...);
-    return hipGetLastError();
+    return neb::launch_bound(kern, dim3(grid), dim3(threads), s, stop, args...);
 }
 
 // Waves of gcm_single_kernel's grid for a batch of at most n packets (a full pass is that many
@@ -2148,10 +2147,11 @@ extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int
 // Launch on s; `stop` (optional) completes with the kernel itself: an event bound to the dispatch
 // (hipExtLaunchKernel) instead of a marker packet recorded after it (a barrier with an
 // agent-scope release between two batches, ≈ 3.3 µs).
+// (A timing pair armed by neb_time_next_kernel goes to the batch's first kernel: the main kernel, or
+// the tail kernel of a small batch.)
 template <class K>
 static void launch_k(K kern, dim3 grid, dim3 block, hipStream_t s, hipEvent_t stop, const neb::GcmArgs& a) {
-    if (stop) hipExtLaunchKernelGGL(kern, grid, block, 0, s, nullptr, stop, 0, a);
-    else hipLaunchKernelGGL(kern, grid, block, 0, s, a);
+    (void)neb::launch_bound(kern, grid, block, s, stop, a);
 }
 
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,

@@ -24,6 +24,7 @@
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
 #include "layout.hpp"
+#include "timing.hpp"
 
 namespace neb {
 
@@ -453,9 +454,7 @@ static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStrea
     uint32_t grid = want < cap ? want : cap;
     if (grid == 0) return stop ? hipEventRecord(stop, s) : hipSuccess;
     // stop (optional): bound to the dispatch, so no marker packet follows the batch (hipExtLaunchKernel)
-    if (stop) hipExtLaunchKernelGGL(kern, dim3(grid), dim3(neb::kChThreads), 0, s, nullptr, stop, 0, a);
-    else hipLaunchKernelGGL(kern, dim3(grid), dim3(neb::kChThreads), 0, s, a);
-    return hipGetLastError();
+    return neb::launch_bound(kern, dim3(grid), dim3(neb::kChThreads), s, stop, a);
 }
 
 // One packet (the per-packet path), as neb_gcm_one.

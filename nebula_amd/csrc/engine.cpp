@@ -23,6 +23,7 @@
 #include "host_common.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
+#include "timing.hpp"
 #include "tx.hpp"
 
 // n keys (32 B each, mapped host memory) into the records of key slots slots[0..n): one launch
@@ -255,6 +256,7 @@ struct neb_cipher {
 };
 
 static thread_local char g_last_error[256] = "";
+thread_local neb::KernelTiming neb::g_kernel_timing;  // timing.hpp: armed by neb_time_next_kernel
 
 static void set_error(const char* where, hipError_t err) {
     std::snprintf(g_last_error, sizeof g_last_error, "%s: %s (%d)", where, hipGetErrorString(err), (int)err);
@@ -354,6 +356,12 @@ static hipEvent_t use_event(neb_engine* e, uint32_t key_hint, hipStream_t s) {
 extern "C" {
 
 NEB_API const char* neb_last_error(void) { return g_last_error; }
+
+NEB_API int neb_time_next_kernel(void* start, void* stop) {
+    if ((start == nullptr) != (stop == nullptr)) return NEB_ERR_INVALID;
+    neb::g_kernel_timing = {(hipEvent_t)start, (hipEvent_t)stop};
+    return NEB_OK;
+}
 
 #ifndef NEB_BUILD_ID
 #define NEB_BUILD_ID "unknown"
