@@ -818,8 +818,9 @@ __device__ __forceinline__ uint4 tree_final(uint4 A, uint32_t lane, uint32_t lg,
 #endif
 struct GhShoup64 {
     const uint4* m16;    // M_1..M_16, 256 B each
-    const uint4* shoup;  // M of H^(2^j), j < 6 (GhShoup's): M_32 is j = 5
+    const uint4* shoup;  // M of H^(2^j), j < 6: M_32 is j = 5 (the tree of the A/B build)
     const uint4* pos;    // position tables of H^64 (the Horner stride)
+    const uint4* hi;     // M_16, M_32, M_48: the quarters' powers
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
 #if NEB_TAIL_TREE
@@ -831,10 +832,8 @@ struct GhShoup64 {
         V = xor4(V, shfl_xor4(V, 4));
         V = xor4(V, shfl_xor4(V, 2));
         V = xor4(V, shfl_xor4(V, 1));
-        const uint4 W = gf_mul_shoup(V, 15u * 256u, m16);     // S_a·H^16
-        V = (a & 1u) ? V : W;                                 // quarters 0, 2
-        const uint4 Y = gf_mul_shoup(V, 5u * 256u, shoup);    // ·H^32
-        V = a < 2u ? Y : V;                                   // quarters 0, 1
+        const uint4 W = gf_mul_shoup(V, (a < 3u ? 2u - a : 0u) * 256u, hi);  // S_a·H^(16(3-a))
+        V = a < 3u ? W : V;
         V = xor4(V, shfl_xor4(V, 16));
         return xor4(V, shfl_xor4(V, 32));
 #endif
@@ -1192,6 +1191,7 @@ struct TailLds {
     uint4 shoup[kTailLg * 16];  // 1.5 KiB
     uint4 pos[8 * 16];          // 2 KiB
     uint4 m16[16 * 16];         // 4 KiB: M_1..M_16 (GhShoup64)
+    uint4 hi[3 * 16];           // M_16, M_32, M_48 (GhShoup64)
 };
 static_assert(kTailLg == 6, "GhShoup64: 64 lanes per packet");
 template <bool OPEN>
@@ -1216,11 +1216,12 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     }
     if (tid < 128u) lds.pos[tid] = ld_rec4(srec, kRecPos64 + 4u * tid);
     if (tid < 256u) lds.m16[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
+    if (tid < 48u) lds.hi[tid] = ld_rec4(srec, (tid < 16u ? kRecShoup + 15u * 64u : tid < 32u ? kRecShoup32 : kRecShoup48) + 4u * (tid & 15u));
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
     const TLook T{lds.ttab, ttab_lane_base(lane)};
-    const GhShoup64 gh{lds.m16, lds.shoup, lds.pos};
+    const GhShoup64 gh{lds.m16, lds.shoup, lds.pos, lds.hi};
     const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
     for (uint32_t t = blockIdx.x * kTailWaves + wave; t < tgroups; t += gridDim.x * kTailWaves) {
         const uint32_t p = p0 + kTailPpw * t + (lane >> kTailLg);
@@ -1283,6 +1284,8 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
         lds.shoup[tdx] = ld_rec4(srec, rec_shoup_pow2(tdx >> 4) + 4u * (tdx & 15u));
     for (uint32_t tdx = tid; tdx < 128u; tdx += kOneFillThreads) lds.pos[tdx] = ld_rec4(srec, kRecPos64 + 4u * tdx);
     for (uint32_t tdx = tid; tdx < 256u; tdx += kOneFillThreads) lds.m16[tdx] = ld_rec4(srec, kRecShoup + 4u * tdx);
+    if (tid < 48u)
+        lds.hi[tid] = ld_rec4(srec, (tid < 16u ? kRecShoup + 15u * 64u : tid < 32u ? kRecShoup32 : kRecShoup48) + 4u * (tid & 15u));
     asm volatile("" ::"v"(warm.x), "v"(warm.y), "v"(warm.z), "v"(warm.w));  // the loads complete
     __syncthreads();
     if (tid >= kWave) return;  // the packet is one wave's
@@ -1292,7 +1295,7 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     uint32_t rks[60];
     load_round_keys(srec, rks);
     const TLook T{lds.ttab, ttab_lane_base(lane)};
-    const GhShoup64 gh{lds.m16, lds.shoup, lds.pos};
+    const GhShoup64 gh{lds.m16, lds.shoup, lds.pos, lds.hi};
     const bool key_ok = key < a.max_keys && __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
     uint8_t* base = const_cast<uint8_t*>(ka + offsetof(OneArgs, in));
     GcmArgs ga{nullptr, 1u, base, a.keys, a.max_keys, key, a.status, nullptr, 0u, 0u};
@@ -2051,6 +2054,7 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
     };
     basis_of(hp[15], 128u);
     const uint4 h32 = mul_by_basis(hp[15]);
+    const uint4 h48 = mul_by_basis(h32);  // (the basis is still H^16's)
     basis_of(h32, 128u);
     const uint4 h64 = mul_by_basis(h32);
     basis_of(h64, 128u);
@@ -2067,11 +2071,11 @@ __global__ __launch_bounds__(256) void gcm_key_setup_kernel(const uint8_t* __res
     const uint4 h256 = mul_by_basis(h128);
     basis_of(h256, 128u);
     const uint4 h512 = mul_by_basis(h256);
-    if (t < 80u) {  // Shoup tables of H^32, H^64, H^128, H^256, H^512
+    if (t < 96u) {  // Shoup tables of H^32, H^64, H^128, H^256, H^512 and H^48
         const uint32_t k = t >> 4, v = t & 15u;
-        const uint4 P = k == 0u ? h32 : k == 1u ? h64 : k == 2u ? h128 : k == 3u ? h256 : h512;
+        const uint4 P = k == 0u ? h32 : k == 1u ? h64 : k == 2u ? h128 : k == 3u ? h256 : k == 4u ? h512 : h48;
         const uint4 e = gf_tab_entry(P, v);
-        uint32_t* o = rec + rec_shoup_pow2(5u + k) + 4u * v;
+        uint32_t* o = rec + (k < 5u ? rec_shoup_pow2(5u + k) : kRecShoup48) + 4u * v;
         o[0] = e.x; o[1] = e.y; o[2] = e.z; o[3] = e.w;
     }
 }

@@ -4,9 +4,9 @@
 
 namespace neb {
 
-// One key record per installed tunnel key (27.75 KiB): the first 512 B hold the key schedule and
+// One key record per installed tunnel key (28 KiB): the first 512 B hold the key schedule and
 // raw H powers; the rest holds GHASH lookup tables precomputed at install time (AES-GCM only).
-constexpr uint32_t kKeyRecDwords = 7104;
+constexpr uint32_t kKeyRecDwords = 7168;
 constexpr uint32_t kKeyRecBytes = kKeyRecDwords * 4;
 
 // AES-256-GCM record
@@ -42,7 +42,9 @@ constexpr uint32_t kRecPos3 = kRecPos2 + 8 * 16 * 4;
 // position tables of H^12: with those of H^4 (kRecFull) and H^8, the mixed-key GHASH pass's
 // aggregated rounds (gcm_ghash_kernel: A·H^12 ⊕ X_0·H^8 ⊕ X_1·H^4 ⊕ X_2, one reduction)
 constexpr uint32_t kRecPos12 = kRecPos3 + 8 * 16 * 4;
-static_assert(kRecPos12 + 8 * 16 * 4 == kKeyRecDwords, "record layout");
+// the Shoup table of H^48: with M_16 and M_32, the 64-lane final's quarter powers (GhShoup64)
+constexpr uint32_t kRecShoup48 = kRecPos12 + 8 * 16 * 4;
+static_assert(kRecShoup48 + 16 * 4 == kKeyRecDwords, "record layout");
 // record offset of the Shoup table of H^(2^j), j = 0..9
 __host__ __device__ constexpr uint32_t rec_shoup_pow2(uint32_t j) {
     return j < 5u ? kRecShoup + 64u * ((1u << j) - 1u) : (j == 5u ? kRecShoup32 : kRecShoupHi + 64u * (j - 6u));
