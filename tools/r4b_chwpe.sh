@@ -1,6 +1,8 @@
 #!/bin/bash
 # ChaCha kernel occupancy A/B on C4: the product (compiler's choice, 4 waves/SIMD) against
 # build_var/chwpe5 / chwpe6 (-DNEB_CH_WPE=5 / 6: 96 / 80 VGPRs, with spills), alternating.
+# (Historical: the NEB_CH_WPE knob was removed after this A/B; build_var/chwpe5, chwpe6 came from a
+# __launch_bounds__(kChThreads, NEB_CH_WPE) variant of chacha_batch_kernel.)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r4b_ch; mkdir -p $OUT
 cd $R
