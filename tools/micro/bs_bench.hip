@@ -1,4 +1,4 @@
-// bs_bench.hip — throughput of the bitsliced AES-256-CTR pass (nebula_amd/csrc/bs_aes.hpp) alone:
+// bs_bench.hip — throughput of the bitsliced AES-256-CTR pass (tools/experimental/bs_aes.hpp) alone:
 // 16 waves per CU, every wave running NPASS passes back to back. Reports ns per pass per wave and
 // VALU instructions per pass from the code object (counted separately). Not part of the engine.
 #include <hip/hip_runtime.h>
