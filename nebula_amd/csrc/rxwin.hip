@@ -214,11 +214,14 @@ __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p
     const uint32_t nb2 = next ? 1u << so.bits[p + 1] : 0u;
     // digit t: the count in earlier workgroups, and the total (exclusive scan over digits below)
     uint32_t pre = 0, tot = 0;
-#pragma unroll 8
-    for (uint32_t q = 0; q < so.nblk; q++) {
+    // every row loaded at once (rows from nblk on are allocated and masked): one memory latency
+    // instead of nblk / 8 of them one after another (C3: the two passes 19.1 -> 17.9 us)
+#pragma unroll
+    for (uint32_t q = 0; q < kRxSortBlocks; q++) {
         const uint32_t h = hist[(size_t)q * 256 + t];
-        tot += h;
-        pre += q < b ? h : 0u;
+        const uint32_t hv = q < so.nblk ? h : 0u;
+        tot += hv;
+        pre += q < b ? hv : 0u;
     }
     uint32_t x = tot;
 #pragma unroll
