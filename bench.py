@@ -5,9 +5,12 @@
 
 One step = seal every packet of the batch, then open every packet of it (in place, on device),
 i.e. one pass of the hot path (inside.go seal + outside.go open) over one 64 Ki x 1300 B batch.
-N > 1: one process per GPU (launched by torch.distributed.run), each rank owns its own batch of
-the same shape (packets are independent: no collective on the data path — SURVEY.md §8e);
-timing is bracketed by a barrier + device sync on both sides and the max over ranks is taken.
+N > 1: one process per GPU, each rank owns its own batch of the same shape (packets are
+independent: no collective on the data path — SURVEY.md §8e; C5 is one batch split over the ranks).
+Launched by torch.distributed.run, or, when no launcher set WORLD_SIZE, by this script itself: it
+starts the N rank processes with the same environment torchrun gives them and relays rank 0's line,
+so `python bench.py --gpus 8` and the torchrun form measure the same thing (spawn_ranks).
+Timing is bracketed by a barrier + device sync on both sides and the max over ranks is taken.
 
 Printed (rank 0, one JSON line): value = (payload sealed + payload opened, all ranks) / time.
 roofline: the seal kernel's algorithmic bytes (2p+32 per packet) / its mean launch time, from HIP
@@ -210,6 +213,68 @@ def pmc_config(cfg_name: str):
         return None
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(nranks: int, argv) -> int:
+    """`--gpus N` with no launcher around this process (WORLD_SIZE unset): start the N rank
+    processes here, each a fresh interpreter running this script with the torch.distributed.run
+    environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), so a bare
+    `python bench.py --gpus 8` measures 8 GPUs exactly as the torchrun form does. This process
+    touches no GPU (children are started, never exec'd into). The ranks run the barrier, the timing
+    and the max / sum over ranks themselves; rank 0's one JSON line is relayed with `launcher` added.
+    If any rank fails the others are stopped and the exit status is non-zero: never a one-GPU line
+    for an N-GPU request."""
+    import subprocess
+    import threading
+
+    port = _free_port()
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks), LOCAL_WORLD_SIZE=str(nranks),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out = []
+    reader = threading.Thread(target=lambda: out.extend(procs[0].stdout), daemon=True)
+    reader.start()
+    rc = 0
+    while None in [p.poll() for p in procs]:  # (a list: every process polled each time)
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.1)
+    for p in procs:
+        p.wait()
+    reader.join(timeout=10)
+    rc = rc or next((p.returncode for p in procs if p.returncode != 0), 0)
+    lines = [ln for ln in out if ln.lstrip().startswith("{")]
+    if rc != 0 or not lines:
+        log(f"bench: {nranks} rank processes, exit statuses {[p.returncode for p in procs]}; no result")
+        return rc or 1
+    for ln in out:
+        if not ln.lstrip().startswith("{"):
+            sys.stdout.write(ln)
+    res = json.loads(lines[-1])
+    if res.get("n_gpus") != nranks:
+        log(f"bench: rank 0 reported n_gpus {res.get('n_gpus')} for {nranks} ranks")
+        return 1
+    res["launcher"] = f"bench.py: {nranks} rank processes (RANK/WORLD_SIZE env, gloo control plane)"
+    print(json.dumps(res), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -231,13 +296,21 @@ def main():
     ap.add_argument("--tx-superpackets", type=int, default=1457,
                     help="tx mode: 64 KiB TSO superpackets per batch (45 segments each; 1457 -> 65 565 wires, "
                          "1456 -> 65 520: within one pass of the 4096 waves of 16 packets)")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # tests: launch + aggregation, no GPU
     args = ap.parse_args()
 
     from nebula_amd.shard import Control, dist_env
 
     if args.inproc:
         return bench_inproc(args)
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # no launcher: this process starts the ranks itself (before anything here touches the GPU)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     rank, world, local = dist_env()
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks; using WORLD_SIZE")
+    if args.stub:
+        return bench_stub(args, rank, world)
     import torch
 
     from nebula_amd import _lib as L
@@ -245,8 +318,6 @@ def main():
     from nebula_amd.batch import DeviceBatch, host_batch, install_keys, slot_desc
     from nebula_amd.noiseutil import Engine
 
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     # one process per GPU; more ranks than devices (a rehearsal on a smaller box) share them round-robin
     ndev = torch.cuda.device_count()
     device = local % ndev if ndev else local
@@ -280,7 +351,7 @@ def main():
     alg_bytes = float(b.algorithmic_bytes)
 
     if args.mode == "host-staged":
-        os.environ["NEB_HOST_MODE"] = "dma"  # read by the engine at its first host batch
+        L.check(L.lib().neb_set_knob(L.KNOB_HOST_MODE, 1), "neb_set_knob")  # DMA staging
     if args.mode in ("host", "host-staged"):
         from nebula_amd.batch import PinnedBuffer
 
@@ -366,26 +437,20 @@ def main():
     dt = te - ts
     seal_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev.values()]))
     open_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev.values()]))
+    call_ms = whole_seal_ms(db, stream)
     st = db.status_host()
     assert (st == 0).all(), "open failed inside the timed region"
     dt = ctrl.max(dt)
     total_payload = ctrl.sum(2 * payload * args.steps)
+    multi = hbm_over_ranks(ctrl, world, alg_bytes, seal_ms, ndev)
 
     if rank != 0:
         return
     value = total_payload / dt / GIB
-    achieved = alg_bytes / (seal_ms * 1e-3) / 1e9  # GB/s, seal kernel
+    achieved = multi["per_gpu"]["achieved_mean"]  # GB/s, seal kernel (rank 0's alone at N = 1)
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
-    fused = os.environ.get("NEB_MIXED_SPLIT") != "1"
-    if b.alg != L.ALG_AESGCM:
-        kern_tag = "chacha_batch_kernel<false>"
-    elif b.nkeys == 1:
-        kern_tag = "gcm_single_tail_kernel<false>" if b.n <= 6144 else "gcm_single_kernel<false, false>"
-    else:
-        kern_tag = "gcm_chunk_kernel<false> (the binning passes before it excluded)" if fused else \
-            "gcm_ctr_kernel<false, true> (the split passes' first)"
-    if not bound:
-        kern_tag += "; event brackets around the whole seal call (an upper bound)"
+    # the kernel the dispatch-bound events were bound to, as the library names it
+    kern_tag = L.lib().neb_time_last_kernel().decode() if bound else "event brackets around the whole seal call"
     pmc = pmc_config(f"C{cfg + 1}")
     lens = b.desc["len"].astype(np.int64)
     out = {
@@ -417,8 +482,15 @@ def main():
             "kernel": kern_tag,
             # the seal's dominant kernel between start / stop events bound to its dispatch
             "kernel_ms": round(seal_ms, 4), "open_kernel_ms": round(open_ms, 4),
+            # the whole seal call (mixed keys: with its binning passes) between marker events,
+            # after the timed loop: a bound on the call, comparable across kernels and rounds
+            "seal_call_ms": round(call_ms, 4),
+            "seal_call_achieved": round(alg_bytes / (call_ms * 1e-3) / 1e9, 2),
             "kernel_timing": "dispatch-bound events" if bound else "marker events around the call",
             "algorithmic_bytes_per_launch": int(alg_bytes),
+            # every rank's own seal kernel: per GPU (min / mean / max over ranks) and the whole job
+            # against N x the HBM peak; devices = distinct GPUs the ranks ran on
+            "per_gpu": multi["per_gpu"], "aggregate": multi["aggregate"],
         },
     }
     if world == 1 and not args.no_cpu_baseline:
@@ -428,6 +500,60 @@ def main():
             log(f"cpu_baseline failed: {e!r}")
             out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
+
+
+def whole_seal_ms(db, stream, reps: int = 4) -> float:
+    """Mean time of the whole seal call (every kernel it launches) between marker events, each
+    sealed batch opened back untimed so the arena stays valid; run after the timed loop."""
+    import torch
+
+    ts = []
+    for _ in range(reps):
+        a, z = TimingEvent(), TimingEvent()
+        a.record(stream)
+        db.seal()
+        z.record(stream)
+        db.open()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(z))
+    return float(np.mean(ts))
+
+
+def hbm_over_ranks(ctrl, world: int, alg_bytes: float, seal_ms: float, ndev: int) -> dict:
+    """Every rank's seal-kernel bandwidth (algorithmic bytes / its own kernel time) over the ranks:
+    per GPU min / mean / max and fraction of one GPU's HBM peak, and the whole job's sum against
+    N x the peak. devices: the distinct GPUs the ranks ran on (fewer than N only in a rehearsal
+    that shares a device)."""
+    ach = alg_bytes / (seal_ms * 1e-3) / 1e9
+    tot = ctrl.sum(ach)
+    lo, hi = -ctrl.max(-ach), ctrl.max(ach)
+    mean = tot / world
+    return {
+        "per_gpu": {"achieved_min": round(lo, 2), "achieved_mean": round(mean, 2), "achieved_max": round(hi, 2),
+                    "frac_mean": round(mean / HBM_PEAK_GBS, 4), "ranks": world},
+        "aggregate": {"achieved": round(tot, 2), "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                      "frac": round(tot / (HBM_PEAK_GBS * world), 4), "devices": min(world, max(ndev, 1))},
+    }
+
+
+def bench_stub(args, rank: int, world: int):
+    """--stub (tests only): the launch and aggregation path without a GPU. Every rank reports a
+    made-up kernel time of 0.1 x (rank + 1) ms over gloo, and rank 0 prints the JSON line."""
+    from nebula_amd.shard import Control
+
+    if os.environ.get("NEB_BENCH_STUB_FAIL") == str(rank):
+        sys.exit(3)  # a rank that dies before the control plane is up
+    ctrl = Control(world)
+    ctrl.barrier()
+    dt = ctrl.max(0.001 * (rank + 1))
+    total = ctrl.sum(1.0 * GIB)
+    multi = hbm_over_ranks(ctrl, world, 1e8, 0.1 * (rank + 1), 0)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": total / dt / GIB, "unit": "GiB/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3,
+                          "roofline": {"per_gpu": multi["per_gpu"], "aggregate": multi["aggregate"]}}), flush=True)
+    if ctrl.dist is not None:
+        ctrl.dist.destroy_process_group()
 
 
 def bench_inproc(args):

@@ -117,7 +117,9 @@ NEB_API int neb_engine_stats(const neb_engine* e, uint64_t stats[4]);
  * passed to the batch calls must stay alive until the work enqueued on them has completed. */
 /* Human-readable text of a return code. */
 NEB_API const char* neb_strerror(int rc);
-/* Detail of the last NEB_ERR_HIP / NEB_ERR_NO_DEVICE on the calling thread (HIP error string). */
+/* Detail of the last NEB_ERR_HIP / NEB_ERR_NO_DEVICE on the calling thread (HIP error string), or of
+ * the last multi-engine batch call that fenced key slots (it returns NEB_OK; the fenced packets get
+ * NEB_STATUS_BAD_KEY — see neb_cipher_create_multi). */
 NEB_API const char* neb_last_error(void);
 /* The first 16 hex digits of the SHA-256 of the library's sources (nebula_amd/Makefile SRC then
  * HDR, concatenated) it was built from: a test compares it with the sources beside it. */
@@ -127,6 +129,24 @@ NEB_API const char* neb_build_id(void);
  * around it — the single-key kernel, the mixed-key chunk kernel or the ChaCha kernel (a small batch:
  * its one kernel). NULL, NULL disarms. */
 NEB_API int neb_time_next_kernel(void* start, void* stop);
+/* Process-wide knobs for A/B measurements and tests. Each starts from the environment variable named
+ * beside it (read once, at the first use of any knob) and can be changed between batches; batches
+ * read them with one atomic load (no getenv on the batch path). */
+enum {
+    NEB_KNOB_HOST_MODE = 0,       /* NEB_HOST_MODE: 0 zero-copy for mapped arenas (default), 1 "dma" staging */
+    NEB_KNOB_SUB_BINS_FROM = 1,   /* NEB_SUB_BINS_FROM: mixed-key batches of at least this many packets
+                                   * count their bins in sub-bins (default 262144) */
+    NEB_KNOB_SINGLE_MAX_GRID = 2, /* NEB_SINGLE_MAX_GRID: cap on the single-key kernel's workgroups (0: none;
+                                   * tests use it to force a partial last pass) */
+    NEB_KNOB_RX_STRICT = 3,       /* NEB_RXDEV_STRICT: a device receive whose windows need the sequential host
+                                   * finish fails with NEB_ERR_INVALID instead (tests: the parallel form ran) */
+    NEB_KNOB_COUNT = 4
+};
+NEB_API int neb_set_knob(int knob, int64_t value);
+NEB_API int64_t neb_get_knob(int knob); /* -1 for an unknown knob */
+/* The (demangled) name of the kernel the last armed pair was bound to on this thread, or "" when
+ * none has been bound yet: what a benchmark's kernel time is the time of. */
+NEB_API const char* neb_time_last_kernel(void);
 
 /* ---- key install: noise.CipherFunc.Cipher(k) ----------------------------------------------- */
 
@@ -278,6 +298,10 @@ NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, 
 NEB_API int neb_dwindows_destroy(neb_dwindows* d);
 NEB_API int neb_dwindows_load(neb_dwindows* d, uint32_t idx, const neb_window* w);
 NEB_API int neb_dwindows_store(neb_dwindows* d, uint32_t idx, neb_window* w);
+/* Fault injection for tests: the polls a device receive's scan may spend waiting for an earlier
+ * workgroup before the batch fails with NEB_ERR_HIP (default 2^20, about 0.1 s; 0 fails every scan
+ * that has to wait). A failed batch moves no window. */
+NEB_API int neb_dwindows_set_spin_limit(neb_dwindows* d, uint32_t limit);
 /* neb_rx_open_batch_host over a device-resident batch (device descriptors, arena and statuses),
  * with the windows of `d` (slot desc.key_id; absent or out of range → NEB_STATUS_BAD_KEY): the
  * same statuses, arena bytes, window contents and counters as Decrypt packet by packet. Runs on

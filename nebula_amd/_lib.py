@@ -42,6 +42,8 @@ HEADER_LEN = 16
 REJECT_HEADROOM = 1 << 40
 REJECT_AFTER_MESSAGES = (1 << 64) - 1 - REJECT_HEADROOM
 KEYS_MIXED = 0xFFFFFFFF
+# neb_set_knob (include/nebula_aead.h)
+KNOB_HOST_MODE, KNOB_SUB_BINS_FROM, KNOB_SINGLE_MAX_GRID, KNOB_RX_STRICT = 0, 1, 2, 3
 RX_OWN_SOURCE = 0x80000000  # or-ed into neb_rx_packet.len: outside.go:66-74 refused the datagram
 
 # neb_desc (include/nebula_aead.h)
@@ -64,6 +66,9 @@ SIGNATURES = {
     "neb_last_error": (C.c_char_p, []),
     "neb_build_id": (C.c_char_p, []),
     "neb_time_next_kernel": (_i, [_vp, _vp]),
+    "neb_time_last_kernel": (C.c_char_p, []),
+    "neb_set_knob": (_i, [_i, C.c_int64]),
+    "neb_get_knob": (C.c_int64, [_i]),
     "neb_cipher_create": (_i, [_vp, _i, _u8p, C.POINTER(_vp)]),
     "neb_cipher_create_batch": (_i, [_vp, _i, _u8p, _u32, _vp]),
     "neb_cipher_create_multi": (_i, [_vp, _u32, _i, _u8p, _vp]),
@@ -96,6 +101,7 @@ SIGNATURES = {
     "neb_dwindows_destroy": (_i, [_vp]),
     "neb_dwindows_load": (_i, [_vp, _u32, _vp]),
     "neb_dwindows_store": (_i, [_vp, _u32, _vp]),
+    "neb_dwindows_set_spin_limit": (_i, [_vp, _u32]),
     "neb_rx_open_batch": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
     "neb_tx_seal_batch": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
     "neb_tx_seal_batch_host": (_i, [_vp, _i, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _vp, _u32, _vp, _vp,
@@ -184,3 +190,18 @@ def strerror(rc: int) -> str:
 def check(rc: int, what: str = "") -> None:
     if rc != OK:
         raise NebError(rc, what)
+
+
+class knob:
+    """`with knob(KNOB_X, v):` sets a process-wide knob (neb_set_knob) and restores it after."""
+
+    def __init__(self, k: int, value: int):
+        self.k, self.value = k, value
+
+    def __enter__(self):
+        self.old = lib().neb_get_knob(self.k)
+        check(lib().neb_set_knob(self.k, self.value), "neb_set_knob")
+        return self
+
+    def __exit__(self, *exc):
+        lib().neb_set_knob(self.k, self.old)

@@ -207,6 +207,10 @@ class DeviceWindows:
     def store(self, idx: int, w: Bits) -> None:
         L.check(self._lib.neb_dwindows_store(self._h, idx, w.handle), "neb_dwindows_store")
 
+    def set_spin_limit(self, limit: int) -> None:
+        """Fault injection (tests): neb_dwindows_set_spin_limit; 0 fails every scan that waits."""
+        L.check(self._lib.neb_dwindows_set_spin_limit(self._h, limit), "neb_dwindows_set_spin_limit")
+
     def destroy(self) -> None:
         if self._h:
             self._lib.neb_dwindows_destroy(self._h)

@@ -21,6 +21,8 @@
 //    position / Shoup tables of the other powers, staged in LDS per workgroup (one key) or per
 //    wave and chunk (mixed keys).
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <hip/hip_ext.h>
 
 #include <cstdlib>
@@ -31,6 +33,7 @@
 
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
+#include "knobs.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
 #include "timing.hpp"
@@ -2112,14 +2115,21 @@ static hipError_t launch_grid(K kern, int threads, uint32_t work_waves, int cu_c
 }
 // the same with `stop` (optional) bound to the dispatch (hipExtLaunchKernel): the event completes
 // with the kernel, and no marker packet follows it on the stream
+constexpr int kMaxDevices = 64;
 template <class K, class... Extra>
 static hipError_t launch_grid_stop(K kern, int threads, uint32_t work_waves, int cu_count, hipStream_t s,
                                    hipEvent_t stop, Extra... args) {
-    static const int per_cu = [&] {  // per instantiation: kernels of one signature share it (same bounds here)
-        int pc = 1;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, threads, 0) != hipSuccess || pc < 1) pc = 1;
-        return pc;
-    }();
+    // workgroups per CU, cached per instantiation and device (engines on GPUs of different
+    // architectures in one process each get their own)
+    static std::atomic<int> cache[kMaxDevices];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int per_cu = dev >= 0 && dev < kMaxDevices ? cache[dev].load(std::memory_order_relaxed) : 0;
+    if (per_cu < 1) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (dev >= 0 && dev < kMaxDevices) cache[dev].store(per_cu, std::memory_order_relaxed);
+    }
     const uint32_t waves = (uint32_t)threads / 64u;
     const uint32_t want = (work_waves + waves - 1) / waves;
     const uint32_t cap = (uint32_t)(per_cu * cu_count);
@@ -2141,7 +2151,7 @@ extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int
         per_cu = 1;
     uint32_t cap = (uint32_t)(per_cu * cu_count);
     // test hook: a smaller grid, so that small batches have a partial last pass (the tail kernel)
-    if (const char* g = std::getenv("NEB_SINGLE_MAX_GRID")) cap = std::max(1u, std::min(cap, (uint32_t)std::atoi(g)));
+    if (const int64_t g = neb::knob(NEB_KNOB_SINGLE_MAX_GRID); g > 0) cap = std::max(1u, std::min<uint32_t>(cap, (uint32_t)g));
     // one workgroup per group up to the cap: a small batch runs one or a few groups per CU
     const uint32_t grid = std::min(groups, cap);
     return grid * neb::kSingleWaves;

@@ -11,15 +11,18 @@
 #include <cstdio>
 #include <deque>
 #include <cstring>
+#include <cxxabi.h>
 #include <cstdlib>
 #include <dlfcn.h>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/nebula_aead.h"
 #include "hip_guard.hpp"
+#include "knobs.hpp"
 #include "host_common.hpp"
 #include "layout.hpp"
 #include "sched.hpp"
@@ -139,11 +142,8 @@ namespace {
 // (hipMemcpyAsync staging); NEB_HOST_STAGED=1 is the older name of "dma". Measured on one MI355X
 // (C2 seal+open, 64 Ki x 1300 B): zero-copy 28.4 GiB/s against 23.9 for DMA staging.
 enum HostMode { kHostZeroCopy, kHostDma };
-HostMode host_mode() {  // read per batch (a few hundred ns), so a process can switch between batches
-    if (std::getenv("NEB_HOST_STAGED")) return kHostDma;
-    const char* v = std::getenv("NEB_HOST_MODE");
-    if (v && !std::strcmp(v, "dma")) return kHostDma;
-    return kHostZeroCopy;
+HostMode host_mode() {  // NEB_KNOB_HOST_MODE, read per batch, so a process can switch between batches
+    return neb::knob(NEB_KNOB_HOST_MODE) == 1 ? kHostDma : kHostZeroCopy;
 }
 
 }  // namespace
@@ -256,7 +256,25 @@ struct neb_cipher {
 };
 
 static thread_local char g_last_error[256] = "";
+
+// neb_set_knob: the environment's values, read once on first use
+static std::atomic<int64_t> g_knobs[NEB_KNOB_COUNT];
+int64_t neb::knob(int k) {
+    static const bool init = [] {
+        const char* hm = std::getenv("NEB_HOST_MODE");
+        g_knobs[NEB_KNOB_HOST_MODE] = (std::getenv("NEB_HOST_STAGED") || (hm && !std::strcmp(hm, "dma"))) ? 1 : 0;
+        const char* sb = std::getenv("NEB_SUB_BINS_FROM");
+        g_knobs[NEB_KNOB_SUB_BINS_FROM] = sb ? (int64_t)std::strtoull(sb, nullptr, 10) : (int64_t)neb::kSubBinsFrom;
+        const char* mg = std::getenv("NEB_SINGLE_MAX_GRID");
+        g_knobs[NEB_KNOB_SINGLE_MAX_GRID] = mg ? std::atoll(mg) : 0;
+        g_knobs[NEB_KNOB_RX_STRICT] = std::getenv("NEB_RXDEV_STRICT") ? 1 : 0;
+        return true;
+    }();
+    (void)init;
+    return g_knobs[k].load(std::memory_order_relaxed);
+}
 thread_local neb::KernelTiming neb::g_kernel_timing;  // timing.hpp: armed by neb_time_next_kernel
+thread_local const void* neb::g_timed_kernel = nullptr;
 
 static void set_error(const char* where, hipError_t err) {
     std::snprintf(g_last_error, sizeof g_last_error, "%s: %s (%d)", where, hipGetErrorString(err), (int)err);
@@ -361,6 +379,27 @@ NEB_API int neb_time_next_kernel(void* start, void* stop) {
     if ((start == nullptr) != (stop == nullptr)) return NEB_ERR_INVALID;
     neb::g_kernel_timing = {(hipEvent_t)start, (hipEvent_t)stop};
     return NEB_OK;
+}
+
+NEB_API int neb_set_knob(int knob, int64_t value) {
+    if (knob < 0 || knob >= NEB_KNOB_COUNT) return NEB_ERR_INVALID;
+    neb::knob(knob);  // (the environment's values first, so a later first use does not overwrite this)
+    g_knobs[knob].store(value, std::memory_order_relaxed);
+    return NEB_OK;
+}
+
+NEB_API int64_t neb_get_knob(int knob) { return knob < 0 || knob >= NEB_KNOB_COUNT ? -1 : neb::knob(knob); }
+
+NEB_API const char* neb_time_last_kernel(void) {
+    static thread_local std::string name;
+    if (!neb::g_timed_kernel) return "";
+    const char* m = hipKernelNameRefByPtr(neb::g_timed_kernel, nullptr);
+    if (!m) return "";
+    int st = 0;
+    char* d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+    name = st == 0 && d ? d : m;
+    std::free(d);
+    return name.c_str();
 }
 
 #ifndef NEB_BUILD_ID
@@ -796,9 +835,12 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
 // per batch) runs the two-pass form instead (gcm_ctr_kernel + gcm_ghash_kernel, DESIGN.md §3.2: measured
 // slower on C3 and C5). NEB_SCHED_SDESC=1: the fused kernel reads the scheduler's sorted descriptor
 // copy (the split passes always do).
-static bool mixed_split() {
-    const char* v = std::getenv("NEB_MIXED_SPLIT");
-    return v && v[0] == '1';
+static bool mixed_split() {  // (A/B knobs are read once: getenv is not safe beside setenv)
+    static const bool on = [] {
+        const char* v = std::getenv("NEB_MIXED_SPLIT");
+        return v && v[0] == '1';
+    }();
+    return on;
 }
 // NEB_BIND_EVENTS=0 (read once): markers after each batch instead of events bound to its last
 // kernel's dispatch (the A/B of round 4's binding for mixed-key AES-GCM and ChaCha batches)
@@ -810,8 +852,11 @@ static bool bind_events() {
     return on;
 }
 static bool sched_sdesc() {
-    const char* v = std::getenv("NEB_SCHED_SDESC");
-    return v && v[0] == '1';
+    static const bool on = [] {
+        const char* v = std::getenv("NEB_SCHED_SDESC");
+        return v && v[0] == '1';
+    }();
+    return on;
 }
 
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
@@ -862,6 +907,21 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
                             s, hdr_from_dst, stop);
 }
 
+// A per-packet call's result from its pool slot into the caller's buffer, by status: a sealed or
+// opened packet is copied; a failed open leaves zeros (the kernel's in-place zeroing, written here
+// so the slot is never read); any other status (no key, exhausted counter) writes nothing, as the
+// reference returns before touching out (aesgcm.go:28-30). The slot's bytes are read only when the
+// kernel wrote them: slots are shared by every thread and cipher of the engine, so anything else
+// there is another call's packet.
+static void copy_result(int open, int32_t st, uint8_t* dst, const uint8_t* slot, size_t pay_len) {
+    const size_t out_len = open ? pay_len : pay_len + 16;
+    if (!out_len) return;
+    if (st == NEB_STATUS_OK)
+        std::memcpy(dst, slot, out_len);
+    else if (open && st == NEB_STATUS_AUTH_FAILED)
+        std::memset(dst, 0, out_len);
+}
+
 // One packet through the device, on a slot of the engine's per-packet pool (PktPool): the packet is
 // copied into the slot's pinned, mapped buffer ([desc | status | aad | payload (+tag)]), the batch
 // kernel seals or opens it there in place (zero-copy: no DMA either way) and the result is copied
@@ -895,8 +955,7 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
                 return NEB_ERR_HIP;
             }
             std::memcpy(st_out, h + o_status, 4);
-            const size_t out_len = open ? pay_len : pay_len + 16;
-            if (out_len) std::memcpy(dst, h + o_pay, out_len);
+            copy_result(open, *st_out, dst, h + o_pay, pay_len);
             return NEB_OK;
         }
         if (err != hipErrorInvalidValue) {  // (too large for the arguments: the batch path below)
@@ -925,8 +984,7 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
         return NEB_ERR_HIP;
     }
     std::memcpy(st_out, h + o_status, 4);
-    const size_t out_len = open ? pay_len : pay_len + 16;
-    if (out_len) std::memcpy(dst, h + o_pay, out_len);
+    copy_result(open, *st_out, dst, h + o_pay, pay_len);
     return NEB_OK;
 }
 
@@ -1464,6 +1522,16 @@ static KeyFence key_fence(neb_engine* const* es, uint32_t m) {
         }
     }
     for (neb_engine* e : order) e->key_mu.unlock();
+    if (f.any) {  // the call still returns NEB_OK (the packets carry NEB_STATUS_BAD_KEY): say why
+        uint32_t first = 0, slots = 0;
+        for (uint32_t k = m; k-- > 1;)
+            if (!f.bad[k].empty()) first = k;
+        for (uint8_t x : f.bad[first]) slots += x;
+        std::snprintf(g_last_error, sizeof g_last_error,
+                      "key fence: engine %u holds other installs than engine 0 in %u key slot(s); their packets get "
+                      "NEB_STATUS_BAD_KEY (install a tunnel key on every engine with neb_cipher_create_multi)",
+                      first, slots);
+    }
     return f;
 }
 

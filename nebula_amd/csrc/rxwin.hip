@@ -305,7 +305,7 @@ __device__ __forceinline__ void rx_pub(uint64_t* g, uint32_t gen, uint32_t v) {
 __device__ __forceinline__ uint64_t rx_peek(const uint64_t* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr uint32_t kRxSpinLimit = 1u << 20;  // ≈ 0.1 s of polling: then the batch fails (need_host bit 1)
+// kRxSpinLimit (rxwin.hpp) polls, ≈ 0.1 s: then the batch fails (need_host bit 1)
 
 // Scan and admission in one launch, kRxBlock run positions per workgroup, in the order the
 // workgroups start (a ticket), so every block a workgroup waits for has started and waits only
@@ -416,6 +416,10 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
                 uint64_t g_max = 0;
                 bool got = !valid;
                 uint32_t spins = 0;
+                if (ws.spin_limit == 0u) {  // test hook: a lookback that has to wait fails at once
+                    timed_out = true;
+                    break;
+                }
                 for (;;) {
                     if (!got) {
                         const uint64_t* g = ws.blk_pub + 3u * (uint64_t)bb;
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
                     const uint64_t in = __ballot(got), heads = __ballot(got && g_fh < kRxBlock);
                     const uint64_t need = heads ? ((heads & (~heads + 1u)) << 1) - 1u : ~0ull;  // lanes <= first head
                     if ((in & need) == need) break;
-                    if (++spins > kRxSpinLimit) {
+                    if (++spins > ws.spin_limit) {
                         timed_out = true;
                         break;
                     }
@@ -662,10 +666,13 @@ __global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
     const uint32_t sub = (uint32_t)t & (L - 1u);
     const uint32_t w = wl < win.count ? (uint32_t)wl : 0u;
     const uint32_t fl = wl < win.count ? ws.wflag[w] : 0u;
-    const bool fast = rx_fast(fl);
     // plain stores into the pinned host word: bit 0 a window for the host, bit 1 a lookback timeout
-    // (every writer reads the same err, so racing writers agree on bit 1)
+    // (every writer reads the same err, so racing writers agree on bit 1). After a timeout the batch
+    // fails and no window moves: the blocks that did finish computed their windows' finals from a
+    // partial prefix, and the failed block's packets were never opened, so their counters are
+    // unauthenticated (a forged high counter must not advance a window).
     const uint32_t errb = *ws.err ? 2u : 0u;
+    const bool fast = rx_fast(fl) && !errb;
     if ((fl & kRxTouched) && (fl & (kRxRisky | kRxSlow)) && sub == 0) *ws.need_host = 1u | errb;
     if (errb && t == 0) *ws.need_host = errb | 1u;
     uint64_t r = 0;

@@ -21,6 +21,8 @@ constexpr uint32_t kRxThreads = 256, kRxItems = 1, kRxBlock = kRxThreads * kRxIt
 // the stable sort by window (rxwin.hip): at most kRxSortBlocks workgroups of 256 x items packets,
 // digits of at most 8 bits for one pass, else passes of at most kRxSortDigit bits
 constexpr uint32_t kRxSortBlocks = 64, kRxSortDigit = 7, kRxSortMaxPasses = 5, kRxSortLoad = 4;
+// polls of a scan-admit lookback before the batch fails (≈ 0.1 s)
+constexpr uint32_t kRxSpinLimit = 1u << 20;
 
 struct RxDevWin {  // a set of windows of one length in device memory (neb_dwindows)
     uint32_t count;
@@ -55,6 +57,7 @@ struct RxDevWs {
     uint64_t* blk_pub;
     uint32_t* ticket;  // the scan-admit blocks' order of start (zeroed by the keys kernel)
     uint32_t* err;     // nonzero: a scan-admit lookback timed out (zeroed by the keys kernel)
+    uint32_t spin_limit;  // kRxSpinLimit; 0 (a test, neb_dwindows_debug) fails every lookback that waits
     // first occurrences: an open-addressing table keyed by (window, counter), 2^tab_lg >= 4n slots,
     // tagged with the batch generation (an entry of an older batch is empty, so the table is
     // never cleared between batches); a slot's owner (gen:32 | arrival index + 1) names its key
@@ -109,6 +112,7 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
     w.blk_pub = (uint64_t*)take(nblk * 3 * 8);
     w.ticket = (uint32_t*)take(4);
     w.err = (uint32_t*)take(4);
+    w.spin_limit = kRxSpinLimit;
     w.tab_lg = 1;
     while ((1ull << w.tab_lg) < 4ull * n) w.tab_lg++;  // at most a quarter full
     w.tab_owner = (uint64_t*)take((size_t)8 << w.tab_lg);

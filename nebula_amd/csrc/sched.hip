@@ -6,6 +6,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include "knobs.hpp"
 #include "sched.hpp"
 
 namespace neb {
@@ -171,11 +172,10 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
     const dim3 ga((nb + neb::kAllocThreads - 1) / neb::kAllocThreads), ta(neb::kAllocThreads);
-    // NEB_SUB_BINS_FROM=<packets> (read per batch): the A/B of the threshold, and the tests' coverage
-    // of both counting layouts
-    const char* bv = std::getenv("NEB_SUB_BINS_FROM");
-    const uint32_t from = bv ? (uint32_t)std::strtoul(bv, nullptr, 10) : neb::kSubBinsFrom;
-    if (n >= from) {
+    // NEB_KNOB_SUB_BINS_FROM (per batch): the A/B of the threshold, and the tests' coverage of both
+    // counting layouts
+    const int64_t from = neb::knob(NEB_KNOB_SUB_BINS_FROM);
+    if ((int64_t)n >= from) {
         hipLaunchKernelGGL(neb::sched_hist_kernel<neb::kSubBins>, dim3(gp), dim3(tpb), 0, s, d_desc, n, d_n, max_keys, lpp,
                            *ws);
         hipLaunchKernelGGL(neb::sched_alloc_kernel<neb::kSubBins>, ga, ta, 0, s, max_keys, *ws);

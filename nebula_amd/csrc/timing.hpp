@@ -16,6 +16,7 @@ struct KernelTiming {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 extern thread_local KernelTiming g_kernel_timing;  // engine.cpp
+extern thread_local const void* g_timed_kernel;    // engine.cpp: the kernel the last armed pair went to
 
 // launch `kern` on s with the armed timing pair (consumed) or `stop` bound to it; with a timing pair
 // armed, `stop` is recorded after the kernel
@@ -24,6 +25,7 @@ inline hipError_t launch_bound(K kern, dim3 grid, dim3 block, hipStream_t s, hip
     const KernelTiming t = g_kernel_timing;
     if (t.start && t.stop) {
         g_kernel_timing = {};
+        g_timed_kernel = reinterpret_cast<const void*>(kern);
         hipExtLaunchKernelGGL(kern, grid, block, 0, s, t.start, t.stop, 0, args...);
         hipError_t err = hipGetLastError();
         if (err == hipSuccess && stop) err = hipEventRecord(stop, s);

@@ -35,6 +35,7 @@
 
 #include "../../include/nebula_aead.h"
 #include "host_common.hpp"
+#include "knobs.hpp"
 #include "rxwin.hpp"
 #include "hip_guard.hpp"
 #include "window_core.hpp"
@@ -371,6 +372,7 @@ struct neb_dwindows {
     uint32_t* h_host = nullptr;  // pinned, mapped: the finish sets it when a window needs the host
     uint8_t* wire_mem = nullptr;  // neb_rx_open_wire_batch: descriptors + gate statuses
     uint32_t wire_n = 0;
+    uint32_t spin_limit = neb::kRxSpinLimit;  // neb_dwindows_set_spin_limit
 };
 
 namespace {
@@ -497,6 +499,13 @@ NEB_API int neb_dwindows_load(neb_dwindows* d, uint32_t idx, const neb_window* w
     return dw_write(d, idx, c);
 }
 
+NEB_API int neb_dwindows_set_spin_limit(neb_dwindows* d, uint32_t limit) {
+    if (!d) return NEB_ERR_INVALID;
+    std::lock_guard<std::mutex> g(d->mu);
+    d->spin_limit = limit;
+    return NEB_OK;
+}
+
 NEB_API int neb_dwindows_store(neb_dwindows* d, uint32_t idx, neb_window* w) {
     if (!d || !w || idx >= d->win.count) return NEB_ERR_INVALID;
     std::lock_guard<std::mutex> g(d->mu);
@@ -548,6 +557,7 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
     }
     *d->h_host = 0;
     d->ws.need_host = d->h_host;
+    d->ws.spin_limit = d->spin_limit;
     const neb::RxDevWs& ws = d->ws;
 
     static const bool prof = std::getenv("NEB_RX_PROF") != nullptr;
@@ -598,7 +608,7 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
         if ((flag[w] & neb::kRxTouched) && (flag[w] & (neb::kRxRisky | neb::kRxSlow))) slow.push_back(w);
     if (slow.empty()) return NEB_OK;
     // test hook: NEB_RXDEV_STRICT=1 refuses the host finish, to prove a batch ran the parallel form
-    if (std::getenv("NEB_RXDEV_STRICT")) return NEB_ERR_INVALID;
+    if (neb::knob(NEB_KNOB_RX_STRICT)) return NEB_ERR_INVALID;
     std::vector<int32_t> verdict, status;
     if (d2h(run_w, ws.run_w, n, s) || d2h(run_i, ws.run_i, n, s) || d2h(run_c, ws.run_c, n, s) ||
         d2h(adm, ws.adm, n, s) || d2h(verdict, ws.verdict, n, s) || d2h(status, d_status, n, s))

@@ -46,3 +46,21 @@ def _no_leaked_keys(request):
         import warnings
 
         warnings.warn(f"{request.node.nodeid} left {len(left)} keys installed (destroyed)")
+
+
+@pytest.fixture
+def knobs():
+    """knobs(name, value): set a process-wide engine knob (neb_set_knob) for this test; every knob
+    it set is restored afterwards."""
+    from nebula_amd import _lib as L
+
+    saved = {}
+
+    def set_(k, v):
+        if k not in saved:
+            saved[k] = L.lib().neb_get_knob(k)
+        L.check(L.lib().neb_set_knob(k, int(v)), "neb_set_knob")
+
+    yield set_
+    for k, v in saved.items():
+        L.lib().neb_set_knob(k, v)

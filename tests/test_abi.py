@@ -122,3 +122,22 @@ def test_batch_rejects_bad_args_without_gpu():
     lib = L.lib()
     assert lib.neb_seal_batch(None, 1, None, 0, None, None, L.KEYS_MIXED, None) == L.ERR_INVALID
     assert lib.neb_strerror(L.ERR_AUTH) == b"cipher: message authentication failed"
+
+
+def test_knobs_set_get_and_defaults():
+    """neb_set_knob / neb_get_knob: process-wide A/B and test knobs (no GPU involved). Defaults come
+    from the environment once; an unknown knob is refused; a set value is read back and restored."""
+    lib = L.lib()
+    assert lib.neb_get_knob(-1) == -1 and lib.neb_get_knob(99) == -1
+    assert lib.neb_set_knob(99, 1) == L.ERR_INVALID
+    if "NEB_SUB_BINS_FROM" not in os.environ:
+        assert lib.neb_get_knob(L.KNOB_SUB_BINS_FROM) == 1 << 18
+    for k in (L.KNOB_HOST_MODE, L.KNOB_SUB_BINS_FROM, L.KNOB_SINGLE_MAX_GRID, L.KNOB_RX_STRICT):
+        old = lib.neb_get_knob(k)
+        with L.knob(k, 12345):
+            assert lib.neb_get_knob(k) == 12345
+        assert lib.neb_get_knob(k) == old
+
+
+def test_time_last_kernel_empty_before_any_batch():
+    assert L.lib().neb_time_last_kernel() == b""

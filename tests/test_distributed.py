@@ -74,3 +74,46 @@ def test_shard_ranges_tile(n, world):
         assert lo == prev and hi >= lo
         prev = hi
     assert prev == n
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_bare_gpus2_starts_two_ranks():
+    """`python bench.py --gpus 2` with no launcher starts two rank processes itself (gloo control
+    plane), and the one JSON line aggregates both ranks: n_gpus 2, the max of the ranks' times, the
+    sum of their bytes, and per-GPU / aggregate bandwidth over both ranks' kernel times."""
+    rc, res, err = _run_bench(["--gpus", "2", "--stub", "--steps", "3", "--warmup", "1"])
+    assert rc == 0, err
+    assert res["n_gpus"] == 2 and "rank processes" in res["launcher"]
+    assert res["ms_per_step"] == pytest.approx(2.0)             # max over ranks: rank 1's 2 ms
+    assert res["value"] == pytest.approx(2.0 / 0.002)           # 2 x 1 GiB over 2 ms
+    pg, ag = res["roofline"]["per_gpu"], res["roofline"]["aggregate"]
+    assert pg["ranks"] == 2 and pg["achieved_max"] == pytest.approx(1000.0) and pg["achieved_min"] == pytest.approx(500.0)
+    assert ag["achieved"] == pytest.approx(1500.0) and ag["frac"] == pytest.approx(1500.0 / 16000.0, abs=1e-4)
+
+
+def test_bench_under_launcher_env_runs_one_rank_per_process():
+    """Under a launcher (WORLD_SIZE already set) bench.py is one rank and does not spawn; a lone
+    rank with WORLD_SIZE=1 and --gpus 1 prints its own line."""
+    rc, res, err = _run_bench(["--gpus", "1", "--stub"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 0, err
+    assert res["n_gpus"] == 1 and "launcher" not in res
+
+
+def test_bench_failed_rank_fails_the_run():
+    """A rank that dies makes the whole run exit non-zero with no JSON line (never a one-GPU line
+    for an N-GPU request)."""
+    rc, res, err = _run_bench(["--gpus", "2", "--stub"], {"NEB_BENCH_STUB_FAIL": "1"})
+    assert rc != 0 and res is None

@@ -193,16 +193,30 @@ def test_concurrent_encrypt_decrypt_danger(engine, oracle_mod):
 
 
 def test_destroy_does_not_wait_for_another_tunnels_batch(engine, oracle_mod):
-    """neb_cipher_destroy waits only for batches that may read the destroyed key: with another
-    tunnel's long single-key batch still running on another stream, destroying a key whose batches
-    are done returns before that batch finishes (the old device-wide drain waited for it)."""
-    import time
+    """neb_cipher_destroy waits only for batches that may read the destroyed key. Another tunnel's
+    single-key batches are queued on a stream behind a host gate (hipLaunchHostFunc blocking on a
+    threading.Event), so they cannot run until the test opens it: the destroy of an unrelated key
+    must return while they are still queued (the old device-wide drain would block until the gate
+    opened). Ordering only, no wall-clock bound: the batch's end event is still pending when the
+    destroy returns, and the batches then complete correctly."""
+    import ctypes as C
+    import threading
 
     import torch
 
     from nebula_amd import workload as W
     from nebula_amd.batch import DeviceBatch, install_keys
     from nebula_amd.noiseutil import CipherAESGCM
+
+    hip = None
+    for line in open("/proc/self/maps"):
+        if "libamdhip64" in line:
+            hip = C.CDLL(line.split()[-1])
+            break
+    assert hip is not None
+    gate = threading.Event()
+    HOSTFN = C.CFUNCTYPE(None, C.c_void_p)
+    hostfn = HOSTFN(lambda _: gate.wait(60))  # (a bound: a broken destroy cannot hang the suite)
 
     b = W.make_batch(1, 65536, 1, name="long")
     ciphers = install_keys(engine, b)
@@ -213,22 +227,25 @@ def test_destroy_does_not_wait_for_another_tunnels_batch(engine, oracle_mod):
         db.seal(stream=s.cuda_stream)  # warm
         s.synchronize()
         ev_end = torch.cuda.Event()
-        with torch.cuda.stream(s):
-            x = torch.randn(4096, 4096, device="cuda")
-            for _ in range(8):  # a few ms ahead of the batch on its stream
-                x = x @ x
-            for _ in range(20):
+        try:
+            assert hip.hipLaunchHostFunc(C.c_void_p(s.cuda_stream), hostfn, None) == 0
+            for _ in range(4):
                 db.seal(stream=s.cuda_stream)
             ev_end.record(s)
-        t0 = time.perf_counter()
-        other.destroy()
-        dt = time.perf_counter() - t0
-        still_running = not ev_end.query()
+            done = threading.Event()
+            th = threading.Thread(target=lambda: (other.destroy(), done.set()))
+            th.start()
+            returned = done.wait(20)
+            pending = not ev_end.query()
+        finally:
+            gate.set()
+        th.join(60)
         s.synchronize()
-        assert still_running, "the other tunnel's batch finished before the destroy returned"
+        assert returned, "the destroy waited for another tunnel's queued batch"
+        assert pending, "the gated batch ran before the gate opened"
         assert (db.status_host() == 0).all()
-        assert dt < 0.05, dt
     finally:
+        gate.set()
         for c in ciphers:
             c.destroy()
 

@@ -178,6 +178,8 @@ def test_host_multi_diverged_key_is_bad_key(oracle_mod, alg, nkeys):
             arena[:] = b.arena
             st = host_batch_multi(engines, alg, False, d, arena, hint)
             assert (st[bad] == L.STATUS_BAD_KEY).all() and (st[~bad] == 0).all()
+            # the call returned NEB_OK; the calling thread's last error says which engine was fenced
+            assert L.lib().neb_last_error().decode().startswith("key fence: engine 1 ")
             got = arena.reshape(n, b.stride)
             assert np.array_equal(got[bad], rows[bad]), "a refused packet was touched"
             assert np.array_equal(got[~bad], ref.reshape(n, b.stride)[~bad])

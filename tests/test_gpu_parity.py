@@ -120,7 +120,7 @@ def test_mixed_key_density_vs_oracle(engine, oracle_mod, alg, n, nkeys, sizes, r
 
 # both counting layouts of the mixed-key scheduler (sched.hip), forced by its per-batch knob: one
 # count word per bin, or kSubBins
-BINNING = {"one_word": {"NEB_SUB_BINS_FROM": "4000000000"}, "subbins": {"NEB_SUB_BINS_FROM": "0"}}
+BINNING = {"one_word": 4000000000, "subbins": 0}
 
 
 @pytest.mark.parametrize("path", sorted(BINNING))
@@ -130,9 +130,8 @@ BINNING = {"one_word": {"NEB_SUB_BINS_FROM": "4000000000"}, "subbins": {"NEB_SUB
     # IMIX over 1000 keys, 21 sub-bin workgroups' worth
     (21000, 1000, (90, 576, 1300), (7, 4, 1)),
 ])
-def test_binning_paths_vs_oracle(engine, oracle_mod, monkeypatch, path, n, nkeys, sizes, ratio):
-    for k, v in BINNING[path].items():
-        monkeypatch.setenv(k, v)
+def test_binning_paths_vs_oracle(engine, oracle_mod, knobs, path, n, nkeys, sizes, ratio):
+    knobs(L.KNOB_SUB_BINS_FROM, BINNING[path])
     b = W.make_batch(L.ALG_AESGCM, n, nkeys, sizes=sizes, ratio=ratio, seed=n ^ nkeys ^ 0x5EED, name="binning")
     ref, st_ref = oracle_seal(oracle_mod, b)
     for rep in range(2):  # twice: each path leaves its counters and bins clear for the next batch
@@ -451,14 +450,14 @@ def test_host_pipeline_matches_device(engine, oracle_mod, alg, arena_kind):
 
 
 @pytest.mark.parametrize("mode", ["zc", "dma"])
-def test_host_modes_shuffled_descriptors(engine, oracle_mod, mode, monkeypatch):
+def test_host_modes_shuffled_descriptors(engine, oracle_mod, mode, knobs):
     """Both host paths (zero-copy, hipMemcpyAsync staging) on a pinned arena with
     the descriptors in random order: pipeline chunks then cover overlapping arena spans, which the
     engine must retire in order (each chunk copies its whole span back). Also an arena that starts
     one byte past a 16-byte boundary (the kernels touch only aligned host arenas: DMA staging)."""
     from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
 
-    monkeypatch.setenv("NEB_HOST_MODE", mode)
+    knobs(L.KNOB_HOST_MODE, 1 if mode == "dma" else 0)
     b = W.make_batch(L.ALG_AESGCM, 20000, 64, sizes=(90, 576, 1300), ratio=(7, 4, 1), name="shuffled")
     ciphers = install_keys(engine, b)
     buf = PinnedBuffer(b.arena.nbytes + 16)
@@ -508,14 +507,14 @@ WRAP = 2**64 - 16  # an offset whose sum with any length wraps around 2^64
 
 @pytest.mark.parametrize("mode", ["zc", "dma"])
 @pytest.mark.parametrize("case", ["src_wrap", "dst_wrap", "aad_wrap", "past_end"])
-def test_host_rejects_invalid_descriptor_untouched(engine, mode, case, monkeypatch):
+def test_host_rejects_invalid_descriptor_untouched(engine, mode, case, knobs):
     """A host batch with one bad descriptor — an offset near 2^64 whose end wraps around, or a
     length past the arena — is refused before anything is copied or launched, in every host mode.
     The bad descriptor is the last of a 20000-packet batch, so the staged modes would otherwise
     have sealed their first chunks in place already."""
     from nebula_amd.batch import PinnedBuffer, host_batch, install_keys, slot_desc
 
-    monkeypatch.setenv("NEB_HOST_MODE", mode)
+    knobs(L.KNOB_HOST_MODE, 1 if mode == "dma" else 0)
     b = W.make_batch(L.ALG_AESGCM, 20000, 4, sizes=(90, 576, 1300), ratio=(7, 4, 1), name="wrap")
     ciphers = install_keys(engine, b)
     buf = PinnedBuffer(b.arena.nbytes)

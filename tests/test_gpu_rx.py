@@ -98,12 +98,9 @@ def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=N
                 d_desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
                 d_arena = torch.from_numpy(arena).to(dev)
                 d_status = torch.full((len(d),), -1, dtype=torch.int32, device=dev)
-                if strict:  # the parallel form only: the call fails if any window needs the host
-                    os.environ["NEB_RXDEV_STRICT"] = "1"
-                try:
+                # strict: the parallel form only: the call fails if any window needs the host
+                with L.knob(L.KNOB_RX_STRICT, 1 if strict else 0):
                     rx_open_batch_device(engine, alg, dw, d_desc, d_arena, d_status)
-                finally:
-                    os.environ.pop("NEB_RXDEV_STRICT", None)
                 torch.cuda.synchronize()
                 got = d_status.cpu().numpy()
                 arena[:] = d_arena.cpu().numpy()
@@ -251,6 +248,62 @@ def test_rx_device_one_big_window(engine, oracle_mod):
     arr = _random_arrivals(rng, 20000, 1, 0.0)
     _run(engine, oracle_mod, L.ALG_CHACHAPOLY, arr, ntunnels=1, window_len=8192, seed=4, lens=[0, 16, 90],
          device=True, strict=True)
+
+
+def test_rx_device_lookback_timeout_moves_no_window(engine, oracle_mod):
+    """A device receive whose scan lookback times out fails the batch (NEB_ERR_HIP) and moves no
+    window: neither the scan blocks that finished (their finals came from a partial prefix) nor the
+    failed one (its packets were never opened, so their counters are unauthenticated) commit
+    anything. Forced with the fault-injection spin limit 0 (every scan block that starts inside a
+    run and has to wait fails); the same batch then passes with the default limit, against the
+    oracle."""
+    import torch
+
+    from nebula_amd.connection_state import Bits, DeviceWindows, rx_open_batch_device
+    from nebula_amd.noiseutil import CipherAESGCM
+
+    rng = random.Random(21)
+    arr = _random_arrivals(rng, 3000, 4, 0.0)  # runs of ~750 packets: most scan blocks start mid-run
+    keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(4)]
+    ciphers = [CipherAESGCM.Cipher(engine, k) for k in keys]
+    dev = torch.device("cuda", engine.device)
+    try:
+        arena, desc, _ = _build(oracle_mod, L.ALG_AESGCM, keys, arr, 3, lens=[0, 16, 60])
+        desc["key_id"] = [ciphers[int(t)].key_id for t in desc["key_id"]]
+        dw = DeviceWindows(engine, engine.max_keys, 1024)
+        try:
+            before = {}
+            for c in ciphers:
+                w = Bits(1024)
+                w.Update(1)
+                w.Update(2)
+                dw.load(c.key_id, w)
+                before[c.key_id] = (w.current, w.lost, w.dupe, w.out_of_window, list(w.snapshot()))
+            d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+            d_arena = torch.from_numpy(arena).to(dev)
+            d_status = torch.full((len(desc),), -1, dtype=torch.int32, device=dev)
+            dw.set_spin_limit(0)
+            with pytest.raises(L.NebError) as ei:
+                rx_open_batch_device(engine, L.ALG_AESGCM, dw, d_desc, d_arena, d_status)
+            assert ei.value.rc == L.ERR_HIP
+            torch.cuda.synchronize()
+            for c in ciphers:
+                w = Bits(1024)
+                dw.store(c.key_id, w)
+                assert (w.current, w.lost, w.dupe, w.out_of_window, list(w.snapshot())) == before[c.key_id]
+            # the windows are intact: the same batch (fresh arena) goes through with the default limit
+            dw.set_spin_limit(1 << 20)
+            d_arena.copy_(torch.from_numpy(arena).to(dev))
+            rx_open_batch_device(engine, L.ALG_AESGCM, dw, d_desc, d_arena, d_status)
+            torch.cuda.synchronize()
+            assert (d_status.cpu().numpy() != -1).all()
+        finally:
+            dw.destroy()
+    finally:
+        for c in ciphers:
+            c.destroy()
+    # and the full check of that batch against the oracle, on fresh windows
+    _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=4, window_len=1024, seed=3, lens=[0, 16, 60], device=True)
 
 
 def test_rx_device_counters_near_wrap(engine, oracle_mod):
@@ -442,12 +495,8 @@ def test_rx_device_batches_one_and_many_windows(engine, oracle_mod, strict):
         for b in batches:
             dd = torch.from_numpy(d[a:a + len(b)].view(np.uint8).copy()).to(dev)
             st = torch.full((len(b),), -1, dtype=torch.int32, device=dev)
-            if strict:
-                os.environ["NEB_RXDEV_STRICT"] = "1"
-            try:
+            with L.knob(L.KNOB_RX_STRICT, 1 if strict else 0):
                 rx_open_batch_device(engine, L.ALG_AESGCM, dw, dd, d_arena, st)
-            finally:
-                os.environ.pop("NEB_RXDEV_STRICT", None)
             got += st.cpu().tolist()
             a += len(b)
         assert got == exp_status

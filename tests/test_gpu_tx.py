@@ -247,17 +247,17 @@ def test_tx_batch_byte_skewed_reads(engine, oracle_mod, alg, single):
 
 
 @pytest.mark.parametrize("grid", [None, 1])
-def test_tx_single_key_checksums_in_seal(engine, oracle_mod, grid, monkeypatch):
+def test_tx_single_key_checksums_in_seal(engine, oracle_mod, grid, knobs):
     """One AES-GCM tunnel key: the seal sums the payloads into the L4 checksums itself (aes_gcm.hip
     gcm_csum_fix) — TSO v4/v6, USO v4/v6, FinishChecksum on TCP and UDP, an odd checksum start, and a
     field straddling two blocks (summed by the segment kernel instead). With `grid`, a 1-workgroup
-    seal grid (NEB_SINGLE_MAX_GRID) leaves a partial last pass to the tail kernel, whose segments
+    seal grid (NEB_KNOB_SINGLE_MAX_GRID) leaves a partial last pass to the tail kernel, whose segments
     the segment kernel sums."""
     import segment_oracle as S
     from test_segment_oracle import build_udpv4_single
 
     if grid is not None:
-        monkeypatch.setenv("NEB_SINGLE_MAX_GRID", str(grid))
+        knobs(L.KNOB_SINGLE_MAX_GRID, grid)
     rng = random.Random(77)
     P = []
     for i in range(24):

@@ -13,5 +13,5 @@ step() {  # name timeout cmd...
 }
 step probe 120 python tools/probe.py
 step smoke 300 python __graft_entry__.py smoke
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 step bench 400 python bench.py --steps 20 --warmup 5
