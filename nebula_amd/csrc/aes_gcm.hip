@@ -35,6 +35,7 @@
 #include "device_common.hpp"
 #include "knobs.hpp"
 #include "layout.hpp"
+#include "rxwin.hpp"
 #include "sched.hpp"
 #include "timing.hpp"
 
@@ -604,6 +605,9 @@ struct GcmArgs {
     // single-key kernel: the waves of its grid (packets past its full passes are left to
     // gcm_single_tail_kernel), 0 = it takes every packet itself
     uint32_t tail_slots;
+    // the device receive's settle and window finish in the epilogue (rxwin.hpp RxFold), or null:
+    // desc is then the admitted packets compacted, and status the receive's, by arrival index
+    const RxFold* rx;
 };
 
 struct PktShape {
@@ -929,17 +933,16 @@ __device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uin
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
-// sdesc (optional): the packet's descriptor in the scheduler's sorted copy (one contiguous read per
-// chunk instead of a gather behind the index load).
+// own (optional): the packet's descriptor itself, not args.desc[p] (the per-packet kernel's, rebased).
 template <bool OPEN, bool CS = false, class GH, class TL>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
                                                  uint32_t lane, uint32_t lg, const uint4* cs_pow = nullptr,
-                                                 const neb_desc* sdesc = nullptr) {
+                                                 const neb_desc* own = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     neb_desc d = {};
-    if (valid) d = sdesc ? *sdesc : args.desc[p];
+    if (valid) d = own ? *own : args.desc[p];
     uint32_t st = NEB_STATUS_OK;
     if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
     if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
@@ -1063,7 +1066,10 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         if (run && cs_on && l == LPP - 1u) V = xor4(V, gcm_csum_fix(d, sh.n, sh.na, cs_acc, cs_fk, args.arena, cs_pow));
     }
     if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
-    if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
+    if (OPEN && args.rx)  // (every lane: the settle aggregates over the wave)
+        rx_fold_settle(*args.rx, args.status, p, (int32_t)st, valid && l == LPP - 1u);
+    else if (valid && l == LPP - 1u)
+        args.status[p] = (int32_t)st;
 }
 
 __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rks[60]) {
@@ -1301,7 +1307,7 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
     const GhShoup64 gh{lds.m16, lds.shoup, lds.pos, lds.hi};
     const bool key_ok = key < a.max_keys && __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
     uint8_t* base = const_cast<uint8_t*>(ka + offsetof(OneArgs, in));
-    GcmArgs ga{nullptr, 1u, base, a.keys, a.max_keys, key, a.status, nullptr, 0u, 0u};
+    GcmArgs ga{nullptr, 1u, base, a.keys, a.max_keys, key, a.status, nullptr, 0u, 0u, nullptr};
     // the host passed the output's address in dst_off: rebase it on the argument block (wrapping)
     neb_desc d = a.d;
     d.dst_off = a.d.dst_off - (uint64_t)(uintptr_t)base;
@@ -1366,11 +1372,9 @@ __device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t
 
 struct ChunkArgs {
     const uint32_t* sorted;
-    const neb_desc* sdesc;  // descriptors in `sorted` order (the split passes)
     const uint4* chunks;
     uint32_t* counters;  // the scheduler's counters (sched.hpp kCnt*)
     uint32_t max_chunks, max_short;
-    uint32_t umax;  // the GHASH pass's largest aggregation (1..3; NEB_GH_UMAX, A/B)
 };
 
 // Chunk order: the chunks of each kind come longest first (size class). Workgroup w owns chunks w,
@@ -1452,8 +1456,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                 const uint32_t q = g0 + (ln >> 2);
                 const bool valid = q < count;
                 const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-                gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u, nullptr,
-                                       ca.sdesc ? ca.sdesc + start + q : nullptr);
+                gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
             }
         } else {
             const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
@@ -1465,8 +1468,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             const bool valid = q < count;
             const uint32_t p = valid ? ca.sorted[start + q] : 0u;
             const GhChunkTree gh{wtab, wpos};
-            gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg, nullptr,
-                                   ca.sdesc ? ca.sdesc + start + q : nullptr);
+            gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
@@ -1477,401 +1479,6 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                        (full ? 2u : (uint32_t)__builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift)) << 4 | (full ? 1u : 0u),
                    c, tc0, __builtin_amdgcn_s_memrealtime());
 #endif
-        c = cn;
-    }
-}
-
-// ---- mixed keys, in two passes (round 4): the CTR pass and the GHASH pass ----------------------
-//
-// The fused chunk kernel above needs one key per wave for both halves of GCM, so a wave's lanes
-// idle whenever a key's packets do not fill its groups (C3: ≈ 16 packets per key, 87% of the
-// lane-rounds busy) and the per-wave GHASH tables leave room for the two-table AES only. But only
-// GHASH needs per-key tables: the AES-CTR half needs a key's round keys, which fit in each lane's
-// registers. So a mixed-key batch runs as
-//  * gcm_ctr_kernel: keystream, payload XOR and E_K(J0) of every packet, 16 packets of the
-//    scheduler's order per group at 4 lanes each, each lane with its own packet's round keys in
-//    VGPRs — groups need not be single-key, so they are full (C3 and C5: all but the last), and
-//    the four-table AES fills the LDS (128 KiB, nothing per wave) as in the single-key kernel;
-//  * gcm_ghash_kernel: GHASH over AAD || CT || lengths per single-key chunk of the scheduler (the
-//    fused kernel's chunk shapes and per-wave tables), with no AES and no T-tables — a quarter of
-//    the LDS work, so its partly filled groups cost a quarter as much.
-// seal: CTR (ciphertext into dst, E_K(J0) into the tag slot), then GHASH (tag = E_K(J0) ^ S there,
-//       statuses);
-// open: GHASH (S into the scheduler's per-packet sums), then CTR (plaintext into dst, the tag
-//       checked against E_K(J0) ^ S, the payload zeroed on a mismatch, statuses).
-
-struct RkLane {  // per-lane round keys (VGPRs): the lanes of a CTR group hold their own packets' keys
-    uint32_t k[60];
-    static constexpr bool kUniform = false;
-    __device__ __forceinline__ uint4 get(int r) const {
-        return make_uint4(k[4 * r], k[4 * r + 1], k[4 * r + 2], k[4 * r + 3]);
-    }
-    __device__ __forceinline__ void load(const uint32_t* rec, bool run, uint32_t) {
-#pragma unroll
-        for (int i = 0; i < 15; i++) {
-            const uint4 v = run ? ld_rec4(rec, kRecRoundKeys + 4u * i) : make_uint4(0, 0, 0, 0);
-            k[4 * i] = v.x;
-            k[4 * i + 1] = v.y;
-            k[4 * i + 2] = v.z;
-            k[4 * i + 3] = v.w;
-        }
-    }
-};
-// The same keys spread over the packet's quad of lanes: lane w holds word w of every round key (15
-// VGPRs instead of 60), and a round's key is broadcast across the quad by four DPP moves (+4 VALU
-// per AES round). A quad's lanes are active together (a packet's lanes share its round count).
-struct RkQuad {
-    uint32_t q[15];
-    static constexpr bool kUniform = false;
-    __device__ __forceinline__ uint4 get(int r) const {
-        return make_uint4((uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0x00, 0xF, 0xF, false),
-                          (uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0x55, 0xF, 0xF, false),
-                          (uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0xAA, 0xF, 0xF, false),
-                          (uint32_t)__builtin_amdgcn_mov_dpp((int)q[r], 0xFF, 0xF, 0xF, false));
-    }
-    __device__ __forceinline__ void load(const uint32_t* rec, bool run, uint32_t lane) {
-        const uint32_t w = lane & 3u;
-#pragma unroll
-        for (int i = 0; i < 15; i++) q[i] = run ? rec[kRecRoundKeys + 4u * i + w] : 0u;
-    }
-};
-
-// One CTR group: packet p on lanes 4·(lane/4) .. +3. A packet's AES blocks are its m ciphertext
-// blocks (counters 2 .. m+1) and J0 (counter 1): block j = 4r + l in round r on lane l, J0 last.
-// CtrPkt holds what a group loads before its rounds (ctr_fetch), so a wave's first group can be
-// fetched while the workgroup fills its T-tables.
-template <class RK>
-struct CtrPkt {
-    neb_desc d;
-    uint32_t p;
-    uint32_t st;
-    bool valid;
-    RK rk;
-};
-template <class RK>
-__device__ __forceinline__ CtrPkt<RK> ctr_fetch(const GcmArgs& args, const uint32_t* sorted, const neb_desc* sdesc,
-                                                uint32_t q, uint32_t npkt, bool open, uint32_t lane) {
-    CtrPkt<RK> c;
-    c.valid = q < npkt;
-    c.p = c.valid ? sorted[q] : 0u;
-    c.d = neb_desc{};
-    if (c.valid) c.d = sdesc[q];
-    const bool key_in = c.d.key_id < args.max_keys;
-    const uint32_t* rec = args.keys + (size_t)(key_in ? c.d.key_id : 0u) * kKeyRecDwords;
-    c.st = NEB_STATUS_OK;
-    if (!key_in || rec[kRecAlg] != NEB_ALG_AESGCM) c.st = NEB_STATUS_BAD_KEY;
-    if (!open && c.st == NEB_STATUS_OK && c.d.counter >= kRejectAfterMessages) c.st = NEB_STATUS_EXHAUSTED;
-    c.rk.load(rec, c.valid && c.st == NEB_STATUS_OK, lane);
-    return c;
-}
-
-template <bool OPEN, class TL, class RK>
-__device__ __forceinline__ void gcm_ctr_group(const GcmArgs& args, const CtrPkt<RK>& cp, const TL& T, uint32_t lane,
-                                              const uint4* sums) {
-    const uint32_t l = lane & 3u;
-    const neb_desc& d = cp.d;
-    const uint32_t p = cp.p, st = cp.st;
-    const bool valid = cp.valid;
-    const RK& rk = cp.rk;
-    const bool run = valid && st == NEB_STATUS_OK;
-    const uint32_t hdr = args.hdr_from_dst ? d.flags & kCsHdrMask : 0u;
-    const uint32_t m = (d.len + 15u) >> 4;
-    const uint32_t R = run ? (m + 4u) >> 2 : 0u;  // m + 1 blocks over 4 lanes
-    const uint32_t c1 = bswap32((uint32_t)(d.counter >> 32)), c2 = bswap32((uint32_t)d.counter);
-    uint4 ej0 = make_uint4(0, 0, 0, 0);
-    auto rounds = [&](auto cm) {
-        constexpr int CM = decltype(cm)::value;
-        CtrConst cc{};
-        if constexpr (CM == 2) cc = aes_ctr_prep8(c1, c2, T, rk);
-        else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
-        for (uint32_t r = 0; __any(r < R); r++) {
-            if (r < R) {
-                const uint32_t j = 4u * r + l, off = 16u * j;
-                const bool is_ct = j < m, is_j0 = j == m;
-                // a common round: every active lane a full ciphertext block at a 16-B aligned
-                // destination (source: dword-aligned or shifted, as in gcm_packet_group)
-                const bool fast = __all(is_ct && off + 16u <= d.len && off >= hdr &&
-                                        ((d.dst_off | (uint32_t)(uintptr_t)args.arena) & 15u) == 0u);
-                uint4 pre = make_uint4(0, 0, 0, 0);
-                if (fast) {
-                    const uint8_t* sp = args.arena + d.src_off + off;
-                    pre = __all(((uint32_t)(uintptr_t)sp & 3u) == 0u) ? load_u4_a4(sp) : load_shifted16(sp);
-                }
-                LaneBlock b;
-                b.ctr = is_ct ? j + 2u : 1u;
-                const uint4 ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
-                if (fast) {
-                    *reinterpret_cast<uint4*>(args.arena + d.dst_off + off) = xor4(pre, ks);
-                } else if (is_ct) {
-                    const uint32_t nb = min(16u, d.len - off);
-                    const uint4 in = off < hdr ? load_block_hdr(args.arena + d.dst_off + off, args.arena + d.src_off + off,
-                                                                nb, hdr - off)
-                                               : load_block(args.arena + d.src_off + off, nb);
-                    store_block(args.arena + d.dst_off + off, xor4(in, mask_block(ks, nb)), nb);
-                }
-                if (is_j0) ej0 = ks;
-            }
-        }
-    };
-    if (__all(m + 1u < 256u)) rounds(std::integral_constant<int, 2>{});
-    else if (__all(m + 1u < 65536u)) rounds(std::integral_constant<int, 1>{});
-    else rounds(std::integral_constant<int, 0>{});
-    const uint32_t jl = m & 3u;  // the lane that computed E_K(J0)
-    if constexpr (!OPEN) {
-        // the GHASH pass turns it into the tag (E_K(J0) ^ S) and writes the status
-        if (run && l == jl) store_block(args.arena + d.dst_off + d.len, ej0, 16);
-    } else {
-        uint32_t fail = 0;
-        if (run && l == jl) {
-            const uint4 tag = xor4(ej0, bswap4(sums[p]));
-            const uint4 df = xor4(load_block(args.arena + d.src_off + d.len, 16), tag);
-            fail = (df.x | df.y | df.z | df.w) != 0u;
-        }
-        fail = (uint32_t)__shfl((int)fail, (int)((lane & ~3u) | jl));
-        if (run && fail)
-            for (uint32_t off = 16u * l; off < d.len; off += 64u)
-                store_block(args.arena + d.dst_off + off, make_uint4(0, 0, 0, 0), min(16u, d.len - off));
-        if (valid && l == jl) args.status[p] = run ? (fail ? NEB_STATUS_AUTH_FAILED : NEB_STATUS_OK) : (int32_t)st;
-    }
-}
-
-constexpr int kCtrWaves = 16;
-constexpr int kCtrThreads = kCtrWaves * kWave;
-struct CtrLds {
-    uint2 ttab[2 * 256 * 32];  // 128 KiB (T0,T1) and (T2,T3) pairs, 32 copies each (TLook4)
-};
-
-// Groups of 16 consecutive packets of the scheduler's order (sorted: bins by size class, then key,
-// so a group's packets are alike in size); group g on workgroup g mod G, as in gcm_single_kernel.
-// QUAD: the round keys spread over each packet's quad (RkQuad), else whole in every lane (RkLane).
-template <bool OPEN, bool QUAD>
-__global__ __launch_bounds__(kCtrThreads, 4) void gcm_ctr_kernel(GcmArgs args, const uint32_t* __restrict__ sorted,
-                                                                 const neb_desc* __restrict__ sdesc,
-                                                                 const uint4* __restrict__ sums) {
-    using RK = std::conditional_t<QUAD, RkQuad, RkLane>;
-    __shared__ CtrLds lds;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    uint32_t npkt = args.npkt;
-    if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
-    const uint32_t ngroups = (npkt + kPpw - 1u) / kPpw;
-    if (blockIdx.x >= ngroups) return;  // uniform over the workgroup
-    // the wave's first group is fetched (index, descriptor, key) before the T-table fill, so its
-    // chain of dependent loads runs under the fill instead of after it
-    uint32_t grp = blockIdx.x + wave * gridDim.x;
-    CtrPkt<RK> cp = ctr_fetch<RK>(args, sorted, sdesc, grp * kPpw + (lane >> 2), npkt, OPEN, lane);
-    fill_ttab<2u * 256u * 32u, kCtrThreads>(lds.ttab, tid, ttab4_entry);
-    __syncthreads();
-    const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
-    const uint32_t slots = gridDim.x * kCtrWaves;
-    for (; grp < ngroups; grp += slots) {
-        gcm_ctr_group<OPEN>(args, cp, T, lane, sums);
-        if (grp + slots < ngroups)
-            cp = ctr_fetch<RK>(args, sorted, sdesc, (grp + slots) * kPpw + (lane >> 2), npkt, OPEN, lane);
-    }
-}
-
-// The GHASH half of a packet group of the mixed-key split (lanes and padding as gcm_packet_group:
-// lane l owns padded blocks 2^lg·r + l + 1 of AAD || CT || lengths), reading the ciphertext (seal:
-// written by the CTR pass at dst; open: at src). Without the AES a round is a few hundred cycles,
-// shorter than a block's load from memory, so the rounds are aggregated U at a time:
-//   A <- A·H^(U·L) ⊕ X_0·H^((U-1)·L) ⊕ ... ⊕ X_(U-2)·H^L ⊕ X_(U-1)      (L = 2^lg lanes per packet)
-// — U independent products reduced once, only the first on the dependent chain, and the next U
-// blocks loaded while they run. pos + 128·k: the position tables of H^((k+1)·L), k < U. A packet
-// whose round count is not a multiple of U starts with zero rounds (a zero block leaves a Horner
-// sum from zero unchanged).
-template <bool OPEN, int U, class GH>
-__device__ __forceinline__ void ghash_packet_group(const GcmArgs& args, const ChunkArgs& ca, uint32_t q, bool valid,
-                                                   uint32_t expect_key, bool key_ok, const GH& gh, uint32_t lane,
-                                                   uint32_t lg, uint4* sums, const uint4* pos) {
-    const uint32_t LPP = 1u << lg;
-    const uint32_t l = lane & (LPP - 1u);
-    uint32_t p = 0;
-    neb_desc d = {};
-    if (valid) {  // two independent loads: the index and the scheduler's copy of the descriptor
-        p = ca.sorted[q];
-        d = ca.sdesc[q];
-    }
-    uint32_t st = NEB_STATUS_OK;
-    if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
-    if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;
-    const bool run = valid && st == NEB_STATUS_OK;
-    PktShape sh;
-    sh.na = (d.aad_len + 15u) >> 4;
-    sh.m = (d.len + 15u) >> 4;
-    sh.n = sh.na + sh.m + 1u;
-    sh.R = run ? (sh.n + LPP - 1u) >> lg : 0u;
-    sh.pad = (sh.R << lg) - sh.n;
-    const uint32_t M = (sh.R + U - 1u) / U;      // aggregated rounds
-    const int32_t front = (int32_t)(U * M - sh.R);  // leading zero rounds
-    const uint8_t* ct = args.arena + (OPEN ? d.src_off : d.dst_off);
-    auto load = [&](int32_t r) -> uint4 {  // round r's GHASH input block (big-endian words)
-        uint4 X = make_uint4(0, 0, 0, 0);
-        if (r < 0 || (uint32_t)r >= sh.R) return X;
-        const LaneBlock b = lane_block(sh, (uint32_t)r, l, lg);
-        if (b.is_ct) {
-            const uint32_t off = 16u * (b.k - 1u);
-            const uint8_t* q = ct + off;
-            X = off + 16u <= d.len && ((uint32_t)(uintptr_t)q & 3u) == 0u ? load_u4_a4(q) : load_block(q, min(16u, d.len - off));
-        } else if (b.is_aad) {
-            const uint32_t off = 16u * (uint32_t)(b.g - 1);
-            X = load_block(args.arena + d.aad_off + off, min(16u, d.aad_len - off));
-        }
-        X = bswap4(X);
-        if (b.is_len) {
-            const uint64_t abits = (uint64_t)d.aad_len * 8u, cbits = (uint64_t)d.len * 8u;
-            X = make_uint4((uint32_t)(abits >> 32), (uint32_t)abits, (uint32_t)(cbits >> 32), (uint32_t)cbits);
-        }
-        return X;
-    };
-    uint4 A = make_uint4(0, 0, 0, 0);
-    uint4 X[U];
-#pragma unroll
-    for (int i = 0; i < U; i++) X[i] = load(i - front);
-    for (uint32_t mr = 0; __any(mr < M); mr++) {
-        uint4 Xn[U];
-#pragma unroll
-        for (int i = 0; i < U; i++) Xn[i] = load((int32_t)(U * (mr + 1u)) + i - front);
-        if (mr < M) {
-            if constexpr (U == 1) {
-                A = mr == 0u ? X[0] : xor4(gh.horner(A, lg), X[0]);
-            } else {
-                uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (mr) gf_acc_pos(A, pos + 128u * (U - 1), z);
-#pragma unroll
-                for (int i = 0; i < U - 1; i++) gf_acc_pos(X[i], pos + 128u * (U - 2 - i), z);
-                A = xor4(gf_reduce(z), X[U - 1]);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < U; i++) X[i] = Xn[i];
-    }
-    const uint4 V = gh.final(A, lane, lg);  // every lane: the final shuffles across lanes
-    if (l == LPP - 1u) {
-        if constexpr (!OPEN) {
-            if (run) {
-                uint8_t* tp = args.arena + d.dst_off + d.len;
-                store_block(tp, xor4(load_block(tp, 16), bswap4(V)), 16);  // E_K(J0) ^ S
-            }
-            if (valid) args.status[p] = (int32_t)st;
-        } else {
-            if (run) sums[p] = V;
-        }
-    }
-}
-
-constexpr int kGhWaves = 8;
-constexpr int kGhThreads = kGhWaves * kWave;
-#ifndef NEB_GH_WPE
-#define NEB_GH_WPE 4  // launch bound: waves per SIMD (2 workgroups of 8 waves per CU; 5 spills)
-#endif
-constexpr int kGhMaxU = 3;
-struct GhLds {
-    uint4 shoup[kGhWaves][4][16];          // per wave: M_1..M_4 (full chunks), M_1, M_2, M_4, M_8 (tails)
-    uint4 pos[kGhWaves][kGhMaxU][8 * 16];  // per wave: position tables of H^4, H^8, H^12 (tails: H^(2^lg))
-};
-
-// A chunk key's GHASH tables for the GHASH pass, copied from the record: lane L loads entry L of
-// the Shoup tables and entries L, L + 64 of each position table — front chunks M_1..M_4 and the
-// position tables of H^4 (the full table's first 8 positions), H^8, H^12; tails M_1, M_2, M_4, M_8
-// and those of H^(2^lg).
-template <bool FULL>
-__device__ __forceinline__ void stage_gh_tables(const uint32_t* rec, uint32_t lane, uint32_t lg, uint4* wtab,
-                                                uint4* wpos) {
-    const uint32_t t = lane >> 4, v = lane & 15u;
-    const uint4 sv = ld_rec4(rec, (FULL ? kRecShoup + 64u * t : rec_shoup_pow2(t)) + 4u * v);
-    if constexpr (FULL) {
-        const uint32_t src[kGhMaxU] = {kRecFull, kRecPos8, kRecPos12};
-        uint4 e[2 * kGhMaxU];
-#pragma unroll
-        for (int k = 0; k < kGhMaxU; k++) {
-            e[2 * k] = ld_rec4(rec, src[k] + 4u * lane);
-            e[2 * k + 1] = ld_rec4(rec, src[k] + 4u * (64u + lane));
-        }
-        wtab[lane] = sv;
-#pragma unroll
-        for (int k = 0; k < kGhMaxU; k++) {
-            wpos[128u * k + lane] = e[2 * k];
-            wpos[128u * k + 64u + lane] = e[2 * k + 1];
-        }
-    } else {
-        const uint32_t src = rec_pos_table(lg);
-        const uint4 e0 = ld_rec4(rec, src + 4u * lane), e1 = ld_rec4(rec, src + 4u * (64u + lane));
-        wtab[lane] = sv;
-        wpos[lane] = e0;
-        wpos[64u + lane] = e1;
-    }
-}
-
-// The scheduler's chunks (sched.hpp), owned and drawn as in gcm_chunk_kernel (workgroup w: chunks
-// w, w + G, ..., its waves through an LDS cursor one chunk ahead).
-template <bool OPEN>
-__global__ __launch_bounds__(kGhThreads, NEB_GH_WPE) void gcm_ghash_kernel(GcmArgs args, ChunkArgs ca, uint4* sums) {
-    __shared__ GhLds lds;
-    __shared__ uint32_t wg_cursor;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
-    const uint32_t nlong = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
-    const uint32_t nback = nlong + min(__builtin_amdgcn_readfirstlane(ca.counters[kCntShortChunks]), ca.max_short);
-    const uint32_t nch = nfront + nback;
-    if (blockIdx.x >= nch) return;
-    if (tid == 0) wg_cursor = kGhWaves;
-    __syncthreads();
-    uint4* wtab = &lds.shoup[wave][0][0];
-    uint4* wpos = &lds.pos[wave][0][0];
-    auto chunk_at = [&](uint32_t c) {
-        return ca.chunks[c < nfront ? c : c < nfront + nlong ? ca.max_chunks - 1u - (c - nfront) : ca.max_chunks + (c - nfront - nlong)];
-    };
-    auto chunk_of = [&](uint32_t k) -> uint32_t { return blockIdx.x + k * gridDim.x; };
-    uint32_t c = 0;
-    if (lane == 0u) c = chunk_of(wave);
-    c = __builtin_amdgcn_readfirstlane(c);
-    uint4 ch_next = make_uint4(0, 0, 0, 0);
-    if (c < nch) ch_next = chunk_at(c);
-    while (c < nch) {
-        const uint4 ch = ch_next;
-        const bool full = c < nfront;
-        uint32_t cn = 0;
-        if (lane == 0u) cn = chunk_of(atomicAdd(&wg_cursor, 1u));
-        cn = __builtin_amdgcn_readfirstlane(cn);
-        if (cn < nch) ch_next = chunk_at(cn);
-        uint32_t ln = lane;
-        asm volatile("" : "+v"(ln));
-        const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
-        const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
-        const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
-        const uint32_t cls = __builtin_amdgcn_readfirstlane(ch.w & ((1u << kChunkLgShift) - 1u));
-        const uint32_t* rec = args.keys + (size_t)(key < args.max_keys ? key : 0u) * kKeyRecDwords;
-        const bool key_ok = key < args.max_keys && rec[kRecAlg] == NEB_ALG_AESGCM;
-        if (full) {
-            stage_gh_tables<true>(rec, ln, 2u, wtab, wpos);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const GhChunk4 gh{wtab, wpos};
-            // aggregation by size class (rounds at 4 lanes: class 0 one, 1-2 up to 4, else 5+)
-            for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
-                const uint32_t q = g0 + (ln >> 2);
-                const bool valid = q < count;
-                if (cls >= 3u && ca.umax >= 3u)
-                    ghash_packet_group<OPEN, 3>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
-                else if (cls >= 1u && ca.umax >= 2u)
-                    ghash_packet_group<OPEN, 2>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
-                else ghash_packet_group<OPEN, 1>(args, ca, start + q, valid, key, key_ok, gh, ln, 2u, sums, wpos);
-            }
-        } else {
-            const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
-            stage_gh_tables<false>(rec, ln, lg, wtab, wpos);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t q = ln >> lg;
-            const bool valid = q < count;
-            const GhChunkTree gh{wtab, wpos};
-            ghash_packet_group<OPEN, 1>(args, ca, start + q, valid, key, key_ok, gh, ln, lg, sums, wpos);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         c = cn;
     }
 }
@@ -2171,8 +1778,8 @@ static void launch_k(K kern, dim3 grid, dim3 block, hipStream_t s, hipEvent_t st
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                           int hdr_from_dst, hipEvent_t stop) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
+                                           int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx) {
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, 0u, rx};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
     const bool cs = !open && hdr_from_dst == 2;  // the TX seal with its checksums (tx.hip)
     if (!d_n && !cs && n <= neb::kSmallBatch) {
@@ -2267,12 +1874,12 @@ extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len
 
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
-                                            const uint32_t* d_sorted, const neb_desc* d_sdesc, const uint4* d_chunks,
+                                            const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst,
-                                            hipEvent_t stop) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u};
-    neb::ChunkArgs ca{d_sorted, d_sdesc, d_chunks, d_counters, max_chunks, max_short, 1u};
+                                            hipEvent_t stop, const neb::RxFold* rx) {
+    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u, rx};
+    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks, max_short};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
     // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.
@@ -2280,48 +1887,4 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
     // stop (optional): an event bound to the kernel's dispatch (no marker packet after it)
     return open ? launch_grid_stop(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, stop, a, ca)
                 : launch_grid_stop(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, stop, a, ca);
-}
-
-// Mixed keys in two passes (gcm_ctr_kernel + gcm_ghash_kernel): seal CTR then GHASH, open GHASH then
-// CTR. d_sums: 16 B per packet (the open's GHASH values between the passes).
-template <bool OPEN>
-static hipError_t launch_split(const neb::GcmArgs& a, const neb::ChunkArgs& ca, uint32_t max_chunks, uint4* d_sums,
-                               int cu_count, hipStream_t s) {
-    const uint32_t groups = (a.npkt + neb::kPpw - 1u) / neb::kPpw;
-    // NEB_CTR_RK=lane: every lane holds its packet's 60 round-key words (A/B against the quad form)
-    static const bool lane_rk = [] {
-        const char* v = std::getenv("NEB_CTR_RK");
-        return v && !std::strcmp(v, "lane");
-    }();
-    auto ctr = [&]() {
-        if (lane_rk)
-            return launch_grid(neb::gcm_ctr_kernel<OPEN, false>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves,
-                               cu_count, s, a, ca.sorted, ca.sdesc, (const uint4*)d_sums);
-        return launch_grid(neb::gcm_ctr_kernel<OPEN, true>, neb::kCtrThreads, groups * (uint32_t)neb::kCtrWaves,
-                           cu_count, s, a, ca.sorted, ca.sdesc, (const uint4*)d_sums);
-    };
-    auto gh = [&]() {
-        return launch_grid(neb::gcm_ghash_kernel<OPEN>, neb::kGhThreads, max_chunks * (uint32_t)neb::kGhWaves, cu_count,
-                           s, a, ca, d_sums);
-    };
-    hipError_t e = OPEN ? gh() : ctr();
-    if (e != hipSuccess) return e;
-    return OPEN ? ctr() : gh();
-}
-
-extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                                          uint8_t* d_arena, const uint32_t* d_keys, uint32_t max_keys,
-                                          int32_t* d_status, const uint32_t* d_sorted, const neb_desc* d_sdesc,
-                                          const uint4* d_chunks, uint32_t* d_counters, uint32_t max_chunks,
-                                          uint32_t max_short, uint4* d_sums, int cu_count, hipStream_t s,
-                                          int hdr_from_dst) {
-    neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, d_n, (uint32_t)hdr_from_dst, 0u};
-    static const uint32_t umax = [] {
-        const char* v = std::getenv("NEB_GH_UMAX");
-        const int u = v ? std::atoi(v) : 3;
-        return (uint32_t)(u < 1 ? 1 : u > 3 ? 3 : u);
-    }();
-    neb::ChunkArgs ca{d_sorted, d_sdesc, d_chunks, d_counters, max_chunks, max_short, umax};
-    return open ? launch_split<true>(a, ca, max_chunks, d_sums, cu_count, s)
-                : launch_split<false>(a, ca, max_chunks, d_sums, cu_count, s);
 }

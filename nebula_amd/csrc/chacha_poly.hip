@@ -24,6 +24,7 @@
 #include "../../include/nebula_aead.h"
 #include "device_common.hpp"
 #include "layout.hpp"
+#include "rxwin.hpp"
 #include "timing.hpp"
 
 namespace neb {
@@ -236,7 +237,17 @@ struct ChachaArgs {
     int32_t* status;
     const uint32_t* npkt_dev;  // optional: the batch's packet count in device memory (min with npkt)
     uint32_t hdr_from_dst;     // TX batches: the first `flags` plaintext bytes from dst (GcmArgs)
+    const RxFold* rx;          // the device receive's epilogue (GcmArgs::rx), or null
 };
+
+// packet p's status, by its 16th lane; with a receive epilogue every lane takes part (RxFold)
+template <bool OPEN>
+__device__ __forceinline__ void chacha_status(const ChachaArgs& args, uint32_t p, uint32_t st, bool holder) {
+    if (OPEN && args.rx)
+        rx_fold_settle(*args.rx, args.status, p, (int32_t)st, holder);
+    else if (holder)
+        args.status[p] = (int32_t)st;
+}
 
 // Payload and AAD blocks loaded one round ahead of their use (1) or in their round (0). Off: a
 // round ahead measured 2-3% slower on C4 (110.0 vs 107.1 µs per seal launch, rocprof A/B,
@@ -276,8 +287,8 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
         uint32_t rmax = nrounds;
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 16));
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 32));
-        if (rmax == 0u) {
-            if (valid && l == 15u) args.status[p] = (int32_t)st;
+        if (rmax == 0u) {  // (wave-uniform)
+            chacha_status<OPEN>(args, p, st, valid && l == 15u);
             return;
         }
 
@@ -347,36 +358,34 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
             }
             A = p5_add(p5_mul(A, r16), mi);
         }
-        if (!run) {
-            if (valid && l == 15u) args.status[p] = (int32_t)st;
-            return;
-        }
-        // lane l's last block is e_l = ((t - l - 1) mod 16) + 1 blocks from the end
-        const uint32_t e = ((t - l - 1u) & 15u) + 1u;
-        P5 re = p5_shfl(pw, (int)(pbase | (e - 1u)));
-        P5 h = p5_mul(A, re);
+        if (run) {  // (the packet's 16 lanes alike: the shuffles stay within the packet)
+            // lane l's last block is e_l = ((t - l - 1) mod 16) + 1 blocks from the end
+            const uint32_t e = ((t - l - 1u) & 15u) + 1u;
+            P5 re = p5_shfl(pw, (int)(pbase | (e - 1u)));
+            P5 h = p5_mul(A, re);
 #pragma unroll
-        for (int s = 1; s < 16; s <<= 1) h = p5_add(h, p5_shfl_xor(h, s));
-        uint4 tag = p5_finish(h, sk);
-        uint32_t fail = 0;
-        if (l == 15u) {
-            if constexpr (!OPEN) {
-                store_block(arena + d.dst_off + d.len, tag, 16);
-            } else {
-                uint4 rt = load_block(arena + d.src_off + d.len, 16);
-                uint4 df = xor4c(rt, tag);
-                fail = (df.x | df.y | df.z | df.w) != 0u;
+            for (int s = 1; s < 16; s <<= 1) h = p5_add(h, p5_shfl_xor(h, s));
+            uint4 tag = p5_finish(h, sk);
+            uint32_t fail = 0;
+            if (l == 15u) {
+                if constexpr (!OPEN) {
+                    store_block(arena + d.dst_off + d.len, tag, 16);
+                } else {
+                    uint4 rt = load_block(arena + d.src_off + d.len, 16);
+                    uint4 df = xor4c(rt, tag);
+                    fail = (df.x | df.y | df.z | df.w) != 0u;
+                }
+            }
+            if constexpr (OPEN) {
+                fail = (uint32_t)__shfl((int)fail, (int)(pbase | 15u));
+                if (fail) {
+                    for (uint32_t off = 16u * l; off < d.len; off += 256u)
+                        store_block(arena + d.dst_off + off, make_uint4(0, 0, 0, 0), min(16u, d.len - off));
+                    st = NEB_STATUS_AUTH_FAILED;
+                }
             }
         }
-        if constexpr (OPEN) {
-            fail = (uint32_t)__shfl((int)fail, (int)(pbase | 15u));
-            if (fail) {
-                for (uint32_t off = 16u * l; off < d.len; off += 256u)
-                    store_block(arena + d.dst_off + off, make_uint4(0, 0, 0, 0), min(16u, d.len - off));
-                st = NEB_STATUS_AUTH_FAILED;
-            }
-        }
-        if (l == 15u) args.status[p] = (int32_t)st;
+        chacha_status<OPEN>(args, p, st, valid && l == 15u);
     }
 }
 
@@ -412,7 +421,7 @@ __global__ __launch_bounds__(kWave) void chacha_one_kernel(ChOneArgs a) {
     uint8_t* base = reinterpret_cast<uint8_t*>(kb);
     neb_desc d = a.d;
     d.dst_off = a.d.dst_off - (uint64_t)(uintptr_t)base;
-    const ChachaArgs ca{nullptr, 1u, base, a.keys, a.max_keys, a.key, a.status, nullptr, 0u};
+    const ChachaArgs ca{nullptr, 1u, base, a.keys, a.max_keys, a.key, a.status, nullptr, 0u, nullptr};
     chacha_group<OPEN>(ca, 0u, 1u, [&](uint32_t) { return d; });
 }
 
@@ -488,7 +497,7 @@ extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                       int hdr_from_dst, hipEvent_t stop) {
-    neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst};
+                                       int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx) {
+    neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, rx};
     return open ? launch_chacha<true>(a, cu_count, s, stop) : launch_chacha<false>(a, cu_count, s, stop);
 }

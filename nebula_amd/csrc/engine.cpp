@@ -25,6 +25,7 @@
 #include "knobs.hpp"
 #include "host_common.hpp"
 #include "layout.hpp"
+#include "rxwin.hpp"
 #include "sched.hpp"
 #include "timing.hpp"
 #include "tx.hpp"
@@ -39,7 +40,7 @@ extern "C" hipError_t neb_fence_keys(const neb_desc* in, neb_desc* out, uint32_t
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                           int hdr_from_dst, hipEvent_t stop);
+                                           int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx);
 extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in, uint32_t in_len,
                                   uint32_t len, uint64_t counter, uint8_t* out, int32_t* status, const uint32_t* d_keys,
                                   uint32_t max_keys, uint32_t key, hipStream_t s);
@@ -48,15 +49,10 @@ extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_
                                      const uint32_t* d_keys, uint32_t max_keys, uint32_t key, hipStream_t s);
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
-                                            const uint32_t* d_sorted, const neb_desc* d_sdesc, const uint4* d_chunks,
+                                            const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
-                                            int cu_count, hipStream_t s, int hdr_from_dst, hipEvent_t stop);
-extern "C" hipError_t neb_gcm_batch_split(int open, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                                          uint8_t* d_arena, const uint32_t* d_keys, uint32_t max_keys,
-                                          int32_t* d_status, const uint32_t* d_sorted, const neb_desc* d_sdesc,
-                                          const uint4* d_chunks, uint32_t* d_counters, uint32_t max_chunks,
-                                          uint32_t max_short, uint4* d_sums, int cu_count, hipStream_t s,
-                                          int hdr_from_dst);
+                                            int cu_count, hipStream_t s, int hdr_from_dst, hipEvent_t stop,
+                                            const neb::RxFold* rx);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int hdr_from_dst);
 #ifndef NEB_TX_CSUM_SEAL
@@ -65,7 +61,7 @@ extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                       int hdr_from_dst, hipEvent_t stop);
+                                       int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx);
 
 // The stream a workspace's `done` event was last recorded on. A batch on that same stream is
 // ordered after it already and skips the cross-stream wait (a barrier packet that cost ≈ 5 µs between
@@ -795,8 +791,7 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     const size_t b_counters = align_up((neb::kSchedCounters + (size_t)neb::kSubBins * nb) * 4u, 256);
     const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up(((size_t)mc + ms) * 16u, 256);
-    const size_t b_sums = (size_t)cap * 16u, b_sdesc = align_up((size_t)cap * sizeof(neb_desc), 256);
-    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_sums + b_sdesc;
+    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
     if (sp.mem) hipFree(sp.mem);
@@ -817,10 +812,6 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     sp.ws.sorted = (uint32_t*)m;
     m += b_idx;
     sp.ws.chunks = (uint4*)m;
-    m += b_chunks;
-    sp.ws.sums = (uint4*)m;
-    m += b_sums;
-    sp.ws.sdesc = (neb_desc*)m;
     sp.ws.max_chunks = mc;
     sp.ws.max_short = ms;
     sp.bytes = bytes;
@@ -831,17 +822,6 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     return hipSuccess;
 }
 
-// Mixed-key AES-GCM runs the fused chunk kernel (aes_gcm.hip gcm_chunk_kernel); NEB_MIXED_SPLIT=1 (read
-// per batch) runs the two-pass form instead (gcm_ctr_kernel + gcm_ghash_kernel, DESIGN.md §3.2: measured
-// slower on C3 and C5). NEB_SCHED_SDESC=1: the fused kernel reads the scheduler's sorted descriptor
-// copy (the split passes always do).
-static bool mixed_split() {  // (A/B knobs are read once: getenv is not safe beside setenv)
-    static const bool on = [] {
-        const char* v = std::getenv("NEB_MIXED_SPLIT");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
 // NEB_BIND_EVENTS=0 (read once): markers after each batch instead of events bound to its last
 // kernel's dispatch (the A/B of round 4's binding for mixed-key AES-GCM and ChaCha batches)
 static bool bind_events() {
@@ -851,49 +831,33 @@ static bool bind_events() {
     }();
     return on;
 }
-static bool sched_sdesc() {
-    static const bool on = [] {
-        const char* v = std::getenv("NEB_SCHED_SDESC");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
 
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
 // only known on the device, e.g. the segments of a TX batch). hdr_from_dst: the TX batch's
 // descriptors (tx.hip) read their first `flags` plaintext bytes from the destination.
-// host_arena: the arena is pinned host memory the kernels reach over PCIe (zero-copy batches, the
-// submission queue): mixed-key AES-GCM then runs the fused chunk kernel, which reads each packet
-// once — the split passes read the ciphertext twice and put two chains of PCIe-latency rounds
-// where the fused kernel has one.
+// rx (optional, opens only): the device receive's settle and window finish run in the open kernel's
+// epilogue (rxwin.hpp RxFold); d_desc is then the admitted packets compacted and d_status the
+// caller's statuses by arrival index.
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr,
                                SchedSpace* sched = nullptr, int hdr_from_dst = 0, hipEvent_t stop = nullptr,
-                               bool host_arena = false) {
+                               const neb::RxFold* rx = nullptr) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
             return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
-                                        e->cu_count, s, hdr_from_dst, stop);
+                                        e->cu_count, s, hdr_from_dst, stop, rx);
         // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
         hipError_t err = sched_reserve(e, sp, n, s);
         if (err == hipSuccess && !sp.last.same(s)) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
-        const bool split = !host_arena && mixed_split();
         neb::SchedWs ws = sp.ws;
-        if (!split && !sched_sdesc()) ws.sdesc = nullptr;
         if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &ws, s);
-        if (err == hipSuccess) {
-            if (split)
-                err = neb_gcm_batch_split(open, d_desc, n, d_n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                          sp.ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
-                                          sp.ws.sums, e->cu_count, s, hdr_from_dst);
-            else  // sp.done bound to the chunk kernel's dispatch: no marker packet between batches
-                err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                            ws.sdesc, sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short,
-                                            e->cu_count, s, hdr_from_dst, bind_events() ? sp.done : nullptr);
-        }
-        if (err == hipSuccess && (split || !bind_events())) err = hipEventRecord(sp.done, s);
+        if (err == hipSuccess)  // sp.done bound to the chunk kernel's dispatch: no marker packet between batches
+            err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
+                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, e->cu_count,
+                                        s, hdr_from_dst, bind_events() ? sp.done : nullptr, rx);
+        if (err == hipSuccess && !bind_events()) err = hipEventRecord(sp.done, s);
         if (err == hipSuccess) sp.last.set(s);
         if (err != hipSuccess) {
             // binning passes of this batch may already be queued on s: let them finish before the
@@ -904,7 +868,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         return err;
     }
     return neb_chacha_batch(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n, e->cu_count,
-                            s, hdr_from_dst, stop);
+                            s, hdr_from_dst, stop, rx);
 }
 
 // A per-packet call's result from its pool slot into the caller's buffer, by status: a sealed or
@@ -1076,9 +1040,9 @@ int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint) { return che
 
 // Open the first *d_n (a count in device memory) of at most n descriptors, on stream s.
 int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s) {
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx) {
     if (n == 0) return NEB_OK;
-    hipError_t err = launch_batch(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, s, d_n);
+    hipError_t err = launch_batch(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, s, d_n, nullptr, 0, nullptr, rx);
     if (err != hipSuccess) {
         set_error("batch launch", err);
         return NEB_ERR_HIP;
@@ -1101,7 +1065,7 @@ int neb_launch_on(neb_engine* e, int alg, int open, const neb_desc* desc, uint32
     if (n == 0) return NEB_OK;
     DeviceGuard dg(e->device);
     hipError_t err = launch_batch(e, alg, open, desc, n, arena, status, key_hint, s, nullptr,
-                                  static_cast<SchedSpace*>(sched), 0, nullptr, true);
+                                  static_cast<SchedSpace*>(sched), 0, nullptr);
     if (err != hipSuccess) {
         set_error("queue batch launch", err);
         return NEB_ERR_HIP;
@@ -1148,8 +1112,7 @@ static int batch_host_zero_copy(neb_engine* e, int alg, int open, const neb_desc
         d_desc = e->zc_desc;
     }
     if (!status_mapped) d_status = e->zc_status;
-    HIP_TRY(launch_batch(e, alg, open, d_desc, n, arena, d_status, key_hint, e->stream, nullptr, nullptr, 0, nullptr,
-                         true));
+    HIP_TRY(launch_batch(e, alg, open, d_desc, n, arena, d_status, key_hint, e->stream));
     if (!status_mapped)
         HIP_TRY(hipMemcpyAsync(status, d_status, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1318,7 +1281,7 @@ int neb_rx_pipe_submit(neb_engine* e, int alg, uint32_t key_hint, uint8_t* arena
     HIP_TRY(hipMemcpyAsync(r.d_desc + c0, r.h_desc + c0, (size_t)cnt * sizeof(neb_desc), hipMemcpyHostToDevice,
                            sl.stream));
     HIP_TRY(launch_batch(e, alg, 1, r.d_desc + c0, cnt, arena, r.d_status + c0, key_hint, sl.stream, nullptr,
-                         sl.sched, 0, nullptr, true));
+                         sl.sched));
     HIP_TRY(hipMemcpyAsync(r.h_status + c0, r.d_status + c0, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost,
                            sl.stream));
     HIP_TRY(hipEventRecord(sl.ev, sl.stream));

@@ -79,11 +79,39 @@ struct RxDevWs {
     uint64_t* exit_hi;
     uint64_t* recv;
     uint64_t* scratch;  // count x words
-    uint32_t* need_host;  // pinned host word: bit 0 when a touched window is risky or slow, bit 1 on
-                          // a lookback timeout (an internal error: the batch fails)
+    uint32_t* need_host;  // pinned host words: [0] nonzero when a touched window is risky or slow,
+                          // [1] nonzero on a lookback timeout (an internal error: the batch fails)
+    uint32_t* pending;    // per window: admitted packets whose verdict is not settled yet (RxFold)
+    struct RxFold* fold;  // device copy of this workspace's RxFold (the open kernels' epilogue)
     // the generation of the last batch whose packets named more than one window (written by the
     // keys kernel); any other value lets the sort passes write the identity order (one window)
     uint32_t* mixed;
+};
+
+// The receive's settle and window finish, folded into the open kernels' epilogue (aes_gcm.hip
+// gcm_packet_group, chacha_poly.hip chacha_group: GcmArgs::rx / ChachaArgs::rx). The open runs over
+// the admitted packets compacted by rx_scan_admit_kernel (sub_desc, position j); as a packet's
+// verdict is known, rx_fold_settle writes it at its arrival index, ORs its counter into the window's
+// scratch bitmap (or counts it as received when it leaves the window), and takes it off its
+// window's pending count. The wave whose decrement brings a window to zero has the window's last
+// verdict, so it finishes the window (rx_fold_finish) right there: the bitmap, lost count and
+// current of a window whose packets all verified, or only the scratch cleared for one that goes to
+// the host. No settle or finish launch after the open (round 5: 6 → 4 window launches).
+struct RxFold {
+    RxDevWin win;
+    const uint32_t* sub_map;  // position j of the open -> arrival index
+    int32_t* verdict;
+    const uint32_t* keyw;
+    const uint64_t* ctr;
+    uint32_t* wflag;
+    const uint64_t* curnew;
+    const uint64_t* exit_lo;
+    const uint64_t* exit_hi;
+    uint64_t* recv;
+    uint64_t* scratch;
+    uint32_t* pending;
+    const uint32_t* err;
+    uint32_t* need_host;
 };
 
 inline size_t rx_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -129,8 +157,151 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
     w.recv = (uint64_t*)take((size_t)count * 8);
     w.scratch = (uint64_t*)take((size_t)count * words * 8);
     w.mixed = (uint32_t*)take(4);
+    w.pending = (uint32_t*)take((size_t)count * 4);
+    w.fold = (RxFold*)take(sizeof(RxFold));
     if (ws) *ws = w;
     return off;
+}
+
+inline RxFold rx_fold_of(const RxDevWin& win, const RxDevWs& ws) {
+    return RxFold{win,        ws.sub_map, ws.verdict, ws.keyw,    ws.ctr,     ws.wflag, ws.curnew,
+                  ws.exit_lo, ws.exit_hi, ws.recv,    ws.scratch, ws.pending, ws.err,   ws.need_host};
+}
+
+__device__ __forceinline__ bool rx_fast_flag(uint32_t fl) { return (fl & kRxTouched) && !(fl & (kRxRisky | kRxSlow)); }
+
+// bits of the slots [a, b) within the word whose first slot is q0 (nb slots)
+__device__ __forceinline__ uint64_t rx_seg_mask(uint64_t q0, uint32_t nb, uint64_t a, uint64_t b) {
+    const uint64_t lo = max(a, q0), hi = min(b, q0 + nb);
+    if (lo >= hi) return 0;
+    const uint32_t m = (uint32_t)(hi - lo);
+    return (m == 64u ? ~0ull : ((1ull << m) - 1u)) << (lo - q0);
+}
+// ... within the circular slot range [start, start + count) mod len (start < len)
+__device__ __forceinline__ uint64_t rx_ring_mask(uint64_t q0, uint32_t nb, uint64_t start, uint64_t count,
+                                                 uint64_t len) {
+    if (count == 0) return 0;
+    if (count >= len) return nb == 64u ? ~0ull : ((1ull << nb) - 1u);
+    uint64_t m = rx_seg_mask(q0, nb, start, min(start + count, len));
+    if (start + count > len) m |= rx_seg_mask(q0, nb, 0, start + count - len);
+    return m;
+}
+
+// Window w's finish, by the whole wave, once every admitted packet of w has its verdict (the wave
+// whose pending decrement reached zero; every other settle's atomics completed before its own
+// decrement). The slots of the counters new in (cur0, cur] are cleared and the admitted counters
+// (the scratch bitmap) ORed in; the old window's counters that leave it are counted as received
+// where their old bit is set (tools/rxwin_model.py finish_ranges, checked against the oracle); then
+// the window's lost count and current. The scratch is read and cleared with atomic exchanges (it
+// was written by other workgroups' atomics in this launch). A window that goes to the host (a
+// failed verdict, a counter near the wrap) or a batch whose scan failed only gets its scratch
+// cleared.
+__device__ __forceinline__ void rx_fold_finish(const RxFold& f, uint32_t w) {
+    const uint32_t lane = __lane_id();
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(atomicOr(&f.wflag[w], 0u));
+    const bool fast = rx_fast_flag(fl) && *f.err == 0u;
+    const RxDevWin& win = f.win;
+    uint64_t* scr = f.scratch + ((size_t)w << win.words_lg);
+    uint64_t r = 0, cur = 0, lo = 1, hi = 0, cur0 = 0;
+    if (fast) {
+        cur0 = win.cur[w];
+        cur = f.curnew[w];
+        lo = f.exit_lo[w];
+        hi = f.exit_hi[w];
+    }
+    const uint64_t len = win.length, mask = len - 1u;
+    const uint32_t nb = len < 64u ? (uint32_t)len : 64u;
+    const uint64_t base = (cur >= len && cur - len > cur0) ? cur - len : cur0;
+    const uint64_t ehi = min(hi, cur0);
+    uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
+    for (uint32_t q = lane; q < win.words; q += 64u) {
+        const uint64_t s = atomicExch(reinterpret_cast<unsigned long long*>(scr + q), 0ull);
+        if (fast) {
+            const uint64_t q0 = (uint64_t)q * 64u;
+            const uint64_t clear = rx_ring_mask(q0, nb, (base + 1u) & mask, cur - base, len);
+            const uint64_t leaving = ehi >= lo ? rx_ring_mask(q0, nb, lo & mask, ehi - lo + 1u, len) : 0ull;
+            const uint64_t old = bits[q];
+            bits[q] = (old & ~clear) | s;
+            r += (uint32_t)__popcll(old & leaving);
+        }
+    }
+    if (!fast) return;  // (wave-uniform)
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    if (lane == 0) {
+        const uint64_t recv = atomicAdd(reinterpret_cast<unsigned long long*>(f.recv + w), 0ull);
+        const uint64_t exits = hi >= lo ? hi - lo + 1u : 0u;
+        win.lost[w] += (int64_t)(exits - recv - r);
+        win.cur[w] = cur;
+    }
+}
+
+// One open wave's verdicts (every lane calls it; `holder` lanes hold packet j's status st): the
+// verdict into status / verdict at the arrival index, the counter into the scratch bitmap when it
+// stays in the final window or into the received count when it leaves it — one atomic per (wave,
+// window, word), not one per packet (one tunnel's batch would serialise tens of thousands of
+// atomics on one address) — then the pending decrements, and the finish of every window this wave
+// completes.
+__device__ __noinline__ void rx_fold_settle(const RxFold& f, int32_t* status, uint32_t j, int32_t st, bool holder) {
+    const uint32_t lane = __lane_id();
+    uint32_t w = f.win.count;
+    uint64_t c = 0, cur = 0, lo = 1, hi = 0;
+    bool ok = false;
+    if (holder) {
+        const uint32_t i = f.sub_map[j];
+        w = f.keyw[i];
+        c = f.ctr[i];
+        f.verdict[i] = st;
+        status[i] = st;
+        ok = st == NEB_STATUS_OK;
+        if (!ok) {
+            atomicOr(&f.wflag[w], kRxSlow);
+            f.need_host[0] = 1u;  // (pinned host word)
+        }
+        cur = f.curnew[w];
+        lo = f.exit_lo[w];
+        hi = f.exit_hi[w];
+    }
+    const uint64_t len = f.win.length;
+    const bool in_final = ok && (cur < len || c > cur - len);
+    const bool leaves = ok && c >= lo && c <= hi;
+    const uint64_t p = c & (len - 1u);
+    const uint64_t wkey = in_final ? (((uint64_t)w << 32) | (p >> 6)) : ~0ull;
+    uint64_t pending = __ballot(in_final);
+    while (pending) {
+        const uint32_t leader = __builtin_ctzll(pending);
+        const uint64_t lk = __shfl(wkey, (int)leader);
+        const bool mine = in_final && wkey == lk;
+        uint64_t b = mine ? 1ull << (p & 63) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) b |= __shfl_xor(b, o);
+        if (lane == leader)
+            atomicOr(reinterpret_cast<unsigned long long*>(f.scratch + ((size_t)w << f.win.words_lg) + (p >> 6)), b);
+        pending &= ~__ballot(mine);
+    }
+    uint64_t pend2 = __ballot(leaves);
+    while (pend2) {
+        const uint32_t leader = __builtin_ctzll(pend2);
+        const uint32_t lw = __shfl(w, (int)leader);
+        const uint64_t same = __ballot(leaves && w == lw);
+        if (lane == leader) atomicAdd(reinterpret_cast<unsigned long long*>(f.recv + w), (unsigned long long)__popcll(same));
+        pend2 &= ~same;
+    }
+    // this wave's bitmap and count atomics are done before its pending decrements (CDNA's vmcnt
+    // counts stores and atomics too), so the wave that takes a window to zero sees all of them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint64_t todo = __ballot(holder);
+    while (todo) {
+        const uint32_t leader = __builtin_ctzll(todo);
+        const uint32_t lw = __shfl(w, (int)leader);
+        const uint64_t same = __ballot(holder && w == lw);
+        uint32_t last = 0;
+        if (lane == leader) {
+            const uint32_t k = (uint32_t)__popcll(same);
+            last = atomicSub(&f.pending[lw], k) == k;
+        }
+        if (__shfl(last, (int)leader)) rx_fold_finish(f, lw);
+        todo &= ~same;
+    }
 }
 
 }  // namespace neb
@@ -192,5 +363,3 @@ extern "C" hipError_t neb_rxdev_wire(const neb_rx_packet* d_pk, uint32_t n, cons
                                      int32_t* d_gate, hipStream_t s);
 // status[i] = gate[i] wherever the gate refused the packet
 extern "C" hipError_t neb_rxdev_wire_fix(const int32_t* d_gate, int32_t* d_status, uint32_t n, hipStream_t s);
-extern "C" hipError_t neb_rxdev_finish(uint32_t n, const neb::RxDevWin* win, const neb::RxDevWs* ws,
-                                       int32_t* d_status, hipStream_t s);

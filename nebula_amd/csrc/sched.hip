@@ -134,14 +134,11 @@ __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max
     }
 }
 
-// pass 3: scatter packet indices and descriptors into their bin's range, at the rank pass 1 drew
+// pass 3: scatter packet indices into their bin's range, at the rank pass 1 drew
 __global__ void sched_scatter_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn, SchedWs ws) {
     if (dn) n = min(n, *dn);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t j = ws.base[ws.binof[i]] + ws.binpos[i];
-        ws.sorted[j] = i;
-        if (ws.sdesc) ws.sdesc[j] = desc[i];
-    }
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        ws.sorted[ws.base[ws.binof[i]] + ws.binpos[i]] = i;
 }
 
 // Descriptors of a shard whose engine disagrees with engine 0 on some key slots (engine.cpp

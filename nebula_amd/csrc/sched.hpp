@@ -67,10 +67,7 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
     uint32_t* binof;      // [n] sub-bin (bin * kSubBins + sub) of each packet
     uint32_t* binpos;     // [n] rank of each packet within its bin (the histogram atomic's return)
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
-    neb_desc* sdesc;      // [n] their descriptors in the same order (sdesc[j] = desc[sorted[j]]), or null:
-                          // a group's descriptors one contiguous read instead of a gather behind the index
     uint4* chunks;        // [max_chunks + max_short] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
-    uint4* sums;          // [n] the open's GHASH values between the split passes (aes_gcm.hip gcm_ctr_kernel)
     uint32_t max_chunks;  // fronts from 0 up, long tails from max_chunks - 1 down
     uint32_t max_short;   // short tails from max_chunks up
 };

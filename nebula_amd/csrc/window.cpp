@@ -51,7 +51,7 @@ void neb_rx_pipe_end(neb_engine* e);
 int neb_engine_device_of(const neb_engine* e);
 int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint);
 int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s);
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx);
 }
 
 using namespace neb_rx;
@@ -369,7 +369,7 @@ struct neb_dwindows {
     size_t ws_bytes = 0;
     neb::RxDevWs ws{};
     uint32_t ws_n = 0;
-    uint32_t* h_host = nullptr;  // pinned, mapped: the finish sets it when a window needs the host
+    uint32_t* h_host = nullptr;  // pinned, mapped, 2 words (RxDevWs::need_host): a window needs the host; the scan failed
     uint8_t* wire_mem = nullptr;  // neb_rx_open_wire_batch: descriptors + gate statuses
     uint32_t wire_n = 0;
     uint32_t spin_limit = neb::kRxSpinLimit;  // neb_dwindows_set_spin_limit
@@ -442,7 +442,7 @@ NEB_API int neb_dwindows_create(neb_engine* e, uint32_t count, uint64_t length, 
         delete d;
         return NEB_ERR_HIP;
     }
-    if (hipHostMalloc((void**)&d->h_host, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc((void**)&d->h_host, 2 * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess) {
         d->h_host = nullptr;
         hipFree(d->mem);
         delete d;
@@ -539,6 +539,11 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
         d->ws_n = 0;
         RX_HIP(hipMalloc((void**)&d->ws_mem, bytes));
         neb::rx_ws_layout(n, v.count, v.words, d->ws_mem, &d->ws);
+        d->ws.need_host = d->h_host;
+        // the open kernels' epilogue reads the workspace through its device copy (rxwin.hpp RxFold)
+        const neb::RxFold fold = neb::rx_fold_of(v, d->ws);
+        RX_HIP(hipMemcpy(d->ws.fold, &fold, sizeof fold, hipMemcpyHostToDevice));
+        RX_HIP(hipStreamSynchronize(nullptr));
         // the scratch bitmap is zeroed once here and again by each batch as it is consumed
         RX_HIP(hipMemsetAsync(d->ws.scratch, 0, ((size_t)v.count << v.words_lg) * 8, s));
         RX_HIP(hipMemsetAsync(d->ws.mixed, 0, 4, s));  // no generation is 0
@@ -555,7 +560,7 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
         RX_HIP(hipMemsetAsync(d->ws.wrisky, 0, (size_t)v.count * 4, s));
         d->ws.gen = 1;
     }
-    *d->h_host = 0;
+    d->h_host[0] = d->h_host[1] = 0;
     d->ws.need_host = d->h_host;
     d->ws.spin_limit = d->spin_limit;
     const neb::RxDevWs& ws = d->ws;
@@ -570,21 +575,19 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
     // 1. group by window, prefix maxima, first occurrences; admission for the safe windows
     RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
     const auto t1 = now();
-    // 2. one open of every admitted packet (compacted by the plan)
-    rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, ws.sub_status, key_hint, s);
+    // 2. one open of every admitted packet (compacted by the plan); its epilogue settles each verdict
+    //    at the packet's arrival index and finishes every window whose packets all verified (RxFold)
+    rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, d_status, key_hint, s, ws.fold);
     if (rc != NEB_OK) return rc;
     const auto t2 = now();
-    // 3. the parallel finish of every window whose admitted packets all verified
-    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, s));
-    const auto t3 = now();
     RX_HIP(hipStreamSynchronize(s));
     if (prof)
-        std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, open %.1f, finish %.1f us, wait %.1f us\n", n, us(t0, t1),
-                     us(t1, t2), us(t2, t3), us(t3, now()));
-    // the finish flags, in pinned host memory, whether any window needs the sequential finish
+        std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, open %.1f us, wait %.1f us\n", n, us(t0, t1), us(t1, t2),
+                     us(t2, now()));
+    // the plan and the open flag, in pinned host memory, whether any window needs the sequential finish
     const uint32_t need = __atomic_load_n(d->h_host, __ATOMIC_ACQUIRE);
+    if (__atomic_load_n(d->h_host + 1, __ATOMIC_ACQUIRE)) return NEB_ERR_HIP;  // a scan lookback timed out
     if (need == 0) return NEB_OK;
-    if (need & 2u) return NEB_ERR_HIP;  // rx_scan_admit_kernel's lookback timed out (an internal error)
     std::vector<uint32_t> flag;
     if (d2h(flag, ws.wflag, v.count, s) != NEB_OK) return NEB_ERR_HIP;
     RX_HIP(hipStreamSynchronize(s));
@@ -648,7 +651,8 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
             RX_HIP(hipMemcpyAsync(ws.sub_map, pk.data(), (size_t)cnt * 4, hipMemcpyHostToDevice, s));
             RX_HIP(hipMemcpyAsync(ws.nsub, &cnt, 4, hipMemcpyHostToDevice, s));
             RX_HIP(neb_rxdev_gather(d_desc, cnt, &ws, s));
-            const int r = neb_open_batch_count(e, alg, ws.sub_desc, cnt, nullptr, d_arena, ws.sub_status, key_hint, s);
+            const int r =
+                neb_open_batch_count(e, alg, ws.sub_desc, cnt, nullptr, d_arena, ws.sub_status, key_hint, s, nullptr);
             if (r != NEB_OK) return r;
             std::vector<int32_t> st(cnt);
             RX_HIP(hipMemcpyAsync(st.data(), ws.sub_status, (size_t)cnt * 4, hipMemcpyDeviceToHost, s));
@@ -691,7 +695,7 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
             }
             std::vector<int32_t> st(cnt, NEB_STATUS_BAD_KEY);
             hipError_t err = hipMemcpyAsync(d_ds, ds.data(), (size_t)cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s);
-            r = err == hipSuccess ? neb_open_batch_count(e, alg, d_ds, cnt, nullptr, d_spec, d_st, key_hint, s)
+            r = err == hipSuccess ? neb_open_batch_count(e, alg, d_ds, cnt, nullptr, d_spec, d_st, key_hint, s, nullptr)
                                   : NEB_ERR_HIP;
             if (r == NEB_OK && (hipMemcpyAsync(st.data(), d_st, (size_t)cnt * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
                                 hipStreamSynchronize(s) != hipSuccess))
