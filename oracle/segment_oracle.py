@@ -1,7 +1,8 @@
 """segment_oracle.py — TEST INFRASTRUCTURE ONLY: a numpy/Python restatement of Nebula's TX
 superpacket path — TSO/USO segmentation with checksum completion, then the per-segment
 header.Encode + EncryptDanger into send-batch slots — used by tests/ and bench.py's cpu_baseline
-leg as the checker for the engine's fused segment+seal batch (nebula_amd/csrc/segment.*).
+leg as the checker for the engine's fused segment+seal batch (nebula_amd/csrc/tx.hip, the TX
+batch's plan, segment and seal kernels).
 The product never imports this module.
 
 Restated from slackhq/nebula (read as text, not copied):
