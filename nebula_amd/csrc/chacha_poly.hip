@@ -421,8 +421,10 @@ __global__ __launch_bounds__(kWave) void chacha_one_kernel(ChOneArgs a) {
     uint8_t* base = reinterpret_cast<uint8_t*>(kb);
     neb_desc d = a.d;
     d.dst_off = a.d.dst_off - (uint64_t)(uintptr_t)base;
-    const ChachaArgs ca{nullptr, 1u, base, a.keys, a.max_keys, a.key, a.status, nullptr, 0u, nullptr};
+    __shared__ int32_t s_status;
+    const ChachaArgs ca{nullptr, 1u, base, a.keys, a.max_keys, a.key, &s_status, nullptr, 0u, nullptr};
     chacha_group<OPEN>(ca, 0u, 1u, [&](uint32_t) { return d; });
+    one_publish_status(a.status, &s_status);
 }
 
 // Key install of a batch of keys, one workgroup per key: the record is cleared (it may have held

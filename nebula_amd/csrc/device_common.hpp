@@ -121,4 +121,17 @@ __device__ __forceinline__ uint4 load_block_hdr(const uint8_t* hp, const uint8_t
     return make_uint4(a.x | (b.x ^ bh.x), a.y | (b.y ^ bh.y), a.z | (b.z ^ bh.z), a.w | (b.w ^ bh.w));
 }
 
+// The per-packet kernels' last step (aes_gcm.hip gcm_one_kernel, chacha_poly.hip chacha_one_kernel):
+// every result store of the wave released at system scope (s_waitcnt + L2 write-back: the host
+// reads the result straight from its pinned slot), then the status, staged in LDS by the packet's
+// last lane, as one system-scope store. The host polls that word (engine.cpp one_packet).
+__device__ __forceinline__ void one_publish_status(int32_t* host_status, const int32_t* staged) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the staging lane's LDS store, wave-wide
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const int32_t st = *staged;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the result stores are visible first
+    if (__lane_id() == 0) __hip_atomic_store(host_status, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace neb
