@@ -934,13 +934,19 @@ __device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uin
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
 // own (optional): the packet's descriptor itself, not args.desc[p] (the per-packet kernel's, rebased).
-template <bool OPEN, bool CS = false, class GH, class TL>
+// RX: the device receive's open (args.rx; rxt the workgroup's RxWgTab), an instantiation of its own
+// so the plain opens keep their registers.
+template <bool OPEN, bool CS = false, bool RX = false, class GH, class TL>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
                                                  uint32_t lane, uint32_t lg, const uint4* cs_pow = nullptr,
-                                                 const neb_desc* own = nullptr) {
+                                                 const neb_desc* own = nullptr, RxWgTab* rxt = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
+    // the device receive opens only what its windows admitted (the rest keep the plan's status)
+    if constexpr (RX) {
+        if (valid) valid = args.rx->adm[p] != 0u;
+    }
     neb_desc d = {};
     if (valid) d = own ? *own : args.desc[p];
     uint32_t st = NEB_STATUS_OK;
@@ -1066,8 +1072,8 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         if (run && cs_on && l == LPP - 1u) V = xor4(V, gcm_csum_fix(d, sh.n, sh.na, cs_acc, cs_fk, args.arena, cs_pow));
     }
     if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
-    if (OPEN && args.rx)  // (every lane: the settle aggregates over the wave)
-        rx_fold_settle(*args.rx, args.status, p, (int32_t)st, valid && l == LPP - 1u);
+    if constexpr (RX)  // (every lane: the settle aggregates over the wave)
+        rx_fold_settle(*args.rx, *rxt, args.status, p, (int32_t)st, valid && l == LPP - 1u);
     else if (valid && l == LPP - 1u)
         args.status[p] = (int32_t)st;
 }
@@ -1112,8 +1118,8 @@ struct SingleLdsCs : SingleLds {
     uint4 pow2[10 * 16];  // 2.5 KiB  Shoup tables of H^(2^j), j < 10 (the TX checksum correction)
 };
 
-// CS: the TX seal with the L4 checksums (gcm_csum_fix)
-template <bool OPEN, bool CS = false>
+// CS: the TX seal with the L4 checksums (gcm_csum_fix); RX: the device receive's open (GcmArgs::rx)
+template <bool OPEN, bool CS = false, bool RX = false>
 __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(GcmArgs args) {
     __shared__ std::conditional_t<CS, SingleLdsCs, SingleLds> lds;
     const uint32_t tid = threadIdx.x;
@@ -1141,6 +1147,8 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
         if (tid < 160u) lds.pow2[tid] = ld_rec4(srec, rec_shoup_pow2(tid >> 4) + 4u * (tid & 15u));
         cs_pow = lds.pow2;
     }
+    __shared__ RxWgTab rxt;
+    if constexpr (RX) rx_wg_init(rxt, tid, kSingleThreads);
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
@@ -1171,12 +1179,14 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
         const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
 #endif
         const uint32_t p = grp * kPpw + lane / kLpp;
-        gcm_packet_group<OPEN, CS>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, cs_pow);
+        gcm_packet_group<OPEN, CS, RX>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, cs_pow, nullptr,
+                                       &rxt);
 #ifdef NEB_WAVE_TRACE
         wave_trace(lane, trace_k++, blockIdx.x << 20 | wave << 16 | 16u << 8 | 2u << 4 | 1u, grp, tc0,
                    __builtin_amdgcn_s_memrealtime());
 #endif
     }
+    if constexpr (RX) rx_wg_flush(*args.rx, rxt, tid, kSingleThreads);
 }
 
 // The tail pass: the packets after gcm_single_kernel's full passes over args.tail_slots waves (the
@@ -1203,7 +1213,7 @@ struct TailLds {
     uint4 hi[3 * 16];           // M_16, M_32, M_48 (GhShoup64)
 };
 static_assert(kTailLg == 6, "GhShoup64: 64 lanes per packet");
-template <bool OPEN>
+template <bool OPEN, bool RX = false>
 __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(GcmArgs args) {
     __shared__ TailLds lds;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -1226,6 +1236,8 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     if (tid < 128u) lds.pos[tid] = ld_rec4(srec, kRecPos64 + 4u * tid);
     if (tid < 256u) lds.m16[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
     if (tid < 48u) lds.hi[tid] = ld_rec4(srec, (tid < 16u ? kRecShoup + 15u * 64u : tid < 32u ? kRecShoup32 : kRecShoup48) + 4u * (tid & 15u));
+    __shared__ RxWgTab rxt;
+    if constexpr (RX) rx_wg_init(rxt, tid, kTailWaves * kWave);
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
@@ -1234,8 +1246,10 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
     for (uint32_t t = blockIdx.x * kTailWaves + wave; t < tgroups; t += gridDim.x * kTailWaves) {
         const uint32_t p = p0 + kTailPpw * t + (lane >> kTailLg);
-        gcm_packet_group<OPEN>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, kTailLg);
+        gcm_packet_group<OPEN, false, RX>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, kTailLg,
+                                          nullptr, nullptr, &rxt);
     }
+    if constexpr (RX) rx_wg_flush(*args.rx, rxt, tid, kTailWaves * kWave);
 }
 
 // ---- one packet, its bytes in the kernel arguments (the per-packet CipherState calls) ---------
@@ -1388,7 +1402,7 @@ struct ChunkArgs {
 // dynamic inside the workgroup and no wave touches a global atomic (a global work cursor: returning
 // atomics on one word serialise across the chip; C3 step -8%, IMIX -27% against it, A/B,
 // profiles/r2_micro/ab_chunk_order.log).
-template <bool OPEN>
+template <bool OPEN, bool RX = false>
 __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(GcmArgs args, ChunkArgs ca) {
     __shared__ ChunkLds lds;
     __shared__ uint32_t wg_cursor;
@@ -1407,6 +1421,8 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
 #endif
     fill_ttab<256u * 32u, kChunkThreads>(lds.ttab, tid, ttab_entry);
     if (tid == 0) wg_cursor = kChunkWaves;
+    __shared__ RxWgTab rxt;
+    if constexpr (RX) rx_wg_init(rxt, tid, kChunkThreads);
     __syncthreads();
 #ifdef NEB_WAVE_TRACE
     uint32_t trace_k = 1;
@@ -1461,7 +1477,8 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                 const uint32_t q = g0 + (ln >> 2);
                 const bool valid = q < count;
                 const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-                gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
+                gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u, nullptr, nullptr,
+                                                  &rxt);
             }
         } else {
             const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
@@ -1473,7 +1490,8 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             const bool valid = q < count;
             const uint32_t p = valid ? ca.sorted[start + q] : 0u;
             const GhChunkTree gh{wtab, wpos};
-            gcm_packet_group<OPEN>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg);
+            gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg, nullptr, nullptr,
+                                              &rxt);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
@@ -1486,6 +1504,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
 #endif
         c = cn;
     }
+    if constexpr (RX) rx_wg_flush(*args.rx, rxt, tid, kChunkThreads);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1792,7 +1811,9 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
         const uint32_t tgrid = std::min<uint32_t>(
             ((n + neb::kTailPpw - 1u) / neb::kTailPpw + neb::kTailWaves - 1u) / neb::kTailWaves,
             2u * (uint32_t)std::max(cu_count, 1));
-        if (open)
+        if (open && rx)
+            launch_k(neb::gcm_single_tail_kernel<true, true>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), s, stop, a);
+        else if (open)
             launch_k(neb::gcm_single_tail_kernel<true>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), s, stop, a);
         else
             launch_k(neb::gcm_single_tail_kernel<false>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), s, stop, a);
@@ -1806,7 +1827,9 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
     const dim3 grid(slots / neb::kSingleWaves);
     if (grid.x == 0) return hipSuccess;
     hipEvent_t main_stop = tail ? nullptr : stop;  // the stop event goes to the batch's last kernel
-    if (open)
+    if (open && rx)
+        launch_k(neb::gcm_single_kernel<true, false, true>, grid, dim3(neb::kSingleThreads), s, main_stop, a);
+    else if (open)
         launch_k(neb::gcm_single_kernel<true>, grid, dim3(neb::kSingleThreads), s, main_stop, a);
     else if (cs)
         launch_k(neb::gcm_single_kernel<false, true>, grid, dim3(neb::kSingleThreads), s, main_stop, a);
@@ -1823,7 +1846,9 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
     const uint32_t tgrid = std::min<uint32_t>(
         ((tail_pkts + neb::kTailPpw - 1u) / neb::kTailPpw + neb::kTailWaves - 1u) / neb::kTailWaves,
         2u * (uint32_t)std::max(cu_count, 1));
-    if (open)
+    if (open && rx)
+        launch_k(neb::gcm_single_tail_kernel<true, true>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), s, stop, a);
+    else if (open)
         launch_k(neb::gcm_single_tail_kernel<true>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), s, stop, a);
     else
         launch_k(neb::gcm_single_tail_kernel<false>, dim3(tgrid), dim3(neb::kTailWaves * neb::kWave), s, stop, a);
@@ -1890,6 +1915,8 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.
     const uint32_t bound = max_chunks * (uint32_t)neb::kChunkWaves;
     // stop (optional): an event bound to the kernel's dispatch (no marker packet after it)
+    if (open && rx)
+        return launch_grid_stop(neb::gcm_chunk_kernel<true, true>, neb::kChunkThreads, bound, cu_count, s, stop, a, ca);
     return open ? launch_grid_stop(neb::gcm_chunk_kernel<true>, neb::kChunkThreads, bound, cu_count, s, stop, a, ca)
                 : launch_grid_stop(neb::gcm_chunk_kernel<false>, neb::kChunkThreads, bound, cu_count, s, stop, a, ca);
 }

@@ -241,10 +241,11 @@ struct ChachaArgs {
 };
 
 // packet p's status, by its 16th lane; with a receive epilogue every lane takes part (RxFold)
-template <bool OPEN>
-__device__ __forceinline__ void chacha_status(const ChachaArgs& args, uint32_t p, uint32_t st, bool holder) {
-    if (OPEN && args.rx)
-        rx_fold_settle(*args.rx, args.status, p, (int32_t)st, holder);
+template <bool OPEN, bool RX>
+__device__ __forceinline__ void chacha_status(const ChachaArgs& args, RxWgTab* rxt, uint32_t p, uint32_t st,
+                                              bool holder) {
+    if constexpr (RX)
+        rx_fold_settle(*args.rx, *rxt, args.status, p, (int32_t)st, holder);
     else if (holder)
         args.status[p] = (int32_t)st;
 }
@@ -254,8 +255,9 @@ __device__ __forceinline__ void chacha_status(const ChachaArgs& args, uint32_t p
 // profiles/r2_s3/ab_chacha_prefetch): the kernel is bound by VALU issue, not by load latency.
 // One wave's group of 4 packets (16 lanes each): packets 4·grp .. 4·grp + 3 of the batch, the
 // descriptor of packet p from desc_of(p).
-template <bool OPEN, class DF>
-__device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t grp, uint32_t npkt, DF&& desc_of) {
+template <bool OPEN, bool RX = false, class DF>
+__device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t grp, uint32_t npkt, DF&& desc_of,
+                                             RxWgTab* rxt = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & 15u;
     const uint32_t w = l & 3u;      // column within the quad
@@ -265,7 +267,8 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
     constexpr uint32_t kConst[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
     {
         const uint32_t p = grp * 4u + q;
-        const bool valid = p < npkt;
+        // the device receive opens only what its windows admitted (the rest keep the plan's status)
+        const bool valid = p < npkt && !(RX && !args.rx->adm[p]);
         neb_desc d = {};
         if (valid) d = desc_of(p);
         uint32_t st = NEB_STATUS_OK;
@@ -288,7 +291,7 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 16));
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 32));
         if (rmax == 0u) {  // (wave-uniform)
-            chacha_status<OPEN>(args, p, st, valid && l == 15u);
+            chacha_status<OPEN, RX>(args, rxt, p, st, valid && l == 15u);
             return;
         }
 
@@ -385,18 +388,24 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
                 }
             }
         }
-        chacha_status<OPEN>(args, p, st, valid && l == 15u);
+        chacha_status<OPEN, RX>(args, rxt, p, st, valid && l == 15u);
     }
 }
 
-template <bool OPEN>
+template <bool OPEN, bool RX = false>
 __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs args) {
     const uint32_t wave = threadIdx.x >> 6;
     uint32_t npkt = args.npkt;
     if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
     const uint32_t ngroups = (npkt + 3u) >> 2;
+    __shared__ RxWgTab rxt;
+    if constexpr (RX) {
+        rx_wg_init(rxt, threadIdx.x, kChThreads);
+        __syncthreads();
+    }
     for (uint32_t grp = blockIdx.x * kChWavesPerWG + wave; grp < ngroups; grp += gridDim.x * kChWavesPerWG)
-        chacha_group<OPEN>(args, grp, npkt, [&](uint32_t p) { return args.desc[p]; });
+        chacha_group<OPEN, RX>(args, grp, npkt, [&](uint32_t p) { return args.desc[p]; }, &rxt);
+    if constexpr (RX) rx_wg_flush(*args.rx, rxt, threadIdx.x, kChThreads);
 }
 
 // One packet, its bytes in the kernel arguments (the per-packet path; aes_gcm.hip gcm_one_kernel
@@ -453,9 +462,9 @@ extern "C" hipError_t neb_chacha_key_setup(const uint8_t* keys, const uint32_t* 
     return hipGetLastError();
 }
 
-template <bool OPEN>
+template <bool OPEN, bool RX = false>
 static hipError_t launch_chacha(const neb::ChachaArgs& a, int cu_count, hipStream_t s, hipEvent_t stop) {
-    auto kern = neb::chacha_batch_kernel<OPEN>;
+    auto kern = neb::chacha_batch_kernel<OPEN, RX>;
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, neb::kChThreads, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
@@ -501,5 +510,6 @@ extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
                                        int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx) {
     neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, rx};
+    if (open && rx) return launch_chacha<true, true>(a, cu_count, s, stop);
     return open ? launch_chacha<true>(a, cu_count, s, stop) : launch_chacha<false>(a, cu_count, s, stop);
 }

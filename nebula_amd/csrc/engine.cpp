@@ -839,10 +839,11 @@ static bool bind_events() {
 // rx (optional, opens only): the device receive's settle and window finish run in the open kernel's
 // epilogue (rxwin.hpp RxFold); d_desc is then the admitted packets compacted and d_status the
 // caller's statuses by arrival index.
+// prebinned: the mixed-key binning of this batch is already in `sched` (neb_prebin, ordered before s).
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr,
                                SchedSpace* sched = nullptr, int hdr_from_dst = 0, hipEvent_t stop = nullptr,
-                               const neb::RxFold* rx = nullptr) {
+                               const neb::RxFold* rx = nullptr, bool prebinned = false) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
             return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
@@ -850,10 +851,13 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         // mixed keys: regroup into single-key, similar-size chunks on the device, then seal/open
         SchedSpace& sp = sched ? *sched : e->sched;
         std::lock_guard<std::mutex> g(sp.mu);
-        hipError_t err = sched_reserve(e, sp, n, s);
-        if (err == hipSuccess && !sp.last.same(s)) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
-        neb::SchedWs ws = sp.ws;
-        if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &ws, s);
+        hipError_t err = hipSuccess;
+        if (!prebinned) {
+            err = sched_reserve(e, sp, n, s);
+            if (err == hipSuccess && !sp.last.same(s)) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
+            neb::SchedWs ws = sp.ws;
+            if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &ws, s);
+        }
         if (err == hipSuccess)  // sp.done bound to the chunk kernel's dispatch: no marker packet between batches
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                         sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, e->cu_count,
@@ -1068,9 +1072,11 @@ int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint) { return che
 
 // Open the first *d_n (a count in device memory) of at most n descriptors, on stream s.
 int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx) {
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx,
+                         void* prebinned) {
     if (n == 0) return NEB_OK;
-    hipError_t err = launch_batch(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, s, d_n, nullptr, 0, nullptr, rx);
+    hipError_t err = launch_batch(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, s, d_n,
+                                  static_cast<SchedSpace*>(prebinned), 0, nullptr, rx, prebinned != nullptr);
     if (err != hipSuccess) {
         set_error("batch launch", err);
         return NEB_ERR_HIP;
@@ -1081,6 +1087,29 @@ int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_
 // For the submission queue (queue.cpp): a scheduler workspace of its own, and a launch of one
 // staged batch (zero-copy on pinned memory) on the queue's stream.
 void* neb_sched_space_new() { return new (std::nothrow) SchedSpace; }
+
+// The device receive (window.cpp): the mixed-key AES-GCM binning of its batch on `aux`, after `fork`
+// (recorded on the receive's stream once the descriptors are there), into the receive's own
+// scheduler workspace, beside the window plan on the receive's stream; `join` marks its end. The
+// open then runs with it (neb_open_batch_count's `prebinned`) after the stream waits on `join`.
+int neb_prebin(neb_engine* e, const neb_desc* d_desc, uint32_t n, void* sched, hipStream_t aux, hipEvent_t fork,
+               hipEvent_t join) {
+    SchedSpace& sp = *static_cast<SchedSpace*>(sched);
+    std::lock_guard<std::mutex> g(sp.mu);
+    hipError_t err = hipStreamWaitEvent(aux, fork, 0);
+    if (err == hipSuccess) err = sched_reserve(e, sp, n, aux);
+    if (err == hipSuccess && !sp.last.same(aux)) err = hipStreamWaitEvent(aux, sp.done, 0);  // the last open's reads
+    neb::SchedWs ws = sp.ws;
+    if (err == hipSuccess) err = neb_sched_build(d_desc, n, nullptr, e->max_keys, 4u, &ws, aux);
+    if (err == hipSuccess) err = hipEventRecord(join, aux);
+    if (err != hipSuccess) {
+        (void)hipStreamSynchronize(aux);
+        sp.dirty = true;
+        set_error("prebin", err);
+        return NEB_ERR_HIP;
+    }
+    return NEB_OK;
+}
 void neb_sched_space_free(void* p) {
     auto* sp = static_cast<SchedSpace*>(p);
     if (!sp) return;

@@ -138,7 +138,6 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
         }
     }
     if (b == 0 && t == 0) {
-        *ws.nsub = 0;
         *ws.ticket = 0;
         *ws.err = 0;
     }
@@ -333,13 +332,15 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
     __shared__ uint32_t s_f[kRxThreads / 64];
     __shared__ uint64_t s_incl[kRxBlock];
     __shared__ uint64_t s_pre;
-    __shared__ uint32_t s_fh, s_b, s_base;
-    __shared__ uint32_t s_cnt[kRxThreads / 64];
+    __shared__ uint32_t s_fh, s_b;
+    __shared__ uint32_t s_pw[kRxThreads], s_pn[kRxThreads];  // admitted packets per window (pending)
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     if (t == 0) {
         s_b = atomicAdd(ws.ticket, 1u);
         s_fh = kRxBlock;
     }
+    s_pw[t] = ~0u;
+    s_pn[t] = 0;
     __syncthreads();
     const uint32_t b = s_b, b0 = b * kRxBlock, k0 = b0 + t * kRxItems;
     const uint32_t gen = ws.gen;
@@ -511,8 +512,9 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
             status[i] = NEB_STATUS_REPLAY;  // (a slow window's statuses are rewritten on the host)
         }
     }
-    // each window's admitted packets, pending until the open settles their verdicts (RxFold): one
-    // atomic per (wave, window)
+    // each window's admitted packets, pending until the open settles their verdicts (RxFold): counted
+    // per window in LDS, then one atomic per (workgroup, window) (one tunnel's batch would otherwise
+    // put a thousand per-wave atomics on one word)
     {
         const uint32_t aw = okm ? wj[0] : win.count;  // (kRxItems == 1)
         uint64_t todo = __ballot(okm != 0u);
@@ -520,34 +522,19 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
             const uint32_t leader = __builtin_ctzll(todo);
             const uint32_t lw = __shfl(aw, (int)leader);
             const uint64_t same = __ballot(okm != 0u && aw == lw);
-            if (lane == leader) atomicAdd(&ws.pending[lw], (uint32_t)__popcll(same));
+            if (lane == leader)
+                for (uint32_t h = lw % kRxThreads;; h = (h + 1u) % kRxThreads) {
+                    const uint32_t o = atomicCAS(&s_pw[h], ~0u, lw);  // (at most kRxThreads windows)
+                    if (o == ~0u || o == lw) {
+                        atomicAdd(&s_pn[h], (uint32_t)__popcll(same));
+                        break;
+                    }
+                }
             todo &= ~same;
         }
+        __syncthreads();
+        if (s_pw[t] != ~0u) atomicAdd(&ws.pending[s_pw[t]], s_pn[t]);
     }
-    // workgroup prefix of the admitted counts
-    const uint32_t take = (uint32_t)__popc(okm);
-    uint32_t xx = take;
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(xx, o);
-        if (lane >= o) xx += y;
-    }
-    if (lane == 63u) s_cnt[wv] = xx;
-    __syncthreads();
-    if (t == 0) {
-        uint32_t tot = 0;
-        for (uint32_t q = 0; q < kRxThreads / 64; q++) tot += s_cnt[q];
-        s_base = tot ? atomicAdd(ws.nsub, tot) : 0u;
-    }
-    __syncthreads();
-    uint32_t j0 = s_base + xx - take;
-    for (uint32_t q = 0; q < wv; q++) j0 += s_cnt[q];
-#pragma unroll
-    for (uint32_t j = 0; j < kRxItems; j++)
-        if (okm >> j & 1u) {
-            ws.sub_map[j0] = ij[j];
-            ws.sub_desc[j0++] = desc[ij[j]];
-        }
 }
 
 __global__ void rx_gather_desc_kernel(const neb_desc* __restrict__ desc, RxDevWs ws) {

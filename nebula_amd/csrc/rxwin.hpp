@@ -18,6 +18,7 @@ enum : uint32_t { kRxTouched = 1u, kRxRisky = 2u, kRxSlow = 4u };
 // run-order elements per workgroup of the scan and admission kernels (one per thread: their
 // per-packet chains of dependent loads and atomics are latency-bound)
 constexpr uint32_t kRxThreads = 256, kRxItems = 1, kRxBlock = kRxThreads * kRxItems;
+static_assert(kRxItems == 1, "rx_scan_admit_kernel's per-window pending counts take one packet per thread");
 // the stable sort by window (rxwin.hip): at most kRxSortBlocks workgroups of 256 x items packets,
 // digits of at most 8 bits for one pass, else passes of at most kRxSortDigit bits
 constexpr uint32_t kRxSortBlocks = 64, kRxSortDigit = 7, kRxSortMaxPasses = 5, kRxSortLoad = 4;
@@ -88,18 +89,21 @@ struct RxDevWs {
     uint32_t* mixed;
 };
 
-// The receive's settle and window finish, folded into the open kernels' epilogue (aes_gcm.hip
-// gcm_packet_group, chacha_poly.hip chacha_group: GcmArgs::rx / ChachaArgs::rx). The open runs over
-// the admitted packets compacted by rx_scan_admit_kernel (sub_desc, position j); as a packet's
-// verdict is known, rx_fold_settle writes it at its arrival index, ORs its counter into the window's
-// scratch bitmap (or counts it as received when it leaves the window), and takes it off its
-// window's pending count. The wave whose decrement brings a window to zero has the window's last
-// verdict, so it finishes the window (rx_fold_finish) right there: the bitmap, lost count and
-// current of a window whose packets all verified, or only the scratch cleared for one that goes to
-// the host. No settle or finish launch after the open (round 5: 6 → 4 window launches).
+// The receive's settle and window finish, folded into the open kernels (aes_gcm.hip
+// gcm_packet_group, chacha_poly.hip chacha_group: GcmArgs::rx / ChachaArgs::rx). The open runs
+// over the whole batch in arrival order and skips the packets rx_scan_admit_kernel did not admit
+// (adm[i] == 0: their statuses are already written, their bytes are never touched), so there is
+// no compaction and the mixed-key binning can run beside the plan on a second stream (window.cpp).
+// As a packet's verdict is known, rx_fold_settle writes it, ORs its counter into the window's
+// scratch bitmap (or counts it as received when it leaves the window) and counts it against its
+// window in the workgroup's LDS table (RxWgTab); at the end of the workgroup, rx_wg_flush takes
+// those counts off the windows' pending counts, and the wave whose decrement brings a window to
+// zero holds its last verdict, so it finishes the window right there (rx_fold_finish): the bitmap,
+// lost count and current of a window whose packets all verified, or only the scratch cleared for
+// one that goes to the host. No settle or finish launch (round 5: 6 → 4 window launches).
 struct RxFold {
     RxDevWin win;
-    const uint32_t* sub_map;  // position j of the open -> arrival index
+    const uint8_t* adm;  // per arrival: admitted by the plan (the open runs only these)
     int32_t* verdict;
     const uint32_t* keyw;
     const uint64_t* ctr;
@@ -112,6 +116,16 @@ struct RxFold {
     uint32_t* pending;
     const uint32_t* err;
     uint32_t* need_host;
+};
+
+// Per workgroup of an open kernel: its settled packets counted per window, flushed at its end (one
+// pending decrement per workgroup and window: a per-wave returning atomic after a drain of the
+// wave's stores cost the C2 receive 466 → 416 GiB/s, one tunnel's 4096 waves on one word). A full
+// table takes the per-wave path.
+constexpr uint32_t kRxWgSlots = 64;
+struct RxWgTab {
+    uint32_t w[kRxWgSlots];
+    uint32_t n[kRxWgSlots];
 };
 
 inline size_t rx_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -164,7 +178,7 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
 }
 
 inline RxFold rx_fold_of(const RxDevWin& win, const RxDevWs& ws) {
-    return RxFold{win,        ws.sub_map, ws.verdict, ws.keyw,    ws.ctr,     ws.wflag, ws.curnew,
+    return RxFold{win,        ws.adm,     ws.verdict, ws.keyw,    ws.ctr,     ws.wflag, ws.curnew,
                   ws.exit_lo, ws.exit_hi, ws.recv,    ws.scratch, ws.pending, ws.err,   ws.need_host};
 }
 
@@ -235,19 +249,33 @@ __device__ __forceinline__ void rx_fold_finish(const RxFold& f, uint32_t w) {
     }
 }
 
-// One open wave's verdicts (every lane calls it; `holder` lanes hold packet j's status st): the
-// verdict into status / verdict at the arrival index, the counter into the scratch bitmap when it
-// stays in the final window or into the received count when it leaves it — one atomic per (wave,
-// window, word), not one per packet (one tunnel's batch would serialise tens of thousands of
-// atomics on one address) — then the pending decrements, and the finish of every window this wave
-// completes.
-__device__ __noinline__ void rx_fold_settle(const RxFold& f, int32_t* status, uint32_t j, int32_t st, bool holder) {
+// Take k settled packets off window w's pending count; the wave that reaches zero finishes w (every
+// lane calls it with the same w and k; its own stores and atomics are complete).
+__device__ __forceinline__ void rx_fold_release(const RxFold& f, uint32_t w, uint32_t k) {
+    uint32_t last = 0;
+    if (__lane_id() == 0) last = atomicSub(&f.pending[w], k) == k;
+    if (__shfl(last, 0)) rx_fold_finish(f, w);
+}
+
+__device__ __forceinline__ void rx_wg_init(RxWgTab& t, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t i = tid; i < kRxWgSlots; i += nthreads) {
+        t.w[i] = ~0u;
+        t.n[i] = 0;
+    }
+}
+
+// One open wave's verdicts (every lane calls it; `holder` lanes hold the status st of packet i):
+// the verdict at i, the counter into the scratch bitmap when it stays in the final window or into
+// the received count when it leaves it — one atomic per (wave, window, word), not one per packet
+// (one tunnel's batch would serialise tens of thousands of atomics on one address) — and the count
+// per window into the workgroup's table.
+__device__ __noinline__ void rx_fold_settle(const RxFold& f, RxWgTab& t, int32_t* status, uint32_t i, int32_t st,
+                                            bool holder) {
     const uint32_t lane = __lane_id();
     uint32_t w = f.win.count;
     uint64_t c = 0, cur = 0, lo = 1, hi = 0;
     bool ok = false;
     if (holder) {
-        const uint32_t i = f.sub_map[j];
         w = f.keyw[i];
         c = f.ctr[i];
         f.verdict[i] = st;
@@ -286,21 +314,42 @@ __device__ __noinline__ void rx_fold_settle(const RxFold& f, int32_t* status, ui
         if (lane == leader) atomicAdd(reinterpret_cast<unsigned long long*>(f.recv + w), (unsigned long long)__popcll(same));
         pend2 &= ~same;
     }
-    // this wave's bitmap and count atomics are done before its pending decrements (CDNA's vmcnt
-    // counts stores and atomics too), so the wave that takes a window to zero sees all of them
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint64_t todo = __ballot(holder);
     while (todo) {
         const uint32_t leader = __builtin_ctzll(todo);
         const uint32_t lw = __shfl(w, (int)leader);
         const uint64_t same = __ballot(holder && w == lw);
-        uint32_t last = 0;
-        if (lane == leader) {
-            const uint32_t k = (uint32_t)__popcll(same);
-            last = atomicSub(&f.pending[lw], k) == k;
+        const uint32_t k = (uint32_t)__popcll(same);
+        uint32_t full = 0;
+        if (lane == leader) {  // the window's slot in the table (open addressing), or none left
+            full = 1;
+            for (uint32_t q = 0, h = lw % kRxWgSlots; q < kRxWgSlots; q++, h = (h + 1u) % kRxWgSlots) {
+                const uint32_t o = atomicCAS(&t.w[h], ~0u, lw);
+                if (o == ~0u || o == lw) {
+                    atomicAdd(&t.n[h], k);
+                    full = 0;
+                    break;
+                }
+            }
         }
-        if (__shfl(last, (int)leader)) rx_fold_finish(f, lw);
+        if (__shfl(full, (int)leader)) {  // no room: this wave releases its packets itself
+            // its bitmap and count atomics complete first (CDNA's vmcnt counts stores and atomics)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            rx_fold_release(f, lw, k);
+        }
         todo &= ~same;
+    }
+}
+
+// The end of an open workgroup (every thread, after its last packet): once every wave's stores and
+// atomics are complete, each counted window's packets come off its pending count, wave by wave.
+__device__ __forceinline__ void rx_wg_flush(const RxFold& f, RxWgTab& t, uint32_t tid, uint32_t nthreads) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint32_t wave = tid >> 6, nwaves = nthreads >> 6;
+    for (uint32_t h = wave; h < kRxWgSlots; h += nwaves) {
+        const uint32_t w = t.w[h];
+        if (w != ~0u) rx_fold_release(f, w, t.n[h]);
     }
 }
 

@@ -51,7 +51,12 @@ void neb_rx_pipe_end(neb_engine* e);
 int neb_engine_device_of(const neb_engine* e);
 int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint);
 int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx);
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx,
+                         void* prebinned);
+void* neb_sched_space_new();
+void neb_sched_space_free(void* p);
+int neb_prebin(neb_engine* e, const neb_desc* d_desc, uint32_t n, void* sched, hipStream_t aux, hipEvent_t fork,
+               hipEvent_t join);
 }
 
 using namespace neb_rx;
@@ -373,6 +378,10 @@ struct neb_dwindows {
     uint8_t* wire_mem = nullptr;  // neb_rx_open_wire_batch: descriptors + gate statuses
     uint32_t wire_n = 0;
     uint32_t spin_limit = neb::kRxSpinLimit;  // neb_dwindows_set_spin_limit
+    // mixed-key AES-GCM receives: the open's binning on a stream of its own, beside the plan
+    hipStream_t aux = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    void* sched = nullptr;
 };
 
 namespace {
@@ -471,6 +480,11 @@ NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
         // neb_rx_open_batch returns only once its stream has run the batch, and holds d->mu
         // throughout: with the lock taken, nothing of this window set is in flight
         std::lock_guard<std::mutex> g(d->mu);
+        if (d->aux) hipStreamSynchronize(d->aux);
+        if (d->sched) neb_sched_space_free(d->sched);
+        if (d->fork) hipEventDestroy(d->fork);
+        if (d->join) hipEventDestroy(d->join);
+        if (d->aux) hipStreamDestroy(d->aux);
         if (d->ws_mem) hipFree(d->ws_mem);
         if (d->wire_mem) hipFree(d->wire_mem);
         if (d->mem) hipFree(d->mem);
@@ -572,12 +586,27 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
     // Everything is queued at once, one host read at the end: windows whose counters come within
     // 2^62 of wrapping hold all their packets back (admitted by none), and exact_rounds opens what
     // their real pass accepts in batches, like the windows where a tag failed.
+    // 0. mixed-key AES-GCM: the open's binning (sched.hip) reads only the descriptors, so it runs on a
+    //    stream of its own beside the plan (17 µs of three launches off the C3 receive's chain)
+    void* prebinned = nullptr;
+    if (alg == NEB_ALG_AESGCM && key_hint == NEB_KEYS_MIXED) {
+        if (!d->aux) {
+            RX_HIP(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
+            RX_HIP(hipEventCreateWithFlags(&d->fork, hipEventDisableTiming | hipEventDisableSystemFence));
+            RX_HIP(hipEventCreateWithFlags(&d->join, hipEventDisableTiming | hipEventDisableSystemFence));
+            if (!(d->sched = neb_sched_space_new())) return NEB_ERR_HIP;
+        }
+        RX_HIP(hipEventRecord(d->fork, s));
+        if ((rc = neb_prebin(e, d_desc, n, d->sched, d->aux, d->fork, d->join)) != NEB_OK) return rc;
+        prebinned = d->sched;
+    }
     // 1. group by window, prefix maxima, first occurrences; admission for the safe windows
     RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
     const auto t1 = now();
-    // 2. one open of every admitted packet (compacted by the plan); its epilogue settles each verdict
-    //    at the packet's arrival index and finishes every window whose packets all verified (RxFold)
-    rc = neb_open_batch_count(e, alg, ws.sub_desc, n, ws.nsub, d_arena, d_status, key_hint, s, ws.fold);
+    // 2. one open over the batch that runs the admitted packets only; its epilogue settles each
+    //    verdict and finishes every window whose packets all verified (rxwin.hpp RxFold)
+    if (prebinned) RX_HIP(hipStreamWaitEvent(s, d->join, 0));
+    rc = neb_open_batch_count(e, alg, d_desc, n, nullptr, d_arena, d_status, key_hint, s, ws.fold, prebinned);
     if (rc != NEB_OK) return rc;
     const auto t2 = now();
     RX_HIP(hipStreamSynchronize(s));
@@ -652,7 +681,7 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
             RX_HIP(hipMemcpyAsync(ws.nsub, &cnt, 4, hipMemcpyHostToDevice, s));
             RX_HIP(neb_rxdev_gather(d_desc, cnt, &ws, s));
             const int r =
-                neb_open_batch_count(e, alg, ws.sub_desc, cnt, nullptr, d_arena, ws.sub_status, key_hint, s, nullptr);
+                neb_open_batch_count(e, alg, ws.sub_desc, cnt, nullptr, d_arena, ws.sub_status, key_hint, s, nullptr, nullptr);
             if (r != NEB_OK) return r;
             std::vector<int32_t> st(cnt);
             RX_HIP(hipMemcpyAsync(st.data(), ws.sub_status, (size_t)cnt * 4, hipMemcpyDeviceToHost, s));
@@ -695,7 +724,7 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
             }
             std::vector<int32_t> st(cnt, NEB_STATUS_BAD_KEY);
             hipError_t err = hipMemcpyAsync(d_ds, ds.data(), (size_t)cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s);
-            r = err == hipSuccess ? neb_open_batch_count(e, alg, d_ds, cnt, nullptr, d_spec, d_st, key_hint, s, nullptr)
+            r = err == hipSuccess ? neb_open_batch_count(e, alg, d_ds, cnt, nullptr, d_spec, d_st, key_hint, s, nullptr, nullptr)
                                   : NEB_ERR_HIP;
             if (r == NEB_OK && (hipMemcpyAsync(st.data(), d_st, (size_t)cnt * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
                                 hipStreamSynchronize(s) != hipSuccess))

@@ -8,7 +8,7 @@ for c in 1 2 3; do
   cat gpurun_out/r5_rx/rxd_c$c.json
 done
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_rx/trace_c3 -o run -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rx/trace_c3 -o run -- \
     python bench.py --mode rx-device --config 2 --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/r5_rx/trace.log 2>&1 || exit $?
 find gpurun_out/r5_rx/trace_c3 -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/r5_rx/c3_kernel_stats.csv
 python - <<'PY'
