@@ -605,9 +605,9 @@ struct GcmArgs {
     // single-key kernel: the waves of its grid (packets past its full passes are left to
     // gcm_single_tail_kernel), 0 = it takes every packet itself
     uint32_t tail_slots;
-    // the device receive's settle and window finish in the epilogue (rxwin.hpp RxFold), or null:
-    // desc is then the admitted packets compacted, and status the receive's, by arrival index
-    const RxFold* rx;
+    // the device receive's admission mask (window.cpp): only packets with adm[p] != 0 are opened, the
+    // others keep the status the receive's plan gave them (RX instantiations only)
+    const uint8_t* adm;
 };
 
 struct PktShape {
@@ -934,18 +934,18 @@ __device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uin
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
 // own (optional): the packet's descriptor itself, not args.desc[p] (the per-packet kernel's, rebased).
-// RX: the device receive's open (args.rx; rxt the workgroup's RxWgTab), an instantiation of its own
-// so the plain opens keep their registers.
+// RX: the device receive's open (args.adm), an instantiation of its own so the plain opens keep their
+// registers.
 template <bool OPEN, bool CS = false, bool RX = false, class GH, class TL>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
                                                  bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
                                                  uint32_t lane, uint32_t lg, const uint4* cs_pow = nullptr,
-                                                 const neb_desc* own = nullptr, RxWgTab* rxt = nullptr) {
+                                                 const neb_desc* own = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
     // the device receive opens only what its windows admitted (the rest keep the plan's status)
     if constexpr (RX) {
-        if (valid) valid = args.rx->adm[p] != 0u;
+        if (valid) valid = args.adm[p] != 0u;
     }
     neb_desc d = {};
     if (valid) d = own ? *own : args.desc[p];
@@ -1072,10 +1072,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         if (run && cs_on && l == LPP - 1u) V = xor4(V, gcm_csum_fix(d, sh.n, sh.na, cs_acc, cs_fk, args.arena, cs_pow));
     }
     if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
-    if constexpr (RX)  // (every lane: the settle aggregates over the wave)
-        rx_fold_settle(*args.rx, *rxt, args.status, p, (int32_t)st, valid && l == LPP - 1u);
-    else if (valid && l == LPP - 1u)
-        args.status[p] = (int32_t)st;
+    if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
 }
 
 __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rks[60]) {
@@ -1118,7 +1115,7 @@ struct SingleLdsCs : SingleLds {
     uint4 pow2[10 * 16];  // 2.5 KiB  Shoup tables of H^(2^j), j < 10 (the TX checksum correction)
 };
 
-// CS: the TX seal with the L4 checksums (gcm_csum_fix); RX: the device receive's open (GcmArgs::rx)
+// CS: the TX seal with the L4 checksums (gcm_csum_fix); RX: the device receive's open (GcmArgs::adm)
 template <bool OPEN, bool CS = false, bool RX = false>
 __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(GcmArgs args) {
     __shared__ std::conditional_t<CS, SingleLdsCs, SingleLds> lds;
@@ -1147,8 +1144,6 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
         if (tid < 160u) lds.pow2[tid] = ld_rec4(srec, rec_shoup_pow2(tid >> 4) + 4u * (tid & 15u));
         cs_pow = lds.pow2;
     }
-    __shared__ RxWgTab rxt;
-    if constexpr (RX) rx_wg_init(rxt, tid, kSingleThreads);
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
@@ -1179,14 +1174,12 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
         const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
 #endif
         const uint32_t p = grp * kPpw + lane / kLpp;
-        gcm_packet_group<OPEN, CS, RX>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, cs_pow, nullptr,
-                                       &rxt);
+        gcm_packet_group<OPEN, CS, RX>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, cs_pow);
 #ifdef NEB_WAVE_TRACE
         wave_trace(lane, trace_k++, blockIdx.x << 20 | wave << 16 | 16u << 8 | 2u << 4 | 1u, grp, tc0,
                    __builtin_amdgcn_s_memrealtime());
 #endif
     }
-    if constexpr (RX) rx_wg_flush(*args.rx, rxt, tid, kSingleThreads);
 }
 
 // The tail pass: the packets after gcm_single_kernel's full passes over args.tail_slots waves (the
@@ -1236,8 +1229,6 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     if (tid < 128u) lds.pos[tid] = ld_rec4(srec, kRecPos64 + 4u * tid);
     if (tid < 256u) lds.m16[tid] = ld_rec4(srec, kRecShoup + 4u * tid);
     if (tid < 48u) lds.hi[tid] = ld_rec4(srec, (tid < 16u ? kRecShoup + 15u * 64u : tid < 32u ? kRecShoup32 : kRecShoup48) + 4u * (tid & 15u));
-    __shared__ RxWgTab rxt;
-    if constexpr (RX) rx_wg_init(rxt, tid, kTailWaves * kWave);
     uint32_t rks[60];
     load_round_keys(srec, rks);
     __syncthreads();
@@ -1246,10 +1237,8 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
     const bool key_ok = __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
     for (uint32_t t = blockIdx.x * kTailWaves + wave; t < tgroups; t += gridDim.x * kTailWaves) {
         const uint32_t p = p0 + kTailPpw * t + (lane >> kTailLg);
-        gcm_packet_group<OPEN, false, RX>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, kTailLg,
-                                          nullptr, nullptr, &rxt);
+        gcm_packet_group<OPEN, false, RX>(args, p, p < npkt, args.key_hint, key_ok, RkRegs{rks}, gh, T, lane, kTailLg);
     }
-    if constexpr (RX) rx_wg_flush(*args.rx, rxt, tid, kTailWaves * kWave);
 }
 
 // ---- one packet, its bytes in the kernel arguments (the per-packet CipherState calls) ---------
@@ -1421,8 +1410,6 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
 #endif
     fill_ttab<256u * 32u, kChunkThreads>(lds.ttab, tid, ttab_entry);
     if (tid == 0) wg_cursor = kChunkWaves;
-    __shared__ RxWgTab rxt;
-    if constexpr (RX) rx_wg_init(rxt, tid, kChunkThreads);
     __syncthreads();
 #ifdef NEB_WAVE_TRACE
     uint32_t trace_k = 1;
@@ -1477,8 +1464,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
                 const uint32_t q = g0 + (ln >> 2);
                 const bool valid = q < count;
                 const uint32_t p = valid ? ca.sorted[start + q] : 0u;
-                gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u, nullptr, nullptr,
-                                                  &rxt);
+                gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
             }
         } else {
             const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
@@ -1490,8 +1476,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             const bool valid = q < count;
             const uint32_t p = valid ? ca.sorted[start + q] : 0u;
             const GhChunkTree gh{wtab, wpos};
-            gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg, nullptr, nullptr,
-                                              &rxt);
+            gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
@@ -1504,7 +1489,6 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
 #endif
         c = cn;
     }
-    if constexpr (RX) rx_wg_flush(*args.rx, rxt, tid, kChunkThreads);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1802,7 +1786,7 @@ static void launch_k(K kern, dim3 grid, dim3 block, hipStream_t s, hipEvent_t st
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                           int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx) {
+                                           int hdr_from_dst, hipEvent_t stop, const uint8_t* rx) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, 0u, rx};
     const uint32_t groups = (n + neb::kPpw - 1u) / neb::kPpw;
     const bool cs = !open && hdr_from_dst == 2;  // the TX seal with its checksums (tx.hip)
@@ -1907,7 +1891,7 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst,
-                                            hipEvent_t stop, const neb::RxFold* rx) {
+                                            hipEvent_t stop, const uint8_t* rx) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u, rx};
     neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks, max_short};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a

@@ -237,18 +237,8 @@ struct ChachaArgs {
     int32_t* status;
     const uint32_t* npkt_dev;  // optional: the batch's packet count in device memory (min with npkt)
     uint32_t hdr_from_dst;     // TX batches: the first `flags` plaintext bytes from dst (GcmArgs)
-    const RxFold* rx;          // the device receive's epilogue (GcmArgs::rx), or null
+    const uint8_t* adm;        // the device receive's admission mask (GcmArgs::adm; RX instantiations)
 };
-
-// packet p's status, by its 16th lane; with a receive epilogue every lane takes part (RxFold)
-template <bool OPEN, bool RX>
-__device__ __forceinline__ void chacha_status(const ChachaArgs& args, RxWgTab* rxt, uint32_t p, uint32_t st,
-                                              bool holder) {
-    if constexpr (RX)
-        rx_fold_settle(*args.rx, *rxt, args.status, p, (int32_t)st, holder);
-    else if (holder)
-        args.status[p] = (int32_t)st;
-}
 
 // Payload and AAD blocks loaded one round ahead of their use (1) or in their round (0). Off: a
 // round ahead measured 2-3% slower on C4 (110.0 vs 107.1 µs per seal launch, rocprof A/B,
@@ -256,8 +246,7 @@ __device__ __forceinline__ void chacha_status(const ChachaArgs& args, RxWgTab* r
 // One wave's group of 4 packets (16 lanes each): packets 4·grp .. 4·grp + 3 of the batch, the
 // descriptor of packet p from desc_of(p).
 template <bool OPEN, bool RX = false, class DF>
-__device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t grp, uint32_t npkt, DF&& desc_of,
-                                             RxWgTab* rxt = nullptr) {
+__device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t grp, uint32_t npkt, DF&& desc_of) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & 15u;
     const uint32_t w = l & 3u;      // column within the quad
@@ -268,7 +257,7 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
     {
         const uint32_t p = grp * 4u + q;
         // the device receive opens only what its windows admitted (the rest keep the plan's status)
-        const bool valid = p < npkt && !(RX && !args.rx->adm[p]);
+        const bool valid = p < npkt && !(RX && !args.adm[p]);
         neb_desc d = {};
         if (valid) d = desc_of(p);
         uint32_t st = NEB_STATUS_OK;
@@ -291,7 +280,7 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 16));
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, 32));
         if (rmax == 0u) {  // (wave-uniform)
-            chacha_status<OPEN, RX>(args, rxt, p, st, valid && l == 15u);
+            if (valid && l == 15u) args.status[p] = (int32_t)st;
             return;
         }
 
@@ -388,7 +377,7 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
                 }
             }
         }
-        chacha_status<OPEN, RX>(args, rxt, p, st, valid && l == 15u);
+        if (valid && l == 15u) args.status[p] = (int32_t)st;
     }
 }
 
@@ -398,14 +387,8 @@ __global__ __launch_bounds__(kChThreads) void chacha_batch_kernel(ChachaArgs arg
     uint32_t npkt = args.npkt;
     if (args.npkt_dev) npkt = min(npkt, __builtin_amdgcn_readfirstlane(*args.npkt_dev));
     const uint32_t ngroups = (npkt + 3u) >> 2;
-    __shared__ RxWgTab rxt;
-    if constexpr (RX) {
-        rx_wg_init(rxt, threadIdx.x, kChThreads);
-        __syncthreads();
-    }
     for (uint32_t grp = blockIdx.x * kChWavesPerWG + wave; grp < ngroups; grp += gridDim.x * kChWavesPerWG)
-        chacha_group<OPEN, RX>(args, grp, npkt, [&](uint32_t p) { return args.desc[p]; }, &rxt);
-    if constexpr (RX) rx_wg_flush(*args.rx, rxt, threadIdx.x, kChThreads);
+        chacha_group<OPEN, RX>(args, grp, npkt, [&](uint32_t p) { return args.desc[p]; });
 }
 
 // One packet, its bytes in the kernel arguments (the per-packet path; aes_gcm.hip gcm_one_kernel
@@ -508,7 +491,7 @@ extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                       int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx) {
+                                       int hdr_from_dst, hipEvent_t stop, const uint8_t* rx) {
     neb::ChachaArgs a{d_desc, n, d_arena, d_keys, max_keys, key_hint, d_status, d_n, (uint32_t)hdr_from_dst, rx};
     if (open && rx) return launch_chacha<true, true>(a, cu_count, s, stop);
     return open ? launch_chacha<true>(a, cu_count, s, stop) : launch_chacha<false>(a, cu_count, s, stop);

@@ -41,7 +41,7 @@ extern "C" hipError_t neb_fence_keys(const neb_desc* in, neb_desc* out, uint32_t
 extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                            const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                            int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                           int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx);
+                                           int hdr_from_dst, hipEvent_t stop, const uint8_t* rx);
 extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in, uint32_t in_len,
                                   uint32_t len, uint64_t counter, uint8_t* out, int32_t* status, const uint32_t* d_keys,
                                   uint32_t max_keys, uint32_t key, hipStream_t s);
@@ -53,7 +53,7 @@ extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, ui
                                             const uint32_t* d_sorted, const uint4* d_chunks,
                                             uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
                                             int cu_count, hipStream_t s, int hdr_from_dst, hipEvent_t stop,
-                                            const neb::RxFold* rx);
+                                            const uint8_t* rx);
 extern "C" hipError_t neb_gcm_probe(void);
 extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int hdr_from_dst);
 #ifndef NEB_TX_CSUM_SEAL
@@ -62,7 +62,7 @@ extern "C" uint32_t neb_gcm_single_slots(uint32_t n, int cu_count, int open, int
 extern "C" hipError_t neb_chacha_batch(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                        const uint32_t* d_keys, uint32_t max_keys, uint32_t key_hint,
                                        int32_t* d_status, const uint32_t* d_n, int cu_count, hipStream_t s,
-                                       int hdr_from_dst, hipEvent_t stop, const neb::RxFold* rx);
+                                       int hdr_from_dst, hipEvent_t stop, const uint8_t* rx);
 
 // The stream a workspace's `done` event was last recorded on. A batch on that same stream is
 // ordered after it already and skips the cross-stream wait (a barrier packet that cost ≈ 5 µs between
@@ -836,14 +836,13 @@ static bool bind_events() {
 // d_n (optional): the batch's real packet count in device memory, at most n (a batch whose size is
 // only known on the device, e.g. the segments of a TX batch). hdr_from_dst: the TX batch's
 // descriptors (tx.hip) read their first `flags` plaintext bytes from the destination.
-// rx (optional, opens only): the device receive's settle and window finish run in the open kernel's
-// epilogue (rxwin.hpp RxFold); d_desc is then the admitted packets compacted and d_status the
-// caller's statuses by arrival index.
+// rx (optional, opens only): the device receive's admission mask; only packets with rx[i] != 0 are
+// opened, the others keep the statuses its plan wrote (window.cpp, rxwin.hip).
 // prebinned: the mixed-key binning of this batch is already in `sched` (neb_prebin, ordered before s).
 static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint32_t* d_n = nullptr,
                                SchedSpace* sched = nullptr, int hdr_from_dst = 0, hipEvent_t stop = nullptr,
-                               const neb::RxFold* rx = nullptr, bool prebinned = false) {
+                               const uint8_t* rx = nullptr, bool prebinned = false) {
     if (alg == NEB_ALG_AESGCM) {
         if (key_hint != NEB_KEYS_MIXED)
             return neb_gcm_batch_single(open, d_desc, n, d_arena, e->d_keys, e->max_keys, key_hint, d_status, d_n,
@@ -1072,7 +1071,7 @@ int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint) { return che
 
 // Open the first *d_n (a count in device memory) of at most n descriptors, on stream s.
 int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx,
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint8_t* rx,
                          void* prebinned) {
     if (n == 0) return NEB_OK;
     hipError_t err = launch_batch(e, alg, 1, d_desc, n, d_arena, d_status, key_hint, s, d_n,

@@ -132,10 +132,7 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
     if (t == 0) s_mixed = 0;
     for (uint32_t x = t; x < so.per_blk; x += 256) {
         const size_t wi = (size_t)b * so.per_blk + x;
-        if (wi < win.count) {
-            ws.wflag[wi] = 0;
-            ws.pending[wi] = 0;
-        }
+        if (wi < win.count) ws.wflag[wi] = 0;
     }
     if (b == 0 && t == 0) {
         *ws.ticket = 0;
@@ -320,9 +317,10 @@ __device__ __forceinline__ uint64_t rx_peek(const uint64_t* g) {
 //     that continues into this block from before it;
 //  3. which packets the sequential receive would decrypt, if every tag verified (safe windows):
 //     c > the run's max so far, or inside the window, not received before and the first
-//     occurrence of its (window, counter) (the table the keys kernel filled); compacted into
-//     sub_map / sub_desc with one atomic per workgroup (order is immaterial to the open); the run's
-//     last packet sets its window's final current and the range of counters that leave it.
+//     occurrence of its (window, counter) (the table the keys kernel filled): the admission mask
+//     adm, which the open reads (it runs over the whole batch and skips the rest: no compaction, so
+//     the mixed-key binning can run beside this plan, window.cpp); the run's last packet sets its
+//     window's final current and the range of counters that leave it.
 // A window with a counter near the wrap (wrisky, from the keys kernel) or a current near it is
 // decided on the host.
 __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_desc* __restrict__ desc, uint32_t n,
@@ -333,14 +331,11 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
     __shared__ uint64_t s_incl[kRxBlock];
     __shared__ uint64_t s_pre;
     __shared__ uint32_t s_fh, s_b;
-    __shared__ uint32_t s_pw[kRxThreads], s_pn[kRxThreads];  // admitted packets per window (pending)
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     if (t == 0) {
         s_b = atomicAdd(ws.ticket, 1u);
         s_fh = kRxBlock;
     }
-    s_pw[t] = ~0u;
-    s_pn[t] = 0;
     __syncthreads();
     const uint32_t b = s_b, b0 = b * kRxBlock, k0 = b0 + t * kRxItems;
     const uint32_t gen = ws.gen;
@@ -460,7 +455,7 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
             if (timed_out) {
                 atomicOr(ws.err, 1u);
                 ws.need_host[0] = 1u;
-                ws.need_host[1] = 1u;  // the batch fails; no window moves (rx_fold_finish reads err)
+                ws.need_host[1] = 1u;  // the batch fails; no window moves (rx_final_window_kernel reads err)
                 s_fh = 0xFFFFFFFFu;    // admit nothing here
             }
         }
@@ -473,7 +468,6 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
         const uint64_t v = s_incl[k - b0];
         return k - b0 >= fh ? v : max(pre, v);
     };
-    uint32_t okm = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kRxItems; j++) {
         const uint32_t k = k0 + j;
@@ -506,34 +500,10 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
             ok = ok && ws.tab_min[rx_slot(ws, i, w, cc, false)] == (((uint64_t)gen << 32) | (0xFFFFFFFFu - i));
         }
         if (ok) {
-            ws.adm[i] = 1;
-            okm |= 1u << j;
+            ws.adm[i] = 1;  // the open runs it (the admission mask)
         } else {
             status[i] = NEB_STATUS_REPLAY;  // (a slow window's statuses are rewritten on the host)
         }
-    }
-    // each window's admitted packets, pending until the open settles their verdicts (RxFold): counted
-    // per window in LDS, then one atomic per (workgroup, window) (one tunnel's batch would otherwise
-    // put a thousand per-wave atomics on one word)
-    {
-        const uint32_t aw = okm ? wj[0] : win.count;  // (kRxItems == 1)
-        uint64_t todo = __ballot(okm != 0u);
-        while (todo) {
-            const uint32_t leader = __builtin_ctzll(todo);
-            const uint32_t lw = __shfl(aw, (int)leader);
-            const uint64_t same = __ballot(okm != 0u && aw == lw);
-            if (lane == leader)
-                for (uint32_t h = lw % kRxThreads;; h = (h + 1u) % kRxThreads) {
-                    const uint32_t o = atomicCAS(&s_pw[h], ~0u, lw);  // (at most kRxThreads windows)
-                    if (o == ~0u || o == lw) {
-                        atomicAdd(&s_pn[h], (uint32_t)__popcll(same));
-                        break;
-                    }
-                }
-            todo &= ~same;
-        }
-        __syncthreads();
-        if (s_pw[t] != ~0u) atomicAdd(&ws.pending[s_pw[t]], s_pn[t]);
     }
 }
 
@@ -572,6 +542,148 @@ __global__ __launch_bounds__(256) void rx_wire_fix_kernel(const int32_t* __restr
     if (i < n && gate[i] != NEB_STATUS_OK) status[i] = gate[i];
 }
 
+__device__ __forceinline__ bool rx_fast(uint32_t fl) { return (fl & kRxTouched) && !(fl & (kRxRisky | kRxSlow)); }
+
+// Per admitted packet, in run order (the windows' runs are contiguous there, so the atomics below
+// aggregate): its tag verdict (the status the open wrote at its arrival index; a failure sends the
+// window to the sequential host pass, which rewrites that window's statuses), its counter into the
+// scratch bitmap when it stays in the final window, and into the received count when it leaves it.
+// The window's fast / slow state is not known yet: the finish applies the scratch and the count to
+// fast windows only and clears the scratch of the others. One atomic per (wave, window, word)
+// instead of one per packet (a single tunnel's batch would otherwise serialise tens of thousands
+// of atomics on one address); every lane runs to the end (the shuffles need the whole wave).
+__global__ void rx_settle_kernel(uint32_t n, RxDevWin win, RxDevWs ws, const int32_t* __restrict__ status) {
+    __shared__ unsigned long long s_recv;
+    if (threadIdx.x == 0) s_recv = 0;
+    __syncthreads();
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t w = win.count;
+    uint64_t c = 0, cur = 0, lo = 1, hi = 0;
+    bool ok = false;
+    if (k < n) {
+        const uint32_t i = ws.run_i[k];
+        if (ws.adm[i]) {
+            const int32_t st = status[i];
+            w = ws.run_w[k];
+            c = ws.run_c[k];
+            ws.verdict[i] = st;
+            ok = st == NEB_STATUS_OK;
+            if (!ok) atomicOr(&ws.wflag[w], kRxSlow);
+            cur = ws.curnew[w];
+            lo = ws.exit_lo[w];
+            hi = ws.exit_hi[w];
+        }
+    }
+    const uint64_t len = win.length;
+    const bool in_final = ok && (cur < len || c > cur - len);
+    const bool leaves = ok && c >= lo && c <= hi;
+    const uint64_t p = c & (len - 1u);
+    // word key of this lane's bit; lanes of one (window, word) OR their bits into one atomic
+    const uint64_t wkey = in_final ? (((uint64_t)w << 32) | (p >> 6)) : ~0ull;
+    uint64_t pending = __ballot(in_final);
+    while (pending) {
+        const uint32_t leader = __builtin_ctzll(pending);
+        const uint64_t lk = __shfl(wkey, (int)leader);
+        const bool mine = in_final && wkey == lk;
+        uint64_t bits = mine ? 1ull << (p & 63) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
+        if (__lane_id() == leader)
+            atomicOr(reinterpret_cast<unsigned long long*>(ws.scratch + ((size_t)w << win.words_lg) + (p >> 6)), bits);
+        pending &= ~__ballot(mine);
+    }
+    // counters leaving the window: one atomic per (wave, window), through LDS for the window of
+    // the workgroup's first run position
+    const uint32_t k0 = blockIdx.x * blockDim.x;
+    const uint32_t w0 = k0 < n ? ws.run_w[k0] : win.count;
+    uint64_t pend2 = __ballot(leaves);
+    while (pend2) {
+        const uint32_t leader = __builtin_ctzll(pend2);
+        const uint32_t lw = __shfl(w, (int)leader);
+        const uint64_t same = __ballot(leaves && w == lw);
+        if (__lane_id() == leader) {
+            if (w == w0)
+                atomicAdd(&s_recv, (unsigned long long)__popcll(same));
+            else
+                atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w), (unsigned long long)__popcll(same));
+        }
+        pend2 &= ~same;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_recv) atomicAdd(reinterpret_cast<unsigned long long*>(ws.recv + w0), s_recv);
+}
+
+// bits of the slots [a, b) within the word whose first slot is q0 (nb slots)
+__device__ __forceinline__ uint64_t rx_seg_mask(uint64_t q0, uint32_t nb, uint64_t a, uint64_t b) {
+    const uint64_t lo = max(a, q0), hi = min(b, q0 + nb);
+    if (lo >= hi) return 0;
+    const uint32_t m = (uint32_t)(hi - lo);
+    return (m == 64u ? ~0ull : ((1ull << m) - 1u)) << (lo - q0);
+}
+// ... within the circular slot range [start, start + count) mod len (start < len)
+__device__ __forceinline__ uint64_t rx_ring_mask(uint64_t q0, uint32_t nb, uint64_t start, uint64_t count,
+                                                 uint64_t len) {
+    if (count == 0) return 0;
+    if (count >= len) return nb == 64u ? ~0ull : ((1ull << nb) - 1u);
+    uint64_t m = rx_seg_mask(q0, nb, start, min(start + count, len));
+    if (start + count > len) m |= rx_seg_mask(q0, nb, 0, start + count - len);
+    return m;
+}
+
+// Per fast window, lanes over its bitmap words (min(words, 64) lanes a window, so a wave holds
+// one or more whole windows): the slots of the counters new in (cur0, cur] are cleared and the
+// admitted counters ORed in; the old window's counters that leave it are counted as received
+// where their old bit is set (tools/rxwin_model.py finish_ranges, checked against the oracle);
+// then the window's lost count and current.
+__global__ void rx_final_window_kernel(RxDevWin win, RxDevWs ws) {
+    const uint32_t lanes_lg = win.words_lg < 6u ? win.words_lg : 6u, L = 1u << lanes_lg;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t wl = t >> lanes_lg;
+    const uint32_t sub = (uint32_t)t & (L - 1u);
+    const uint32_t w = wl < win.count ? (uint32_t)wl : 0u;
+    const uint32_t fl = wl < win.count ? ws.wflag[w] : 0u;
+    // After a scan lookback timeout the batch fails and no window moves: the blocks that did finish
+    // computed their windows' finals from a partial prefix, and the failed block's packets were never
+    // opened, so their counters are unauthenticated (a forged high counter must not advance a window).
+    const bool err = *ws.err != 0u;
+    const bool fast = rx_fast(fl) && !err;
+    // a touched window that is risky or slow goes to the host (pinned host word 0; word 1: the
+    // timeout, set by the scan)
+    if ((fl & kRxTouched) && (fl & (kRxRisky | kRxSlow)) && sub == 0) ws.need_host[0] = 1u;
+    uint64_t r = 0;
+    uint64_t cur = 0, lo = 1, hi = 0;
+    if ((fl & kRxTouched) && !fast) {  // the settle may have set bits of a window finished on the host
+        uint64_t* scr = ws.scratch + ((size_t)w << win.words_lg);
+        for (uint32_t q = sub; q < win.words; q += L) scr[q] = 0;
+    }
+    if (fast) {
+        const uint64_t len = win.length, mask = len - 1u, cur0 = win.cur[w];
+        cur = ws.curnew[w];
+        lo = ws.exit_lo[w];
+        hi = ws.exit_hi[w];
+        const uint32_t nb = len < 64u ? (uint32_t)len : 64u;
+        const uint64_t base = (cur >= len && cur - len > cur0) ? cur - len : cur0;
+        const uint64_t ehi = min(hi, cur0);
+        uint64_t* bits = win.bits + ((size_t)w << win.words_lg);
+        uint64_t* scr = ws.scratch + ((size_t)w << win.words_lg);
+        for (uint32_t q = sub; q < win.words; q += L) {
+            const uint64_t q0 = (uint64_t)q * 64u;
+            const uint64_t clear = rx_ring_mask(q0, nb, (base + 1u) & mask, cur - base, len);
+            const uint64_t leaving = ehi >= lo ? rx_ring_mask(q0, nb, lo & mask, ehi - lo + 1u, len) : 0ull;
+            const uint64_t old = bits[q];
+            bits[q] = (old & ~clear) | scr[q];
+            scr[q] = 0;  // zero again for the next batch (zeroed once at allocation)
+            r += (uint32_t)__popcll(old & leaving);
+        }
+    }
+    for (uint32_t o = L >> 1; o > 0; o >>= 1) r += __shfl_xor(r, (int)o);  // within the window's lanes
+    if (fast && sub == 0) {
+        const uint64_t exits = hi >= lo ? hi - lo + 1u : 0u;
+        win.lost[w] += (int64_t)(exits - ws.recv[w] - r);
+        win.cur[w] = cur;
+    }
+}
+
 }  // namespace neb
 
 using neb::RxDevWin;
@@ -585,8 +697,8 @@ static int rx_bits_for(uint32_t v) {
     return bits;
 }
 
-// Phase 1: group by window, prefix maxima, first occurrences, admission for the safe windows, and
-// the admitted packets' descriptors compacted (count in *ws->nsub).
+// Phase 1: group by window, prefix maxima, first occurrences, and the admission mask for the safe
+// windows (ws->adm).
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const RxDevWin* win, const RxDevWs* ws,
                                      int32_t* d_status, hipStream_t s) {
     neb::RxSort so{};
@@ -647,5 +759,14 @@ extern "C" hipError_t neb_rxdev_wire(const neb_rx_packet* d_pk, uint32_t n, cons
 extern "C" hipError_t neb_rxdev_wire_fix(const int32_t* d_gate, int32_t* d_status, uint32_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(neb::rx_wire_fix_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, d_gate, d_status, n);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t neb_rxdev_finish(uint32_t n, const RxDevWin* win, const RxDevWs* ws, int32_t* d_status,
+                                       hipStream_t s) {
+    hipLaunchKernelGGL(neb::rx_settle_kernel, rx_grid(n), dim3(256), 0, s, n, *win, *ws, d_status);
+    const uint32_t lanes_lg = win->words_lg < 6u ? win->words_lg : 6u;
+    hipLaunchKernelGGL(neb::rx_final_window_kernel, rx_grid((size_t)win->count << lanes_lg), dim3(256), 0, s, *win,
+                       *ws);
     return hipGetLastError();
 }

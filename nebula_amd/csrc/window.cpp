@@ -51,7 +51,7 @@ void neb_rx_pipe_end(neb_engine* e);
 int neb_engine_device_of(const neb_engine* e);
 int neb_check_batch_args(neb_engine* e, int alg, uint32_t key_hint);
 int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_t n, const uint32_t* d_n,
-                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const neb::RxFold* rx,
+                         uint8_t* d_arena, int32_t* d_status, uint32_t key_hint, hipStream_t s, const uint8_t* rx,
                          void* prebinned);
 void* neb_sched_space_new();
 void neb_sched_space_free(void* p);
@@ -553,11 +553,7 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
         d->ws_n = 0;
         RX_HIP(hipMalloc((void**)&d->ws_mem, bytes));
         neb::rx_ws_layout(n, v.count, v.words, d->ws_mem, &d->ws);
-        d->ws.need_host = d->h_host;
-        // the open kernels' epilogue reads the workspace through its device copy (rxwin.hpp RxFold)
-        const neb::RxFold fold = neb::rx_fold_of(v, d->ws);
-        RX_HIP(hipMemcpy(d->ws.fold, &fold, sizeof fold, hipMemcpyHostToDevice));
-        RX_HIP(hipStreamSynchronize(nullptr));
+
         // the scratch bitmap is zeroed once here and again by each batch as it is consumed
         RX_HIP(hipMemsetAsync(d->ws.scratch, 0, ((size_t)v.count << v.words_lg) * 8, s));
         RX_HIP(hipMemsetAsync(d->ws.mixed, 0, 4, s));  // no generation is 0
@@ -603,16 +599,19 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
     // 1. group by window, prefix maxima, first occurrences; admission for the safe windows
     RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
     const auto t1 = now();
-    // 2. one open over the batch that runs the admitted packets only; its epilogue settles each
-    //    verdict and finishes every window whose packets all verified (rxwin.hpp RxFold)
+    // 2. one open over the batch that runs the admitted packets only (the plan's mask), writing their
+    //    statuses at their arrival indices
     if (prebinned) RX_HIP(hipStreamWaitEvent(s, d->join, 0));
-    rc = neb_open_batch_count(e, alg, d_desc, n, nullptr, d_arena, d_status, key_hint, s, ws.fold, prebinned);
+    rc = neb_open_batch_count(e, alg, d_desc, n, nullptr, d_arena, d_status, key_hint, s, ws.adm, prebinned);
     if (rc != NEB_OK) return rc;
     const auto t2 = now();
+    // 3. the verdicts into the windows, and the parallel finish of every window whose packets all verified
+    RX_HIP(neb_rxdev_finish(n, &v, &ws, d_status, s));
+    const auto t3 = now();
     RX_HIP(hipStreamSynchronize(s));
     if (prof)
-        std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, open %.1f us, wait %.1f us\n", n, us(t0, t1), us(t1, t2),
-                     us(t2, now()));
+        std::fprintf(stderr, "rxdev n=%u enqueue plan %.1f, open %.1f, finish %.1f us, wait %.1f us\n", n, us(t0, t1),
+                     us(t1, t2), us(t2, t3), us(t3, now()));
     // the plan and the open flag, in pinned host memory, whether any window needs the sequential finish
     const uint32_t need = __atomic_load_n(d->h_host, __ATOMIC_ACQUIRE);
     if (__atomic_load_n(d->h_host + 1, __ATOMIC_ACQUIRE)) return NEB_ERR_HIP;  // a scan lookback timed out
