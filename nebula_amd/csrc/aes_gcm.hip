@@ -943,12 +943,14 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                                                  const neb_desc* own = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
-    // the device receive opens only what its windows admitted (the rest keep the plan's status)
-    if constexpr (RX) {
-        if (valid) valid = args.adm[p] != 0u;
-    }
     neb_desc d = {};
-    if (valid) d = own ? *own : args.desc[p];
+    uint32_t admit = 1u;
+    if (valid) {
+        d = own ? *own : args.desc[p];
+        if constexpr (RX) admit = args.adm[p];  // (beside the descriptor's load, not behind it)
+    }
+    // the device receive opens only what its windows admitted (the rest keep the plan's status)
+    if constexpr (RX) valid = valid && admit != 0u;
     uint32_t st = NEB_STATUS_OK;
     if (!key_ok || d.key_id != expect_key) st = NEB_STATUS_BAD_KEY;
     if (!OPEN && st == NEB_STATUS_OK && d.counter >= kRejectAfterMessages) st = NEB_STATUS_EXHAUSTED;

@@ -1087,27 +1087,29 @@ int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_
 // staged batch (zero-copy on pinned memory) on the queue's stream.
 void* neb_sched_space_new() { return new (std::nothrow) SchedSpace; }
 
-// The device receive (window.cpp): the mixed-key AES-GCM binning of its batch on `aux`, after `fork`
-// (recorded on the receive's stream once the descriptors are there), into the receive's own
-// scheduler workspace, beside the window plan on the receive's stream; `join` marks its end. The
-// open then runs with it (neb_open_batch_count's `prebinned`) after the stream waits on `join`.
-int neb_prebin(neb_engine* e, const neb_desc* d_desc, uint32_t n, void* sched, hipStream_t aux, hipEvent_t fork,
-               hipEvent_t join) {
+// The device receive (window.cpp): its mixed-key AES-GCM open is binned by extra workgroups of the
+// receive's own plan launches (rxwin.hpp RxBin) into the receive's scheduler workspace `sched`,
+// which this sizes for n packets and orders after its last open; the open then runs with it
+// (neb_open_batch_count's `prebinned`). neb_rx_sched_abort after a failed plan (the counters are
+// then in an unknown state: the next batch clears them).
+int neb_rx_sched_begin(neb_engine* e, uint32_t n, void* sched, hipStream_t s, neb::SchedWs* ws, uint32_t* max_keys) {
     SchedSpace& sp = *static_cast<SchedSpace*>(sched);
     std::lock_guard<std::mutex> g(sp.mu);
-    hipError_t err = hipStreamWaitEvent(aux, fork, 0);
-    if (err == hipSuccess) err = sched_reserve(e, sp, n, aux);
-    if (err == hipSuccess && !sp.last.same(aux)) err = hipStreamWaitEvent(aux, sp.done, 0);  // the last open's reads
-    neb::SchedWs ws = sp.ws;
-    if (err == hipSuccess) err = neb_sched_build(d_desc, n, nullptr, e->max_keys, 4u, &ws, aux);
-    if (err == hipSuccess) err = hipEventRecord(join, aux);
+    hipError_t err = sched_reserve(e, sp, n, s);
+    if (err == hipSuccess && !sp.last.same(s)) err = hipStreamWaitEvent(s, sp.done, 0);  // the last open's reads
     if (err != hipSuccess) {
-        (void)hipStreamSynchronize(aux);
         sp.dirty = true;
-        set_error("prebin", err);
+        set_error("rx binning", err);
         return NEB_ERR_HIP;
     }
+    *ws = sp.ws;
+    *max_keys = e->max_keys;
     return NEB_OK;
+}
+void neb_rx_sched_abort(void* sched) {
+    SchedSpace& sp = *static_cast<SchedSpace*>(sched);
+    std::lock_guard<std::mutex> g(sp.mu);
+    sp.dirty = true;
 }
 void neb_sched_space_free(void* p) {
     auto* sp = static_cast<SchedSpace*>(p);

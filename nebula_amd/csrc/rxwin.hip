@@ -26,6 +26,7 @@
 
 #include "../../include/nebula_aead.h"
 #include "rxwin.hpp"
+#include "sched_body.hpp"
 
 namespace neb {
 
@@ -113,11 +114,13 @@ struct RxSort {
 // keys work instead of after it: inside the keys workgroups' loop (4 packets per thread on 64
 // workgroups) they cost 33-35 µs on C3, as a launch of their own 14 after the keys' 8.
 __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict__ desc, RxDevWin win, RxDevWs ws,
-                                                      RxSort so, uint32_t kgrid) {
+                                                      RxSort so, uint32_t kgrid, RxBin bin) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t s_mixed;
     if (blockIdx.x >= kgrid) {
         const uint32_t e = (blockIdx.x - kgrid) * 256u + threadIdx.x;
+        // the open's binning, pass 1, over the same 256 packets (every lane: its shuffles)
+        if (bin.on) sched_hist_round<1>(desc, so.n, bin.max_keys, 4u, bin.ws, e - threadIdx.x, blockIdx.x - kgrid);
         if (e >= so.n) return;
         const uint32_t k = desc[e].key_id;
         if (k >= win.count || !win.present[k]) return;
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(256) void rx_keys_kernel(const neb_desc* __restrict
         *ws.ticket = 0;
         *ws.err = 0;
     }
+    if (b == 0 && bin.on) sched_clear_cursors(bin.ws);
     if (b >= so.nblk) return;
     for (uint32_t p = 1; p < so.passes; p++) ws.sort_hist[((size_t)p * kRxSortBlocks + b) * 256 + t] = 0;
     __syncthreads();
@@ -194,9 +198,20 @@ __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p
                                                            const uint32_t* __restrict__ src_k,
                                                            const uint32_t* __restrict__ src_v, uint32_t* dst_k,
                                                            uint32_t* dst_v, const uint32_t* mixed, uint32_t gen,
-                                                           uint32_t* run_w, uint32_t* run_i) {
+                                                           uint32_t* run_w, uint32_t* run_i, RxBin bin) {
     __shared__ uint32_t gbase[256], run[256], wcnt[4][256], wtot[4];
     __shared__ uint32_t agg[kRxSortBlocks << kRxSortDigit];
+    if (blockIdx.x >= so.nblk) {  // the open's binning: pass 2 beside the first sort pass, 3 beside the second
+        const uint32_t r = blockIdx.x - so.nblk;
+        if (FIRST) {
+            __shared__ SchedAllocLds<1> sl;
+            sched_alloc_block<1>(bin.max_keys, bin.ws, r, sl);
+        } else {
+            const uint32_t i = r * 256u + threadIdx.x;
+            if (i < so.n) sched_scatter_one(bin.ws, i);
+        }
+        return;
+    }
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
     if (__builtin_amdgcn_readfirstlane(*mixed) != gen) {
         if (FIRST) {
@@ -325,7 +340,13 @@ __device__ __forceinline__ uint64_t rx_peek(const uint64_t* g) {
 // decided on the host.
 __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_desc* __restrict__ desc, uint32_t n,
                                                                      RxDevWin win, RxDevWs ws,
-                                                                     int32_t* __restrict__ status) {
+                                                                     int32_t* __restrict__ status, uint32_t nscan,
+                                                                     RxBin bin) {
+    if (blockIdx.x >= nscan) {  // the open's binning, pass 3, when the sort took one pass (no ticket)
+        const uint32_t i = (blockIdx.x - nscan) * 256u + threadIdx.x;
+        if (i < n) sched_scatter_one(bin.ws, i);
+        return;
+    }
     __shared__ uint64_t s_v[kRxThreads / 64];
     __shared__ uint32_t s_f[kRxThreads / 64];
     __shared__ uint64_t s_incl[kRxBlock];
@@ -700,7 +721,14 @@ static int rx_bits_for(uint32_t v) {
 // Phase 1: group by window, prefix maxima, first occurrences, and the admission mask for the safe
 // windows (ws->adm).
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const RxDevWin* win, const RxDevWs* ws,
-                                     int32_t* d_status, hipStream_t s) {
+                                     int32_t* d_status, const neb::RxBin* binp, hipStream_t s) {
+    neb::RxBin bin{};
+    if (binp && binp->on) {
+        bin = *binp;
+        bin.hist_blocks = (n + 255u) / 256u;  // (the keys launch's insert workgroups: one packet per thread)
+        bin.alloc_blocks = (neb::sched_nbins(bin.max_keys) + neb::kAllocThreads - 1) / neb::kAllocThreads;
+        bin.scatter_blocks = (n + 255u) / 256u;
+    }
     neb::RxSort so{};
     so.n = n;
     so.items = (n + 256u * neb::kRxSortBlocks - 1) / (256u * neb::kRxSortBlocks);
@@ -714,7 +742,8 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
         sh += so.bits[p];
     }
     const uint32_t kgrid = std::max<uint32_t>(so.nblk, (win->count + so.per_blk - 1) / so.per_blk);
-    hipLaunchKernelGGL(neb::rx_keys_kernel, dim3(kgrid + (n + 255u) / 256u), dim3(256), 0, s, d_desc, *win, *ws, so, kgrid);
+    hipLaunchKernelGGL(neb::rx_keys_kernel, dim3(kgrid + (n + 255u) / 256u), dim3(256), 0, s, d_desc, *win, *ws, so, kgrid,
+                       bin);
     // pass p writes the run arrays when (passes - 1 - p) is even, so the last pass ends there
     for (uint32_t p = 0; p < so.passes; p++) {
         const bool to_run = ((so.passes - 1 - p) & 1u) == 0;
@@ -722,15 +751,21 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
         uint32_t* dv = to_run ? ws->run_i : ws->tmp_v;
         const uint32_t* sk = p == 0 ? ws->keyw : (to_run ? ws->tmp_k : ws->run_w);
         const uint32_t* sv = p == 0 ? nullptr : (to_run ? ws->tmp_v : ws->run_i);
+        // extra workgroups: the binning's pass 2 beside pass 0, its pass 3 beside pass 1
+        const uint32_t extra = !bin.on ? 0u : p == 0 ? bin.alloc_blocks : p == 1 ? bin.scatter_blocks : 0u;
+        neb::RxBin b = bin;
+        if (p > 1) b.on = 0;
         if (p == 0)
-            hipLaunchKernelGGL(neb::rx_sort_pass_kernel<true>, dim3(so.nblk), dim3(256), 0, s, so, p, ws->sort_hist,
-                               sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i);
+            hipLaunchKernelGGL(neb::rx_sort_pass_kernel<true>, dim3(so.nblk + extra), dim3(256), 0, s, so, p,
+                               ws->sort_hist, sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i, b);
         else
-            hipLaunchKernelGGL(neb::rx_sort_pass_kernel<false>, dim3(so.nblk), dim3(256), 0, s, so, p, ws->sort_hist,
-                               sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i);
+            hipLaunchKernelGGL(neb::rx_sort_pass_kernel<false>, dim3(so.nblk + extra), dim3(256), 0, s, so, p,
+                               ws->sort_hist, sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i, b);
     }
-    const dim3 blocks((n + neb::kRxBlock - 1) / neb::kRxBlock);
-    hipLaunchKernelGGL(neb::rx_scan_admit_kernel, blocks, dim3(neb::kRxThreads), 0, s, d_desc, n, *win, *ws, d_status);
+    const uint32_t nscan = (n + neb::kRxBlock - 1) / neb::kRxBlock;
+    const uint32_t extra = bin.on && so.passes == 1 ? bin.scatter_blocks : 0u;  // pass 3 here after one sort pass
+    hipLaunchKernelGGL(neb::rx_scan_admit_kernel, dim3(nscan + extra), dim3(neb::kRxThreads), 0, s, d_desc, n, *win,
+                       *ws, d_status, nscan, bin);
     return hipGetLastError();
 }
 

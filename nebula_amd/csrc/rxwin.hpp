@@ -7,6 +7,7 @@
 #include <algorithm>
 
 #include "../../include/nebula_aead.h"
+#include "sched.hpp"
 
 namespace neb {
 
@@ -35,6 +36,19 @@ struct RxDevWin {  // a set of windows of one length in device memory (neb_dwind
     int64_t* dupe;
     int64_t* oow;
     uint64_t* bits;     // count x words
+};
+
+// The mixed-key open's binning (sched_body.hpp), run by extra workgroups of the plan's own launches
+// instead of three launches of its own: the histogram beside the keys, the allocation beside the
+// first sort pass, the scatter beside the next launch (the second pass, or the scan when there is
+// one pass). The passes depend only on the descriptors and on each other, so each role waits on
+// nothing inside its launch. on = 0: no binning (one key, ChaCha20-Poly1305, or a batch large
+// enough for sub-bins: the open bins it itself).
+struct RxBin {
+    SchedWs ws;
+    uint32_t on;
+    uint32_t max_keys;
+    uint32_t hist_blocks, alloc_blocks, scatter_blocks;
 };
 
 struct RxDevWs {
@@ -136,7 +150,8 @@ inline size_t rx_ws_layout(uint32_t n, uint32_t count, uint32_t words, uint8_t* 
 }  // namespace neb
 
 extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const neb::RxDevWin* win,
-                                     const neb::RxDevWs* ws, int32_t* d_status, hipStream_t s);
+                                     const neb::RxDevWs* ws, int32_t* d_status, const neb::RxBin* bin,
+                                     hipStream_t s);
 extern "C" hipError_t neb_rxdev_gather(const neb_desc* d_desc, uint32_t n, const neb::RxDevWs* ws, hipStream_t s);
 // readOutsidePackets (outside.go:30-114) for one wire packet, up to the decrypt: returns
 // NEB_STATUS_OK with *d describing the Decrypt (header as AAD, in place) or the VerifyRelay (GMAC

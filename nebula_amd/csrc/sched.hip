@@ -4,141 +4,29 @@
 
 #include <cstdlib>
 
-#include <hipcub/hipcub.hpp>
-
 #include "knobs.hpp"
-#include "sched.hpp"
+#include "sched_body.hpp"
 
 namespace neb {
 
-__device__ __forceinline__ uint32_t size_class(const neb_desc& d, uint32_t lpp) {
-    const uint32_t n = ((d.aad_len + 15u) >> 4) + ((d.len + 15u) >> 4) + 1u;  // GHASH / Poly1305 blocks
-    const uint32_t R = (n + lpp - 1u) / lpp;
-    const uint32_t c = R <= 1u ? 0u : 32u - (uint32_t)__builtin_clz(R - 1u);
-    return c < kSizeClasses ? c : kSizeClasses - 1u;
-}
-
-// pass 1: histogram of (size class, key) bins; keys outside the table go to key index max_keys.
-// The returning add also ranks the packet inside its bin, so pass 3 needs no atomics: the adds
-// execute at the memory side (MI355X_MICROARCH.md, global atomics), ≈55 µs per 1 Mi packets each.
-// SUB: sub-bins per bin for this batch (kSubBins for large batches, 1 for small ones: the contention
-// the sub-bins spread is a large batch's, and pass 2 reads SUB words per bin)
 template <uint32_t SUB>
 __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn,
                                   uint32_t max_keys, uint32_t lpp, SchedWs ws) {
-    // the cursors are cleared here (the previous batch's crypto kernel has finished with them);
-    // the bin counts were cleared by the previous batch's pass 2 as it read them
-    if (blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i < kSchedCounters; i += blockDim.x) ws.counters[i] = 0;
+    if (blockIdx.x == 0) sched_clear_cursors(ws);
     if (dn) n = min(n, *dn);
-    // Neighbouring lanes in the same bin (a batch already grouped by key, e.g. a receive batch in
-    // its windows' order) add their count once: the run's first lane adds the run's length and
-    // hands each lane its rank (one returning atomic per run instead of one per packet on the
-    // same word). Every lane of a wave runs every pass (the shuffles), valid lanes are a prefix.
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t upto = lane == 63u ? ~0ull : (2ull << lane) - 1u;  // lanes <= this one
-    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {
-        const uint32_t i = i0 + threadIdx.x;
-        const bool valid = i < n;
-        uint32_t b = 0xFFFFFFFFu;
-        if (valid) {
-            const neb_desc d = desc[i];
-            const uint32_t key = d.key_id < max_keys ? d.key_id : max_keys;
-            b = (size_class(d, lpp) * (max_keys + 1u) + key) * SUB + (blockIdx.x & (SUB - 1u));
-        }
-        const uint32_t pb = (uint32_t)__shfl_up((int)b, 1);
-        const bool head = valid && (lane == 0u || pb != b);
-        const uint64_t hm = __ballot(head);
-        const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
-        const uint32_t hl = 63u - (uint32_t)__builtin_clzll((hm & upto) | 1ull);  // this lane's run head
-        const uint64_t after = hm & ~upto;
-        const uint32_t next = after ? (uint32_t)__builtin_ctzll(after) : nvalid;  // the next run's head
-        uint32_t base = 0;
-        if (head) base = atomicAdd(&ws.hist[b], next - lane);
-        base = (uint32_t)__shfl((int)base, (int)hl);
-        if (valid) {
-            ws.binof[i] = b;
-            ws.binpos[i] = base + (lane - hl);
-        }
-    }
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x)
+        sched_hist_round<SUB>(desc, n, max_keys, lpp, ws, i0, blockIdx.x);
 }
 
-// pass 2: every non-empty bin reserves its range of `sorted` and its chunks. The reservations are
-// aggregated per workgroup (block scans, then one atomic per counter and workgroup): one atomic per
-// bin put ~4096 returning atomics on a single word for a 4096-tunnel batch.
-constexpr int kAllocThreads = 256;
 template <uint32_t SUB>
 __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
-    using Scan = hipcub::BlockScan<uint32_t, kAllocThreads>;
-    __shared__ typename Scan::TempStorage tmp;
-    __shared__ uint32_t wg_base[4];
-    const uint32_t nb = sched_nbins(max_keys);
-    const uint32_t b = blockIdx.x * kAllocThreads + threadIdx.x;  // grid covers the bins exactly once
-    uint32_t sc[SUB], c = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < SUB; j++) {
-        sc[j] = b < nb ? ws.hist[b * SUB + j] : 0u;
-        c += sc[j];
-    }
-    if (c)  // clear for the next batch
-#pragma unroll
-        for (uint32_t j = 0; j < SUB; j++) ws.hist[b * SUB + j] = 0u;
-    const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
-    const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
-    const uint32_t lg = tail ? sched_tail_lg(tail, cls) : 2u;
-    // the bin's first `fpk` packets run in groups at 4 lanes per packet (a 9-15 packet tail is a
-    // partial group), packed sched_groups(cls) groups to a front chunk; a tail at 8 or 16 lanes is
-    // one back chunk. The crypto kernels take the front chunks, then the back ones. Front <= n/16 +
-    // bins, back <= bins and front + back <= n/16 + min(n, bins): the ranges never meet inside
-    // max_chunks (sched_max_chunks).
-    const uint32_t fpk = nfull * kChunkPkts + (tail && lg == 2u ? tail : 0u);
-    const uint32_t cpk = sched_groups(cls) * kChunkPkts;  // packets per front chunk
-    const uint32_t nfront = (fpk + cpk - 1u) / cpk;
-    const bool back = tail && lg != 2u;
-    const bool is_long = back && sched_tail_long(cls, lg);
-    const uint32_t nlong = is_long ? 1u : 0u, nshort = back && !is_long ? 1u : 0u;
-    uint32_t off_p, off_f, off_l, off_s, tot_p, tot_f, tot_l, tot_s;
-    Scan(tmp).ExclusiveSum(c, off_p, tot_p);
-    __syncthreads();
-    Scan(tmp).ExclusiveSum(nfront, off_f, tot_f);
-    __syncthreads();
-    Scan(tmp).ExclusiveSum(nlong, off_l, tot_l);
-    __syncthreads();
-    Scan(tmp).ExclusiveSum(nshort, off_s, tot_s);
-    if (threadIdx.x == 0) {
-        wg_base[0] = tot_p ? atomicAdd(&ws.counters[kCntPackets], tot_p) : 0u;
-        wg_base[1] = tot_f ? atomicAdd(&ws.counters[kCntFrontChunks], tot_f) : 0u;
-        wg_base[2] = tot_l ? atomicAdd(&ws.counters[kCntBackChunks], tot_l) : 0u;
-        wg_base[3] = tot_s ? atomicAdd(&ws.counters[kCntShortChunks], tot_s) : 0u;
-    }
-    __syncthreads();
-    if (c == 0u) return;
-    const uint32_t base = wg_base[0] + off_p;
-    uint32_t sb = base;
-#pragma unroll
-    for (uint32_t j = 0; j < SUB; j++) {
-        ws.base[b * SUB + j] = sb;
-        sb += sc[j];
-    }
-    const uint32_t cf = wg_base[1] + off_f;
-    for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
-        ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));
-    if (back) {
-        const uint4 ch = make_uint4(base + fpk, tail, key, cls | (lg << kChunkLgShift));
-        const uint32_t tl = wg_base[2] + off_l, ts = wg_base[3] + off_s;
-        if (is_long) {
-            if (tl < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - tl] = ch;
-        } else if (ts < ws.max_short) {
-            ws.chunks[ws.max_chunks + ts] = ch;
-        }
-    }
+    __shared__ SchedAllocLds<SUB> sl;
+    sched_alloc_block<SUB>(max_keys, ws, blockIdx.x, sl);
 }
 
-// pass 3: scatter packet indices into their bin's range, at the rank pass 1 drew
 __global__ void sched_scatter_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn, SchedWs ws) {
     if (dn) n = min(n, *dn);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        ws.sorted[ws.base[ws.binof[i]] + ws.binpos[i]] = i;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) sched_scatter_one(ws, i);
 }
 
 // Descriptors of a shard whose engine disagrees with engine 0 on some key slots (engine.cpp

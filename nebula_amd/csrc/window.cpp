@@ -55,8 +55,8 @@ int neb_open_batch_count(neb_engine* e, int alg, const neb_desc* d_desc, uint32_
                          void* prebinned);
 void* neb_sched_space_new();
 void neb_sched_space_free(void* p);
-int neb_prebin(neb_engine* e, const neb_desc* d_desc, uint32_t n, void* sched, hipStream_t aux, hipEvent_t fork,
-               hipEvent_t join);
+int neb_rx_sched_begin(neb_engine* e, uint32_t n, void* sched, hipStream_t s, neb::SchedWs* ws, uint32_t* max_keys);
+void neb_rx_sched_abort(void* sched);
 }
 
 using namespace neb_rx;
@@ -378,10 +378,7 @@ struct neb_dwindows {
     uint8_t* wire_mem = nullptr;  // neb_rx_open_wire_batch: descriptors + gate statuses
     uint32_t wire_n = 0;
     uint32_t spin_limit = neb::kRxSpinLimit;  // neb_dwindows_set_spin_limit
-    // mixed-key AES-GCM receives: the open's binning on a stream of its own, beside the plan
-    hipStream_t aux = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    void* sched = nullptr;
+    void* sched = nullptr;  // mixed-key AES-GCM receives: the open's scheduler workspace (rxwin.hpp RxBin)
 };
 
 namespace {
@@ -480,11 +477,7 @@ NEB_API int neb_dwindows_destroy(neb_dwindows* d) {
         // neb_rx_open_batch returns only once its stream has run the batch, and holds d->mu
         // throughout: with the lock taken, nothing of this window set is in flight
         std::lock_guard<std::mutex> g(d->mu);
-        if (d->aux) hipStreamSynchronize(d->aux);
         if (d->sched) neb_sched_space_free(d->sched);
-        if (d->fork) hipEventDestroy(d->fork);
-        if (d->join) hipEventDestroy(d->join);
-        if (d->aux) hipStreamDestroy(d->aux);
         if (d->ws_mem) hipFree(d->ws_mem);
         if (d->wire_mem) hipFree(d->wire_mem);
         if (d->mem) hipFree(d->mem);
@@ -582,26 +575,25 @@ static int rx_open_batch_locked(neb_engine* e, int alg, neb_dwindows* d, const n
     // Everything is queued at once, one host read at the end: windows whose counters come within
     // 2^62 of wrapping hold all their packets back (admitted by none), and exact_rounds opens what
     // their real pass accepts in batches, like the windows where a tag failed.
-    // 0. mixed-key AES-GCM: the open's binning (sched.hip) reads only the descriptors, so it runs on a
-    //    stream of its own beside the plan (17 µs of three launches off the C3 receive's chain)
+    // 0. mixed-key AES-GCM: the open's binning (sched_body.hpp) reads only the descriptors, so extra
+    //    workgroups of the plan's own launches run it (rxwin.hpp RxBin): three launches off the chain.
+    //    A batch large enough for sub-bins is binned by the open itself.
     void* prebinned = nullptr;
-    if (alg == NEB_ALG_AESGCM && key_hint == NEB_KEYS_MIXED) {
-        if (!d->aux) {
-            RX_HIP(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
-            RX_HIP(hipEventCreateWithFlags(&d->fork, hipEventDisableTiming | hipEventDisableSystemFence));
-            RX_HIP(hipEventCreateWithFlags(&d->join, hipEventDisableTiming | hipEventDisableSystemFence));
-            if (!(d->sched = neb_sched_space_new())) return NEB_ERR_HIP;
-        }
-        RX_HIP(hipEventRecord(d->fork, s));
-        if ((rc = neb_prebin(e, d_desc, n, d->sched, d->aux, d->fork, d->join)) != NEB_OK) return rc;
+    neb::RxBin bin{};
+    if (alg == NEB_ALG_AESGCM && key_hint == NEB_KEYS_MIXED && (int64_t)n < neb::knob(NEB_KNOB_SUB_BINS_FROM)) {
+        if (!d->sched && !(d->sched = neb_sched_space_new())) return NEB_ERR_HIP;
+        if ((rc = neb_rx_sched_begin(e, n, d->sched, s, &bin.ws, &bin.max_keys)) != NEB_OK) return rc;
+        bin.on = 1;
         prebinned = d->sched;
     }
     // 1. group by window, prefix maxima, first occurrences; admission for the safe windows
-    RX_HIP(neb_rxdev_plan(d_desc, n, &v, &ws, d_status, s));
+    if (neb_rxdev_plan(d_desc, n, &v, &ws, d_status, &bin, s) != hipSuccess) {
+        if (prebinned) neb_rx_sched_abort(prebinned);
+        return NEB_ERR_HIP;
+    }
     const auto t1 = now();
     // 2. one open over the batch that runs the admitted packets only (the plan's mask), writing their
     //    statuses at their arrival indices
-    if (prebinned) RX_HIP(hipStreamWaitEvent(s, d->join, 0));
     rc = neb_open_batch_count(e, alg, d_desc, n, nullptr, d_arena, d_status, key_hint, s, ws.adm, prebinned);
     if (rc != NEB_OK) return rc;
     const auto t2 = now();
