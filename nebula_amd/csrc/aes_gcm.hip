@@ -1464,8 +1464,9 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             const GhChunk4 gh{wtab, wpos};
             for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
                 const uint32_t q = g0 + (ln >> 2);
-                const bool valid = q < count;
-                const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+                const uint32_t sp = q < count ? ca.sorted[start + q] : kSortedSkip;
+                const bool valid = sp != kSortedSkip;  // (a device receive's refused packet: skipped)
+                const uint32_t p = valid ? sp : 0u;
                 gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
             }
         } else {
@@ -1475,8 +1476,9 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t q = ln >> lg;
-            const bool valid = q < count;
-            const uint32_t p = valid ? ca.sorted[start + q] : 0u;
+            const uint32_t sp = q < count ? ca.sorted[start + q] : kSortedSkip;
+            const bool valid = sp != kSortedSkip;
+            const uint32_t p = valid ? sp : 0u;
             const GhChunkTree gh{wtab, wpos};
             gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg);
         }

@@ -860,7 +860,8 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         if (err == hipSuccess)  // sp.done bound to the chunk kernel's dispatch: no marker packet between batches
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
                                         sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, e->cu_count,
-                                        s, hdr_from_dst, bind_events() ? sp.done : nullptr, rx);
+                                        s, hdr_from_dst, bind_events() ? sp.done : nullptr,
+                                        prebinned ? nullptr : rx);  // (prebinned: refused packets unlisted)
         if (err == hipSuccess && !bind_events()) err = hipEventRecord(sp.done, s);
         if (err == hipSuccess) sp.last.set(s);
         if (err != hipSuccess) {

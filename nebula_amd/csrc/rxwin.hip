@@ -304,6 +304,13 @@ __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p
     }
 }
 
+// The open's binning, pass 3, as a launch of its own when the sort took one pass (the scan after it
+// rewrites refused packets' places in sorted[], so the scatter cannot run beside it).
+__global__ __launch_bounds__(256) void rx_bin_scatter_kernel(uint32_t n, RxBin bin) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) sched_scatter_one(bin.ws, i);
+}
+
 // (head, max) pairs of the segmented max scan: a head starts a new run
 struct RxSeg {
     uint32_t f;
@@ -340,13 +347,7 @@ __device__ __forceinline__ uint64_t rx_peek(const uint64_t* g) {
 // decided on the host.
 __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_desc* __restrict__ desc, uint32_t n,
                                                                      RxDevWin win, RxDevWs ws,
-                                                                     int32_t* __restrict__ status, uint32_t nscan,
-                                                                     RxBin bin) {
-    if (blockIdx.x >= nscan) {  // the open's binning, pass 3, when the sort took one pass (no ticket)
-        const uint32_t i = (blockIdx.x - nscan) * 256u + threadIdx.x;
-        if (i < n) sched_scatter_one(bin.ws, i);
-        return;
-    }
+                                                                     int32_t* __restrict__ status, RxBin bin) {
     __shared__ uint64_t s_v[kRxThreads / 64];
     __shared__ uint32_t s_f[kRxThreads / 64];
     __shared__ uint64_t s_incl[kRxBlock];
@@ -497,6 +498,9 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
         const uint32_t i = ij[j];
         ws.verdict[i] = NEB_STATUS_OK;
         ws.adm[i] = 0;
+        // the open's binning (RxBin) placed every packet: a packet not admitted leaves its place
+        // empty (kSortedSkip), so the plain chunk kernel skips it with no mask of its own
+        if (bin.on) bin.ws.sorted[bin.ws.base[bin.ws.binof[i]] + bin.ws.binpos[i]] = kSortedSkip;
         if (w >= win.count) {
             status[i] = NEB_STATUS_BAD_KEY;  // no window: no ConnectionState for this index
             continue;
@@ -522,6 +526,7 @@ __global__ __launch_bounds__(kRxThreads) void rx_scan_admit_kernel(const neb_des
         }
         if (ok) {
             ws.adm[i] = 1;  // the open runs it (the admission mask)
+            if (bin.on) bin.ws.sorted[bin.ws.base[bin.ws.binof[i]] + bin.ws.binpos[i]] = i;
         } else {
             status[i] = NEB_STATUS_REPLAY;  // (a slow window's statuses are rewritten on the host)
         }
@@ -762,10 +767,11 @@ extern "C" hipError_t neb_rxdev_plan(const neb_desc* d_desc, uint32_t n, const R
             hipLaunchKernelGGL(neb::rx_sort_pass_kernel<false>, dim3(so.nblk + extra), dim3(256), 0, s, so, p,
                                ws->sort_hist, sk, sv, dk, dv, ws->mixed, ws->gen, ws->run_w, ws->run_i, b);
     }
+    if (bin.on && so.passes == 1)
+        hipLaunchKernelGGL(neb::rx_bin_scatter_kernel, dim3(bin.scatter_blocks), dim3(256), 0, s, n, bin);
     const uint32_t nscan = (n + neb::kRxBlock - 1) / neb::kRxBlock;
-    const uint32_t extra = bin.on && so.passes == 1 ? bin.scatter_blocks : 0u;  // pass 3 here after one sort pass
-    hipLaunchKernelGGL(neb::rx_scan_admit_kernel, dim3(nscan + extra), dim3(neb::kRxThreads), 0, s, d_desc, n, *win,
-                       *ws, d_status, nscan, bin);
+    hipLaunchKernelGGL(neb::rx_scan_admit_kernel, dim3(nscan), dim3(neb::kRxThreads), 0, s, d_desc, n, *win, *ws,
+                       d_status, bin);
     return hipGetLastError();
 }
 

@@ -40,9 +40,10 @@ struct RxDevWin {  // a set of windows of one length in device memory (neb_dwind
 
 // The mixed-key open's binning (sched_body.hpp), run by extra workgroups of the plan's own launches
 // instead of three launches of its own: the histogram beside the keys, the allocation beside the
-// first sort pass, the scatter beside the next launch (the second pass, or the scan when there is
-// one pass). The passes depend only on the descriptors and on each other, so each role waits on
-// nothing inside its launch. on = 0: no binning (one key, ChaCha20-Poly1305, or a batch large
+// first sort pass, the scatter beside the second (a launch of its own after a one-pass sort). The
+// passes depend only on the descriptors and on each other, so each role waits on nothing inside its
+// launch. The scan then marks every packet it did not admit as skipped in sorted[] (kSortedSkip),
+// so the open runs the plain chunk kernel. on = 0: no binning (one key, ChaCha20-Poly1305, or a batch large
 // enough for sub-bins: the open bins it itself).
 struct RxBin {
     SchedWs ws;

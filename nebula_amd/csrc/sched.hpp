@@ -43,6 +43,8 @@ constexpr uint32_t kCntFrontChunks = 1;  // chunks of groups at 4 lanes per pack
 constexpr uint32_t kCntBackChunks = 2;   // long tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
 constexpr uint32_t kCntShortChunks = 3;  // short tails, chunks[max_chunks + j] (sched_tail_long)
 constexpr uint32_t kSchedCounters = 4;
+// sorted[] entry of a packet the crypto kernel must skip (the device receive's refused packets)
+constexpr uint32_t kSortedSkip = 0xFFFFFFFFu;
 
 // Each bin counts its packets in kSubBins sub-bins (sub-bin = the counting workgroup's index mod
 // kSubBins), so the returning atomics of one bin's packets spread over kSubBins words: a 4096-key
