@@ -7,6 +7,7 @@
 //   shr64:   v_lshrrev_b64 (the Poly1305 carries)
 // (each through inline asm, so the compiler neither folds a chain nor picks another instruction)
 //   dpp:     v_mov_b32 with a DPP quad_perm (the quarter-round diagonals)
+//   perm, bitop3, lshl_or, xor, add_dpp+nop: candidates for the rotates and the folded DPP adds
 // Reports wave-instructions per CU per ns and, with the clock the kernel measured itself
 // (s_memtime cycles over s_memrealtime at 100 MHz), cycles per wave-instruction per SIMD.
 //
@@ -56,8 +57,19 @@ __global__ __launch_bounds__(1024, 4) void mix_kernel(uint32_t* out, uint64_t* c
                     asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(q[c]), "=s"(carry) : "v"(a[c]), "v"(b[c]));
                 } else if constexpr (OP == 3) {
                     asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(q[c]));
-                } else {
+                } else if constexpr (OP == 4) {
                     a[c] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[c], 0x39, 0xF, 0xF, false);
+                } else if constexpr (OP == 5) {
+                    asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(a[c]) : "v"(b[c]));
+                } else if constexpr (OP == 6) {
+                    asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(a[c]) : "v"(b[c]));
+                } else if constexpr (OP == 7) {
+                    asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(a[c]) : "v"(b[c]));
+                } else if constexpr (OP == 8) {
+                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[c]) : "v"(b[c]));
+                } else {
+                    asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %0, %1 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf"
+                                 : "+v"(a[c]) : "v"(b[c]));
                 }
             }
         }
@@ -118,5 +130,10 @@ int main() {
     if (run<2>("mad64", blocks, d_out, d_clk, 1)) return 1;
     if (run<3>("shr64", blocks, d_out, d_clk, 1)) return 1;
     if (run<4>("dpp", blocks, d_out, d_clk, 1)) return 1;
+    if (run<5>("perm", blocks, d_out, d_clk, 1)) return 1;
+    if (run<6>("bitop3", blocks, d_out, d_clk, 1)) return 1;
+    if (run<7>("lshl_or", blocks, d_out, d_clk, 1)) return 1;
+    if (run<8>("xor", blocks, d_out, d_clk, 1)) return 1;
+    if (run<9>("add_dpp+nop", blocks, d_out, d_clk, 1)) return 1;
     return 0;
 }
