@@ -140,7 +140,10 @@ enum {
                                    * tests use it to force a partial last pass) */
     NEB_KNOB_RX_STRICT = 3,       /* NEB_RXDEV_STRICT: a device receive whose windows need the sequential host
                                    * finish fails with NEB_ERR_INVALID instead (tests: the parallel form ran) */
-    NEB_KNOB_COUNT = 4
+    NEB_KNOB_TILE_BINS_FROM = 4,  /* NEB_TILE_BINS_FROM: mixed-key batches of at least this many packets bin
+                                   * through per-workgroup LDS histograms (sched.hpp: no per-packet global
+                                   * atomic); smaller ones through the atomic histogram */
+    NEB_KNOB_COUNT = 5
 };
 NEB_API int neb_set_knob(int knob, int64_t value);
 NEB_API int64_t neb_get_knob(int knob); /* -1 for an unknown knob */

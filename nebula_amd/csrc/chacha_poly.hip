@@ -327,8 +327,36 @@ __device__ __forceinline__ void chacha_group(const ChachaArgs& args, uint32_t gr
             }
             return b;
         };
+        // whole-block rounds need dword-aligned AAD, source and destination (load_u4_a4 / store_u4_a4)
+        const bool a4 =
+            (((uintptr_t)(arena + d.src_off) | (uintptr_t)(arena + d.dst_off) | (uintptr_t)(arena + d.aad_off)) & 3u) == 0u;
         // (loading each round's block one round ahead measured 2-3% slower: DESIGN.md §3.3)
         for (uint32_t rho = 0; rho < rmax; rho++) {
+            {
+                // A round in which every lane of the wave holds a whole block — AAD or payload —
+                // or lies before the packet's first block (round 0's lanes below φ): one straight
+                // path, without the length-block, partial-block and header-from-dst cases below.
+                // At 1300 B that is every round but a packet's last.
+                const int32_t i = (int32_t)(16u * rho + l) - (int32_t)phi;
+                const bool is_data = i >= (int32_t)na;
+                const uint32_t off = 16u * ((uint32_t)i - na);
+                const bool ok = rho < nrounds && a4 &&
+                                (i < 0 || (is_data ? off + 16u <= d.len && off >= hdr : 16u * (uint32_t)i + 16u <= d.aad_len));
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) {  // (wave-uniform)
+                    uint4 in = make_uint4(0, 0, 0, 0);
+                    if (i >= 0) in = load_u4_a4(is_data ? arena + d.src_off + off : arena + d.aad_off + 16u * (uint32_t)i);
+                    if (rho > kappa) ks = chacha_quad(kConst[w], ka, kc, w == 0u ? 4u * (rho - kappa) + j : dn, w);
+                    uint4 c = in;
+                    if (is_data) {
+                        const uint4 out = xor4c(in, ks);
+                        store_u4_a4(arena + d.dst_off + off, out);
+                        if (!OPEN) c = out;
+                    }
+                    // lanes before the first block: zero words and no 2^128 bit, so A stays 0
+                    A = p5_add(p5_mul(A, r16), p5_from_words(c.x, c.y, c.z, c.w, i >= 0 ? 1u : 0u));
+                    continue;
+                }
+            }
             if (rho >= nrounds) continue;
             const uint4 blk = fetch(rho);
             if (rho > kappa) ks = chacha_quad(kConst[w], ka, kc, w == 0u ? 4u * (rho - kappa) + j : dn, w);

@@ -81,6 +81,10 @@ __device__ __forceinline__ uint4 load_u4_a4(const uint8_t* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+__device__ __forceinline__ void store_u4_a4(uint8_t* p, uint4 v) {
+    *reinterpret_cast<U4a4*>(p) = U4a4{v.x, v.y, v.z, v.w};
+}
+
 // 16 bytes at any byte address p from the two aligned 16-byte blocks that hold them (never beyond
 // the aligned block of the last byte read, so never into another page).
 __device__ __forceinline__ uint4 load_shifted16(const uint8_t* p) {

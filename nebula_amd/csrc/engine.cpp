@@ -265,6 +265,8 @@ int64_t neb::knob(int k) {
         const char* mg = std::getenv("NEB_SINGLE_MAX_GRID");
         g_knobs[NEB_KNOB_SINGLE_MAX_GRID] = mg ? std::atoll(mg) : 0;
         g_knobs[NEB_KNOB_RX_STRICT] = std::getenv("NEB_RXDEV_STRICT") ? 1 : 0;
+        const char* tb = std::getenv("NEB_TILE_BINS_FROM");
+        g_knobs[NEB_KNOB_TILE_BINS_FROM] = tb ? (int64_t)std::strtoull(tb, nullptr, 10) : (int64_t)neb::kTileBinsFrom;
         return true;
     }();
     (void)init;
@@ -778,8 +780,12 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
         hipError_t err = hipEventCreateWithFlags(&sp.done, hipEventDisableTiming | hipEventDisableSystemFence);
         if (err != hipSuccess) return err;
     }
-    if (n <= sp.n_cap && sp.mem && !sp.dirty) return hipSuccess;
-    if (n <= sp.n_cap && sp.mem) {  // the bins are cleared as they are consumed, except after a failure
+    // the tile binning's arrays (sched.hpp), only for workspaces that see batches that large: a
+    // queue's small batches keep the atomic histogram and need none
+    const bool tiles = (int64_t)n >= neb::knob(NEB_KNOB_TILE_BINS_FROM) || sp.ws.tcnt;
+    const bool fits = n <= sp.n_cap && sp.mem && (!tiles || sp.ws.tcnt);
+    if (fits && !sp.dirty) return hipSuccess;
+    if (fits) {  // the bins are cleared as they are consumed, except after a failure
         hipError_t err = hipEventSynchronize(sp.done);
         if (err == hipSuccess)
             err = hipMemsetAsync(sp.ws.counters, 0, (neb::kSchedCounters + (size_t)neb::kSubBins * neb::sched_nbins(e->max_keys)) * 4u, s);
@@ -792,7 +798,9 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     const size_t b_counters = align_up((neb::kSchedCounters + (size_t)neb::kSubBins * nb) * 4u, 256);
     const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
     const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up(((size_t)mc + ms) * 16u, 256);
-    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks;
+    const size_t b_tcnt = tiles ? align_up((size_t)neb::kTileMax * neb::sched_tile_words(nb) * 4u, 256) : 0;
+    const size_t b_tpre = tiles ? align_up((size_t)neb::kTileMax * nb * 4u, 256) : 0;
+    const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_tcnt + b_tpre;
     hipError_t err = hipEventSynchronize(sp.done);  // the old buffer may still be in use
     if (err != hipSuccess) return err;
     if (sp.mem) hipFree(sp.mem);
@@ -813,6 +821,10 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     sp.ws.sorted = (uint32_t*)m;
     m += b_idx;
     sp.ws.chunks = (uint4*)m;
+    m += b_chunks;
+    sp.ws.tcnt = tiles ? (uint32_t*)m : nullptr;
+    m += b_tcnt;
+    sp.ws.tpre = tiles ? (uint32_t*)m : nullptr;
     sp.ws.max_chunks = mc;
     sp.ws.max_short = ms;
     sp.bytes = bytes;

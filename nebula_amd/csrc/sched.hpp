@@ -62,6 +62,24 @@ constexpr uint32_t kSubBins = NEB_SUB_BINS;
 constexpr uint32_t kSubBinsFrom = NEB_SUB_BINS_FROM;
 static_assert(kSubBins == 1 || kSubBins == 2 || kSubBins == 4 || kSubBins == 8, "sub-bins: a power of two <= 8");
 
+// Large batches bin without a global atomic per packet (round 5; the histogram pass was bound by
+// the memory-side atomic rate, ≈ 23 G returning adds/s chip-wide whatever their scope or spread,
+// tools/micro/xcd_atomic.hip): the batch is cut into T ≤ kTileMax tiles of ≤ 65535 packets, one
+// 1024-thread workgroup per tile counts its packets per bin in LDS (two 16-bit counts per word,
+// the LDS add's return is the packet's rank within the tile), a scan over the tiles gives each
+// (tile, bin) its offset inside the bin and each bin its count, the allocation pass runs as for
+// one sub-bin, and the scatter puts packet i at base[bin] + tile offset + rank.
+constexpr uint32_t kTileMax = 128;       // tiles (workgroups of the counting pass)
+constexpr uint32_t kTileMinPkts = 1024;  // packets per tile at least
+constexpr uint32_t kTileThreads = 1024;
+constexpr uint32_t kTileLdsMax = 152u * 1024u;  // the counting pass's LDS budget (160 KiB per CU)
+#ifndef NEB_TILE_BINS_FROM
+#define NEB_TILE_BINS_FROM (1u << 18)
+#endif
+constexpr uint32_t kTileBinsFrom = NEB_TILE_BINS_FROM;
+// 16-bit counts, two per word; rows padded to 16 words (the scan takes 16 words per workgroup)
+__host__ __device__ inline uint32_t sched_tile_words(uint32_t nbins) { return ((nbins + 1u) / 2u + 15u) & ~15u; }
+
 struct SchedWs {          // device workspace, sized for n packets and nbins bins
     uint32_t* counters;   // [kSchedCounters] counters, then hist[nbins * kSubBins]
     uint32_t* hist;       // [bin * kSubBins + sub] packets counted
@@ -72,6 +90,8 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
     uint4* chunks;        // [max_chunks + max_short] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
     uint32_t max_chunks;  // fronts from 0 up, long tails from max_chunks - 1 down
     uint32_t max_short;   // short tails from max_chunks up
+    uint32_t* tcnt;       // [kTileMax][sched_tile_words] per-tile bin counts, 16 bits each (null: no tiles)
+    uint32_t* tpre;       // [kTileMax][nbins] each (tile, bin)'s offset inside its bin
 };
 
 __host__ __device__ inline uint32_t sched_nbins(uint32_t max_keys) { return kSizeClasses * (max_keys + 1u); }

@@ -132,7 +132,7 @@ def test_knobs_set_get_and_defaults():
     assert lib.neb_set_knob(99, 1) == L.ERR_INVALID
     if "NEB_SUB_BINS_FROM" not in os.environ:
         assert lib.neb_get_knob(L.KNOB_SUB_BINS_FROM) == 1 << 18
-    for k in (L.KNOB_HOST_MODE, L.KNOB_SUB_BINS_FROM, L.KNOB_SINGLE_MAX_GRID, L.KNOB_RX_STRICT):
+    for k in (L.KNOB_HOST_MODE, L.KNOB_SUB_BINS_FROM, L.KNOB_SINGLE_MAX_GRID, L.KNOB_RX_STRICT, L.KNOB_TILE_BINS_FROM):
         old = lib.neb_get_knob(k)
         with L.knob(k, 12345):
             assert lib.neb_get_knob(k) == 12345

@@ -118,9 +118,12 @@ def test_mixed_key_density_vs_oracle(engine, oracle_mod, alg, n, nkeys, sizes, r
     assert np.array_equal(got_o, ref_o)
 
 
-# both counting layouts of the mixed-key scheduler (sched.hip), forced by its per-batch knob: one
-# count word per bin, or kSubBins
-BINNING = {"one_word": 4000000000, "subbins": 0}
+# the three counting layouts of the mixed-key scheduler (sched.hip), forced by its per-batch knobs
+# (NEB_KNOB_SUB_BINS_FROM, NEB_KNOB_TILE_BINS_FROM): one count word per bin, kSubBins words, or the
+# per-tile LDS histograms with a scan over the tiles (4-21 tiles here; the engine's 8192 key slots
+# make the 65 544-bin, 128 KiB-LDS case)
+NEVER = 4000000000
+BINNING = {"one_word": (NEVER, NEVER), "subbins": (0, NEVER), "tiles": (NEVER, 0)}
 
 
 @pytest.mark.parametrize("path", sorted(BINNING))
@@ -131,7 +134,8 @@ BINNING = {"one_word": 4000000000, "subbins": 0}
     (21000, 1000, (90, 576, 1300), (7, 4, 1)),
 ])
 def test_binning_paths_vs_oracle(engine, oracle_mod, knobs, path, n, nkeys, sizes, ratio):
-    knobs(L.KNOB_SUB_BINS_FROM, BINNING[path])
+    knobs(L.KNOB_SUB_BINS_FROM, BINNING[path][0])
+    knobs(L.KNOB_TILE_BINS_FROM, BINNING[path][1])
     b = W.make_batch(L.ALG_AESGCM, n, nkeys, sizes=sizes, ratio=ratio, seed=n ^ nkeys ^ 0x5EED, name="binning")
     ref, st_ref = oracle_seal(oracle_mod, b)
     for rep in range(2):  # twice: each path leaves its counters and bins clear for the next batch
@@ -142,6 +146,31 @@ def test_binning_paths_vs_oracle(engine, oracle_mod, knobs, path, n, nkeys, size
     got_o, st_o = run_device(engine, b, seal=False, arena=ref)
     assert (st_o == 0).all()
     assert np.array_equal(got_o, ref_o)
+
+
+@pytest.mark.parametrize("max_keys", [1024, 4096])
+def test_tile_binning_lds_rows_vs_oracle(oracle_mod, knobs, max_keys):
+    """The tile binning's scatter with each tile's row of bin offsets in LDS (sched.hip), which the
+    shared 8192-slot engine's 65 544 bins do not fit: engines with 1024 and 4096 key slots (8200 /
+    32 776 bins), an IMIX batch over 1000 keys in 21 tiles, seal twice and open."""
+    from nebula_amd import Engine
+
+    knobs(L.KNOB_TILE_BINS_FROM, 0)
+    e = Engine(0, max_keys=max_keys)
+    try:
+        b = W.make_batch(L.ALG_AESGCM, 21000, 1000, sizes=(90, 576, 1300), ratio=(7, 4, 1), seed=0x711E5,
+                         name="tiles")
+        ref, st_ref = oracle_seal(oracle_mod, b)
+        for rep in range(2):
+            got, st = run_device(e, b, seal=True)
+            assert (st == 0).all() and (st_ref == 0).all()
+            assert np.array_equal(got, ref)
+        ref_o, _ = oracle_open(oracle_mod, b, ref)
+        got_o, st_o = run_device(e, b, seal=False, arena=ref)
+        assert (st_o == 0).all()
+        assert np.array_equal(got_o, ref_o)
+    finally:
+        e.close()
 
 
 def _edge_batch(alg, lens, alens, nkeys=3, seed=99):

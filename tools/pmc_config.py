@@ -9,7 +9,10 @@ pmc_lds.json, trace_kernel_stats.csv) it takes, for the config's dominant kernel
                          2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes; MI355X_MICROARCH.md §HBM: on
                          gfx950 FETCH_SIZE reports half the bytes of 16 B/lane streaming reads)
   lds_busy  = SQ_LDS_IDX_ACTIVE / SQ_BUSY_CU_CYCLES
-  valu_busy = SQ_INSTS_VALU x 2 cycles per wave64 op / 4 SIMDs per CU, over the CU-busy cycles
+  valu_busy = VALU issue cycles per SIMD over the CU-busy cycles: a wave64 VALU instruction takes
+              one quad-cycle (4 cycles), two VOP1/VOP2 of two waves share one (SQ_ACTIVE_INST_VALU2
+              counts the second), so 4 x (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / 4 SIMDs per CU
+              (tools/valu_issue.py); passes without VALU2 count no co-issue
   mean_ns   = the kernel's rocprof mean duration (the same passes' kernel trace)
 usage: python tools/pmc_config.py CONFIG KERNEL_SUBSTRING profiles/<tag> [profiles/<tag with the lds pass>]
    e.g. python tools/pmc_config.py C3 "gcm_chunk_kernel<false>" profiles/r3q_c3 profiles/r3_c3
@@ -19,7 +22,7 @@ import json
 import os
 import sys
 
-CUS, SIMDS_PER_CU, VALU_CYCLES = 256, 4, 2
+CUS, SIMDS_PER_CU, VALU_CYCLES = 256, 4, 4
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
@@ -58,7 +61,9 @@ def main():
         lds = pick(load("lds", lds_tag), sub)
         busy = lds["SQ_BUSY_CU_CYCLES"]
         ent["lds_busy"] = round(lds["SQ_LDS_IDX_ACTIVE"] / busy, 3)
-        ent["valu_busy"] = round(lds["SQ_INSTS_VALU"] / (CUS * SIMDS_PER_CU) * VALU_CYCLES / (busy / CUS), 3)
+        issued = lds["SQ_INSTS_VALU"] - lds.get("SQ_ACTIVE_INST_VALU2", 0.0)
+        ent["valu_busy"] = round(issued / (CUS * SIMDS_PER_CU) * VALU_CYCLES / (busy / CUS), 3)
+        ent["valu_coissue_counted"] = "SQ_ACTIVE_INST_VALU2" in lds
     except (OSError, KeyError, SystemExit):
         pass
     stats = os.path.join(tag, "trace_kernel_stats.csv")
