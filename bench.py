@@ -530,17 +530,18 @@ def whole_seal_ms(db, stream, reps: int = 4) -> float:
 def hbm_over_ranks(ctrl, world: int, alg_bytes: float, seal_ms: float, ndev: int) -> dict:
     """Every rank's seal-kernel bandwidth (algorithmic bytes / its own kernel time) over the ranks:
     per GPU min / mean / max and fraction of one GPU's HBM peak, and the whole job's sum against
-    N x the peak. devices: the distinct GPUs the ranks ran on (fewer than N only in a rehearsal
-    that shares a device)."""
+    the peak of the distinct GPUs the ranks ran on (`devices`: N on a node, fewer only in a
+    rehearsal that shares a device, whose ranks then split one GPU's HBM)."""
     ach = alg_bytes / (seal_ms * 1e-3) / 1e9
     tot = ctrl.sum(ach)
     lo, hi = -ctrl.max(-ach), ctrl.max(ach)
     mean = tot / world
+    dev = min(world, max(ndev, 1))
     return {
         "per_gpu": {"achieved_min": round(lo, 2), "achieved_mean": round(mean, 2), "achieved_max": round(hi, 2),
                     "frac_mean": round(mean / HBM_PEAK_GBS, 4), "ranks": world},
-        "aggregate": {"achieved": round(tot, 2), "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
-                      "frac": round(tot / (HBM_PEAK_GBS * world), 4), "devices": min(world, max(ndev, 1))},
+        "aggregate": {"achieved": round(tot, 2), "peak": HBM_PEAK_GBS * dev, "unit": "GB/s",
+                      "frac": round(tot / (HBM_PEAK_GBS * dev), 4), "devices": dev},
     }
 
 
@@ -555,7 +556,7 @@ def bench_stub(args, rank: int, world: int):
     ctrl.barrier()
     dt = ctrl.max(0.001 * (rank + 1))
     total = ctrl.sum(1.0 * GIB)
-    multi = hbm_over_ranks(ctrl, world, 1e8, 0.1 * (rank + 1), 0)
+    multi = hbm_over_ranks(ctrl, world, 1e8, 0.1 * (rank + 1), world)  # (as if one GPU each)
     if rank == 0:
         print(json.dumps({"metric": "stub", "value": total / dt / GIB, "unit": "GiB/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3,
