@@ -9,6 +9,9 @@
 //   K5  K0 at 1 wave per SIMD (4 per CU)
 //   K6  add, xor, rotate of one quarter-round step on 4 chains (the lane layout's pattern)
 //   K7  K6 with the 4 chains' adds and xors interleaved with 4 more chains' (8 chains)
+//   K8  v_mov_b32_sdwa writing one byte of its destination (an LDS address byte), 8 chains
+//   K9  K8's SDWA moves alternating with v_xor_b32 (VOP2), 8 chains
+//   K10 v_perm_b32 (the T-table lookup address the kernels build today), 8 chains
 // build: hipcc --offload-arch=gfx950 -O3 -o valu_pair valu_pair.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,10 +31,13 @@ constexpr int kIters = 4000;
 #define ADD(a, b) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a) : "v"(b))
 #define XOR(a, b) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b))
 #define ROT(a) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(a))
+#define SDWA(a, b) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a) : "v"(b))
+#define PERM(a, b, sel) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(a) : "v"(b), "v"(sel))
 
 template <int K>
 __global__ __launch_bounds__(1024) void pair_kernel(uint32_t* out, uint32_t seed) {
     uint32_t a[8], b[8];
+    const uint32_t sel = 0x0c020500u ^ (seed & 0x01000000u);  // (a register operand: no literal in VOP3 here)
 #pragma unroll
     for (int c = 0; c < 8; c++) {
         a[c] = seed ^ (threadIdx.x * 2654435761u) ^ c;
@@ -79,6 +85,24 @@ __global__ __launch_bounds__(1024) void pair_kernel(uint32_t* out, uint32_t seed
 #pragma unroll
                 for (int c = 0; c < 4; c++) ROT(b[c]);
             }
+        } else if constexpr (K == 8) {
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int c = 0; c < 8; c++) SDWA(a[c], b[c]);
+        } else if constexpr (K == 9) {
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    SDWA(a[c], b[c]);
+                    XOR(b[c + 4], a[c + 4]);
+                }
+        } else if constexpr (K == 10) {
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int c = 0; c < 8; c++) PERM(a[c], b[c], sel);
         } else {
 #pragma unroll
             for (int c = 0; c < 4; c++) { ADD(a[c], b[c]); ADD(a[c + 4], b[c + 4]); }
@@ -121,7 +145,8 @@ int main() {
     const int b = cus * 2;  // 16 waves per CU at a time
     if (run<0>(b, 1024, d_out, cus) || run<1>(b, 1024, d_out, cus) || run<2>(b, 1024, d_out, cus) ||
         run<3>(b, 1024, d_out, cus) || run<4>(b, 1024, d_out, cus) || run<5>(cus, 256, d_out, cus) ||
-        run<6>(b, 1024, d_out, cus) || run<7>(b, 1024, d_out, cus))
+        run<6>(b, 1024, d_out, cus) || run<7>(b, 1024, d_out, cus) || run<8>(b, 1024, d_out, cus) ||
+        run<9>(b, 1024, d_out, cus) || run<10>(b, 1024, d_out, cus))
         return 1;
     return 0;
 }
