@@ -3,6 +3,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "knobs.hpp"
@@ -164,6 +165,23 @@ extern "C" hipError_t neb_fence_keys(const neb_desc* in, neb_desc* out, uint32_t
     return hipGetLastError();
 }
 
+// The counting pass's LDS above the default 64 KiB, asked for once per device (an engine per GPU
+// in one process); a device that refuses it bins through the atomic histogram.
+static bool tile_lds_granted() {
+    constexpr int kMaxDevices = 64;
+    static std::atomic<int> state[kMaxDevices];  // 0 not asked, 1 granted, -1 refused
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return false;
+    int st = state[dev].load(std::memory_order_relaxed);
+    if (st == 0) {
+        st = hipFuncSetAttribute((const void*)neb::sched_tile_hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)neb::kTileLdsMax) == hipSuccess ? 1 : -1;
+        if (st < 0) (void)hipGetLastError();  // (not the batch's error: it bins the other way)
+        state[dev].store(st, std::memory_order_relaxed);
+    }
+    return st > 0;
+}
+
 extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const uint32_t* d_n, uint32_t max_keys,
                                       uint32_t lpp, const neb::SchedWs* ws, hipStream_t s) {
     const uint32_t nb = neb::sched_nbins(max_keys);
@@ -176,12 +194,8 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     const uint32_t words = neb::sched_tile_words(nb);
     const uint32_t T = std::min<uint32_t>(neb::kTileMax, (n + neb::kTileMinPkts - 1) / neb::kTileMinPkts);
     const uint32_t P = T ? ((n + T - 1) / T + 255u) & ~255u : 0u;  // (whole workgroups of the scatter)
-    // (the counting pass's LDS above the default 64 KiB: granted once per process, else atomics)
-    static const bool tile_lds = hipFuncSetAttribute((const void*)neb::sched_tile_hist_kernel,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)neb::kTileLdsMax) == hipSuccess;
-    if (n && ws->tcnt && tile_lds && (int64_t)n >= neb::knob(NEB_KNOB_TILE_BINS_FROM) && words * 4u <= neb::kTileLdsMax &&
-        P <= 0xFFFFu) {
+    if (n && ws->tcnt && (int64_t)n >= neb::knob(NEB_KNOB_TILE_BINS_FROM) && words * 4u <= neb::kTileLdsMax &&
+        P <= 0xFFFFu && tile_lds_granted()) {
         hipLaunchKernelGGL(neb::sched_tile_hist_kernel, dim3(T), dim3(neb::kTileThreads), words * 4u, s, d_desc, n, d_n,
                            max_keys, lpp, *ws, P, words);
         hipLaunchKernelGGL(neb::sched_tile_scan_kernel, dim3(words / 16u), dim3(256), 0, s, *ws, T, words, nb);
