@@ -4,7 +4,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r5_chfast; mkdir -p $OUT
 cd $R
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu -k "chacha or ChaCha or CHACHA" \
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
     tests/test_gpu_parity.py tests/test_gpu_cipher_state.py tests/test_gpu_rx.py tests/test_gpu_tx.py tests/test_gpu_queue.py \
     > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -3 $OUT/tests.log
