@@ -104,6 +104,21 @@ def test_bench_bare_gpus2_starts_two_ranks():
     assert ag["achieved"] == pytest.approx(1500.0) and ag["frac"] == pytest.approx(1500.0 / 16000.0, abs=1e-4)
 
 
+def test_bench_bare_gpus4_starts_four_ranks():
+    """The self-launch at world size 4 (the driver's 1-2-4-8 sweep, a stub worker per rank): n_gpus 4,
+    the slowest rank's time, every rank's bytes and kernel bandwidth in the per-GPU min / max and the
+    aggregate over 4 devices."""
+    rc, res, err = _run_bench(["--gpus", "4", "--stub", "--steps", "2", "--warmup", "1"])
+    assert rc == 0, err
+    assert res["n_gpus"] == 4 and "4 rank processes" in res["launcher"]
+    assert res["ms_per_step"] == pytest.approx(4.0)             # max over ranks: rank 3's 4 ms
+    assert res["value"] == pytest.approx(4.0 / 0.004)           # 4 x 1 GiB over 4 ms
+    pg, ag = res["roofline"]["per_gpu"], res["roofline"]["aggregate"]
+    assert pg["ranks"] == 4 and pg["achieved_max"] == pytest.approx(1000.0) and pg["achieved_min"] == pytest.approx(250.0)
+    assert ag["devices"] == 4 and ag["peak"] == pytest.approx(32000.0)
+    assert ag["achieved"] == pytest.approx(1000.0 + 500.0 + 1000.0 / 3 + 250.0, abs=0.01)  # (rounded to 0.01)
+
+
 def test_bench_under_launcher_env_runs_one_rank_per_process():
     """Under a launcher (WORLD_SIZE already set) bench.py is one rank and does not spawn; a lone
     rank with WORLD_SIZE=1 and --gpus 1 prints its own line."""
