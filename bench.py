@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — device-resident AES-256-GCM seal+open throughput (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..4] [--mode device|host]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--settle-ms MS] [--config 1..4] [--mode device|host]
 
 One step = seal every packet of the batch, then open every packet of it (in place, on device),
 i.e. one pass of the hot path (inside.go seal + outside.go open) over one 64 Ki x 1300 B batch.
@@ -11,6 +11,10 @@ Launched by torch.distributed.run, or, when no launcher set WORLD_SIZE, by this 
 starts the N rank processes with the same environment torchrun gives them and relays rank 0's line,
 so `python bench.py --gpus 8` and the torchrun form measure the same thing (spawn_ranks).
 Timing is bracketed by a barrier + device sync on both sides and the max over ranks is taken.
+Before the W warmup steps the device modes settle (--settle-ms, default 300): untimed steps of the
+same work until that much wall time has passed, so the GPU runs at the clocks a sustained load
+holds (an idle MI355X needs a few hundred ms of load; the line's `settle` reports it, and
+--settle-ms 0 measures from a cold start).
 
 Printed (rank 0, one JSON line): value = (payload sealed + payload opened, all ranks) / time.
 roofline: the seal kernel's algorithmic bytes (2p+32 per packet) / its mean launch time, from HIP
@@ -41,6 +45,26 @@ EV_EVERY = 4  # kernel-timing events bracket every 4th step (see the timed loop)
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def settle(args, step) -> dict:
+    """An idle MI355X takes a few hundred ms of load to reach the clocks a sustained load holds:
+    after the 5 default warmup steps of C2 (1.2 ms) the seal kernel ran 115-122 µs, against 95-98
+    µs at steady state (profiles/r5/settle). Before the W warmup steps, untimed,
+    `step` (the mode's own work) repeats until --settle-ms of wall time has passed, synchronised
+    every 16 steps so the host does not run ahead of the device. The line reports it."""
+    import torch
+
+    n = 0
+    if args.settle_ms > 0:
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < args.settle_ms:
+            step()
+            n += 1
+            if n % 16 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+    return {"ms": args.settle_ms, "steps": n}
 
 
 class TimingEvent:
@@ -288,6 +312,10 @@ def main():
                          "(TSO superpackets -> sealed wire packets); rx: batched receive with replay windows; "
                          "rx-device: the same with the batch and the windows in device memory; relay: GMAC-only "
                          "seal+verify of 1348-B relayed packets (VerifyRelay), device-resident")
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="device mode: before the W warmup steps, untimed seal+open steps until this much wall "
+                         "time has passed, so the GPU runs at the clocks a sustained load holds (0: none; "
+                         "reported as `settle` in the line)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inproc", action="store_true",
                     help="device mode, --gpus N engines in ONE process (Nebula is one process): each engine its "
@@ -399,6 +427,7 @@ def main():
     torch.cuda.synchronize()
     assert (db.status_host() == 0).all(), "round trip failed before timing"
 
+    settled = settle(args, lambda: (db.seal(), db.open()))
     for _ in range(args.warmup):
         db.seal()
         db.open()
@@ -469,6 +498,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": settled,  # untimed, before the warmup (settle())
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
         # C5 is one 1 Mi-packet batch split over the GPUs (BASELINE.json "sharded over 8xMI355X"):
@@ -613,6 +643,7 @@ def bench_inproc(args):
 
     step()
     assert all((db.status_host() == 0).all() for db in dbs)
+    settled = settle(args, step)
     for _ in range(args.warmup):
         step()
     t0 = time.perf_counter()
@@ -624,7 +655,8 @@ def bench_inproc(args):
     print(json.dumps({
         "metric": f"GiB/s device-resident seal+open, {m} engine(s) in one process (config {cfg + 1})",
         "value": round(2 * payload * args.steps / dt / GIB, 3), "unit": "GiB/s", "n_gpus": min(m, ndev),
-        "engines": m, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "engines": m, "steps": args.steps, "warmup": args.warmup, "settle": settled,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"C{cfg + 1} per engine, {m} engine(s) over {ndev} visible device(s), one process, "
                                "neb_*_batch_sharded (no collective)"},
@@ -657,6 +689,7 @@ def bench_relay(args, ctrl, rank, world, device):
     db.open()
     torch.cuda.synchronize()
     assert (db.status_host() == 0).all(), "relay round trip failed before timing"
+    settled = settle(args, lambda: (db.seal(), db.open()))
     for _ in range(args.warmup):
         db.seal()
         db.open()
@@ -675,7 +708,8 @@ def bench_relay(args, ctrl, rank, world, device):
             "metric": "GiB/s relay AD (" + ("Poly1305-only ChaCha20-Poly1305" if alg == L.ALG_CHACHAPOLY else
                                            "GMAC-only AES-256-GCM") + " seal + VerifyRelay), device-resident",
             "value": round(2 * ad * args.steps * world / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "settle": settled,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "dtype": "u8", "data": "synthetic",
             "config": {"workload": f"65536 relayed packets, AD 1348 B, empty plaintext, {nkeys} key(s)"},
         }), flush=True)
@@ -726,6 +760,7 @@ def bench_tx(args, eng, ctrl, rank, world):
     torch.cuda.synchronize()
     r = db.result()
     assert len(r.wires) == nwire and (r.wire_status == 0).all() and (r.packet_status == 0).all()
+    settled = settle(args, db.seal)
     for _ in range(args.warmup):
         db.seal()
     torch.cuda.synchronize()
@@ -741,8 +776,8 @@ def bench_tx(args, eng, ctrl, rank, world):
             "metric": "GiB/s TUN bytes in, device TX batch (TSO 64 KiB superpackets -> segment + checksum + "
                       "header + AES-256-GCM seal)",
             "value": round(tun_bytes / dt / GIB, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "dtype": "u8", "data": "synthetic",
+            "warmup": args.warmup, "settle": settled, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "dtype": "u8", "data": "synthetic",
             "wire_packets_per_s": round(nwire * args.steps * world / dt, 1),
             "config": {"workload": f"{nsp} IPv4/TCP TSO superpackets x {per} segments of {mss} B "
                                    f"({nwire} wire packets), 1 tunnel, device-resident"},
@@ -785,7 +820,7 @@ def bench_rx(args, eng, b, ciphers, ctrl, rank, world):
         print(json.dumps({
             "metric": "GiB/s host-resident batched receive (replay window Check -> GPU open -> Update)",
             "value": round(payload / times["rx"] / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
-            "warmup": args.warmup, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+            "warmup": args.warmup, "settle": settled, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
             "open_only_gibs": round(payload / times["open"] / GIB, 3),
             "config": {"workload": f"{b.name}: {b.n} packets, {b.nkeys} tunnel(s), host pinned arena"},
         }), flush=True)
@@ -810,6 +845,7 @@ def bench_rx_device(args, eng, b, ciphers, ctrl, rank, world):
         w.Update(1)
         w.Update(2)
         dw.load(c.key_id, w)
+    settled = settle(args, lambda: (db.seal(), db.open()))
     times = {"rx": 0.0, "open": 0.0}
     for it in range(args.warmup + args.steps):
         d = base.copy()
@@ -837,7 +873,7 @@ def bench_rx_device(args, eng, b, ciphers, ctrl, rank, world):
         print(json.dumps({
             "metric": "GiB/s device-resident batched receive (replay windows in HBM: Check -> open -> Update)",
             "value": round(payload / times["rx"] / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
-            "warmup": args.warmup, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+            "warmup": args.warmup, "settle": settled, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
             "ms_per_step": round(times["rx"] / args.steps * 1e3, 4),
             "open_only_gibs": round(payload / times["open"] / GIB, 3),
             "open_only_ms": round(times["open"] / args.steps * 1e3, 4),
