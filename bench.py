@@ -820,7 +820,7 @@ def bench_rx(args, eng, b, ciphers, ctrl, rank, world):
         print(json.dumps({
             "metric": "GiB/s host-resident batched receive (replay window Check -> GPU open -> Update)",
             "value": round(payload / times["rx"] / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
-            "warmup": args.warmup, "settle": settled, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+            "warmup": args.warmup, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
             "open_only_gibs": round(payload / times["open"] / GIB, 3),
             "config": {"workload": f"{b.name}: {b.n} packets, {b.nkeys} tunnel(s), host pinned arena"},
         }), flush=True)
