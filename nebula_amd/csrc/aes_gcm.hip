@@ -132,16 +132,36 @@ __device__ __forceinline__ uint2 ttab_entry(uint32_t i) {  // i = x*32 + c
     return (i & 16u) ? make_uint2(t2, t) : make_uint2(t, t2);
 }
 
+// Wave priority while a round's 16 lookups are issued (s_setprio): the SIMD arbiter then prefers
+// the wave that feeds the LDS over waves busy with their XOR phase, which keeps the LDS queue
+// full. Measured on C2: 0.150 -> 0.136 ms per seal launch (priority 1, 2 and 3 alike; raising it
+// for the GHASH lookups as well was slower). NEB_PRIO=0 disables it.
+#ifndef NEB_PRIO
+#define NEB_PRIO 3
+#endif
+#ifndef NEB_PRIO_AGE  // gcm_single_kernel: the younger half of each SIMD's waves at 1 between lookups
+#define NEB_PRIO_AGE 1
+#endif
+
 struct RkRegs {  // wave-uniform round keys (scalar registers)
     const uint32_t* k;
     static constexpr bool kUniform = true;
+    // s_setprio levels around a round's lookups (kPrioHi) and after them (kPrioLo)
+    static constexpr int kPrioHi = NEB_PRIO, kPrioLo = 0;
     __device__ __forceinline__ uint4 get(int r) const {
         return make_uint4(k[4 * r], k[4 * r + 1], k[4 * r + 2], k[4 * r + 3]);
     }
 };
+// The same keys with the priority levels of one age rank (gcm_single_kernel: the SIMD arbiter
+// prefers a SIMD's older waves at equal priority, §3.1)
+template <int HI, int LO>
+struct RkRegsPrio : RkRegs {
+    static constexpr int kPrioHi = HI, kPrioLo = LO;
+};
 struct RkLds {  // per-packet round keys staged in LDS
     const uint4* base;
     static constexpr bool kUniform = false;
+    static constexpr int kPrioHi = NEB_PRIO, kPrioLo = 0;
     __device__ __forceinline__ uint4 get(int r) const { return base[r]; }
 };
 
@@ -209,14 +229,6 @@ struct TLook4 {
     static constexpr bool kFour = true;
 };
 
-// Wave priority while a round's 16 lookups are issued (s_setprio): the SIMD arbiter then prefers
-// the wave that feeds the LDS over waves busy with their XOR phase, which keeps the LDS queue
-// full. Measured on C2: 0.150 -> 0.136 ms per seal launch (priority 1, 2 and 3 alike; raising it
-// for the GHASH lookups as well was slower). NEB_PRIO=0 disables it.
-#ifndef NEB_PRIO
-#define NEB_PRIO 3
-#endif
-
 // AES-256 rounds FIRST..13 (full) and 14 (final) on the state s0..s3 (after round FIRST-1).
 template <int FIRST, class TL, class RK>
 __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, const TL& T,
@@ -227,7 +239,7 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
         k = rk.get(r);
 #if NEB_PRIO
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(NEB_PRIO);
+        __builtin_amdgcn_s_setprio(RK::kPrioHi);
 #endif
         const uint32_t a0 = T.t0(s0, 0), a1 = T.t1r(s1, 1), a2 = T.t2(s2, 2), a3 = T.t3r(s3, 3);
         const uint32_t b0 = T.t0(s1, 0), b1 = T.t1r(s2, 1), b2 = T.t2(s3, 2), b3 = T.t3r(s0, 3);
@@ -235,7 +247,7 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
         const uint32_t d0 = T.t0(s3, 0), d1 = T.t1r(s0, 1), d2 = T.t2(s1, 2), d3 = T.t3r(s2, 3);
 #if NEB_PRIO
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(RK::kPrioLo);
 #endif
         // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k; with two tables T1 = rotl8 T0, T3 = rotl8 T2
         if constexpr (TL::kFour) {
@@ -266,7 +278,7 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
     // last round: SubBytes+ShiftRows; S[x] is byte 1 of T0[x]
 #if NEB_PRIO
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(NEB_PRIO);
+    __builtin_amdgcn_s_setprio(RK::kPrioHi);
 #endif
     const uint32_t a0 = T.t0(s0, 0), a1 = T.t0(s1, 1), a2 = T.t0(s2, 2), a3 = T.t0(s3, 3);
     const uint32_t b0 = T.t0(s1, 0), b1 = T.t0(s2, 1), b2 = T.t0(s3, 2), b3 = T.t0(s0, 3);
@@ -274,7 +286,7 @@ __device__ __forceinline__ uint4 aes256_rounds(uint32_t s0, uint32_t s1, uint32_
     const uint32_t d0 = T.t0(s3, 0), d1 = T.t0(s0, 1), d2 = T.t0(s1, 2), d3 = T.t0(s2, 3);
 #if NEB_PRIO
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(RK::kPrioLo);
 #endif
     uint4 o;
     if constexpr (RK::kUniform) {
@@ -936,9 +948,9 @@ __device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uin
 // own (optional): the packet's descriptor itself, not args.desc[p] (the per-packet kernel's, rebased).
 // RX: the device receive's open (args.adm), an instantiation of its own so the plain opens keep their
 // registers.
-template <bool OPEN, bool CS = false, bool RX = false, class GH, class TL>
+template <bool OPEN, bool CS = false, bool RX = false, class GH, class TL, class RK>
 __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p, bool valid, uint32_t expect_key,
-                                                 bool key_ok, const RkRegs& rk, const GH& gh, const TL& T,
+                                                 bool key_ok, const RK& rk, const GH& gh, const TL& T,
                                                  uint32_t lane, uint32_t lg, const uint4* cs_pow = nullptr,
                                                  const neb_desc* own = nullptr) {
     const uint32_t LPP = 1u << lg;
@@ -1171,17 +1183,32 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
     uint32_t trace_k = 1;
     wave_trace(lane, 0, blockIdx.x << 20 | wave << 16, ~0u, tk0, __builtin_amdgcn_s_memrealtime());
 #endif
-    for (uint32_t grp = blockIdx.x + wave * gridDim.x; grp < main_groups; grp += slots) {
+    auto groups = [&](const auto& rkp) {
+        for (uint32_t grp = blockIdx.x + wave * gridDim.x; grp < main_groups; grp += slots) {
 #ifdef NEB_WAVE_TRACE
-        const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        const uint32_t p = grp * kPpw + lane / kLpp;
-        gcm_packet_group<OPEN, CS, RX>(args, p, p < npkt, args.key_hint, key_ok, rk, gh, T, lane, kLg, cs_pow);
+            const uint32_t p = grp * kPpw + lane / kLpp;
+            gcm_packet_group<OPEN, CS, RX>(args, p, p < npkt, args.key_hint, key_ok, rkp, gh, T, lane, kLg, cs_pow);
 #ifdef NEB_WAVE_TRACE
-        wave_trace(lane, trace_k++, blockIdx.x << 20 | wave << 16 | 16u << 8 | 2u << 4 | 1u, grp, tc0,
-                   __builtin_amdgcn_s_memrealtime());
+            wave_trace(lane, trace_k++, blockIdx.x << 20 | wave << 16 | 16u << 8 | 2u << 4 | 1u, grp, tc0,
+                       __builtin_amdgcn_s_memrealtime());
 #endif
-    }
+        }
+    };
+#if NEB_PRIO && NEB_PRIO_AGE
+    // A workgroup's waves w, w+4, w+8, w+12 share a SIMD in that age order (wave >> 2 is the
+    // rank), and the SIMD arbiter serves the older first at equal priority: ranks 0-3 finished
+    // their groups in 74 / 78 / 84 / 88 µs (tools/wave_trace.py, C2 seal, settled clock). Ranks 2
+    // and 3 keep priority 1 instead of 0 between their lookup phases, so they are not passed over
+    // by the older pair there. Alternating A/B against the same code at 0 (tools/r5_prio_ab.sh,
+    // profiles/r5/ab_balance): seal 96.5-98.7 -> 94.2-95.6 µs. Every other split tried — lookup levels by
+    // rank, four distinct levels, 0/1/1/1, 0/0/2/2 — was equal or slower.
+    if (__builtin_amdgcn_readfirstlane(wave) >> 3) groups(RkRegsPrio<NEB_PRIO, 1>{rk});
+    else groups(rk);
+#else
+    groups(rk);
+#endif
 }
 
 // The tail pass: the packets after gcm_single_kernel's full passes over args.tail_slots waves (the
@@ -1388,9 +1415,8 @@ struct ChunkArgs {
 };
 
 // Chunk order: the chunks of each kind come longest first (size class). Workgroup w owns chunks w,
-// w + G, w + 2G, ... of its kind (G workgroups) and its waves draw them from an LDS cursor, one
-// chunk ahead, so the next chunk's descriptor load overlaps the current chunk. Balance stays
-// dynamic inside the workgroup and no wave touches a global atomic (a global work cursor: returning
+// w + G, w + 2G, ... of its kind (G workgroups) and its waves draw them from an LDS cursor as
+// each finishes its chunk. Balance stays dynamic inside the workgroup and no wave touches a global atomic (a global work cursor: returning
 // atomics on one word serialise across the chip; C3 step -8%, IMIX -27% against it, A/B,
 // profiles/r2_micro/ab_chunk_order.log).
 template <bool OPEN, bool RX = false>
@@ -1423,7 +1449,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         return ca.chunks[c < nfront ? c : c < nfront + nlong ? ca.max_chunks - 1u - (c - nfront) : ca.max_chunks + (c - nfront - nlong)];
     };
     // Workgroup w owns chunks w, w + G, w + 2G, ... (front chunks first: the longest) and its waves
-    // draw them from an LDS cursor, one chunk ahead. Drawing the last 10-50% from a global cursor
+    // draw them from an LDS cursor as they finish. Drawing the last 10-50% from a global cursor
     // instead (dynamic balance across workgroups) made the C3 kernel 26-50% slower: the returning
     // atomics on one word serialise across the chip (A/B).
     auto chunk_of = [&](uint32_t k) -> uint32_t { return c0 + blockIdx.x + k * gridDim.x; };
@@ -1432,16 +1458,17 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     c = __builtin_amdgcn_readfirstlane(c);
     uint4 ch_next = make_uint4(0, 0, 0, 0);
     if (c < nch) ch_next = chunk_at(c);
+    auto claim = [&]() -> uint32_t {
+        uint32_t k = 0;
+        if (lane == 0u) k = chunk_of(atomicAdd(&wg_cursor, 1u));
+        return __builtin_amdgcn_readfirstlane(k);
+    };
     while (c < nch) {
         const uint4 ch = ch_next;
         const bool full = c < nfront;
 #ifdef NEB_WAVE_TRACE
         const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        uint32_t cn = 0;
-        if (lane == 0u) cn = chunk_of(atomicAdd(&wg_cursor, 1u));
-        cn = __builtin_amdgcn_readfirstlane(cn);
-        if (cn < nch) ch_next = chunk_at(cn);
         // Lane-derived constants (the T-table lane base, shuffle sources, the final's permutation)
         // are rebuilt per chunk from an opaque copy of the lane index: hoisted out of the chunk loop
         // they stay live across it and the compiler spills them (36-104 B of scratch per lane).
@@ -1485,6 +1512,14 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the next chunk is claimed when this one is done, not when it starts: a claim at the start
+        // handed the workgroup's second round of chunks to whichever waves reached the cursor first
+        // at time 0 (the older ones), and C3's waves then finished 97-115 µs apart
+        // (tools/wave_trace.py). A/B, alternating (profiles/r5/ab_balance): C3 526-527 -> 536-537 GiB/s,
+        // C5 504-505 -> 515-516; claiming ahead only while more than a round of chunks is left:
+        // C3 537-542, C5 506-508.
+        const uint32_t cn = claim();
+        if (cn < nch) ch_next = chunk_at(cn);
 #ifdef NEB_WAVE_TRACE
         wave_trace(lane, trace_k++,
                    blockIdx.x << 20 | wave << 16 | min((uint32_t)__builtin_amdgcn_readfirstlane(ch.y), 255u) << 8 |

@@ -73,6 +73,10 @@ def analyse(tr, waves_per_wg=16):
         kinds.setdefault(key, []).append(d)
     out["chunk_us"] = {k: {"n": len(v), "mean": round(float(np.mean(v)), 2), "max": round(float(np.max(v)), 2)}
                        for k, v in sorted(kinds.items())}
+    # mean chunk duration by wave index in the workgroup (index // 4 is the wave's age rank on its
+    # SIMD: a workgroup's waves go to the SIMDs in turn) and the order the waves finish in
+    out["chunk_us_by_wave"] = [round(float(dur[ch & (wave == w)].mean()), 2) for w in range(waves_per_wg)
+                               if (ch & (wave == w)).any()]
     # chunks per wave
     per_wave = np.bincount((wg[ch] * waves_per_wg + wave[ch]).astype(np.int64))
     out["chunks_per_wave"] = {int(k): int(v) for k, v in zip(*np.unique(per_wave, return_counts=True))}
@@ -124,10 +128,13 @@ def main():
     eng = Engine(0, max_keys=max(4096, b.nkeys))
     ciphers = install_keys(eng, b)
     db = DeviceBatch(eng, b, ciphers)
-    for _ in range(3):
-        db.seal()
-        db.open()
-    torch.cuda.synchronize()
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:  # settle the clocks (bench.py settle())
+        for _ in range(8):
+            db.seal()
+            db.open()
+        torch.cuda.synchronize()
     fetch(lib)
     res = {}
     for name, fn in (("seal", db.seal), ("open", db.open)):
