@@ -29,7 +29,10 @@
 
 namespace neb {
 
-constexpr int kChWavesPerWG = 4;
+#ifndef NEB_CH_WAVES
+#define NEB_CH_WAVES 4
+#endif
+constexpr int kChWavesPerWG = NEB_CH_WAVES;
 constexpr int kChThreads = kChWavesPerWG * kWave;
 
 // ---- ChaCha20 quad ---------------------------------------------------------------------------
