@@ -1147,12 +1147,6 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
     if (tid < 512u) r_full = ld_rec4(srec, kRecFull + 4u * tid);
     if (tid < 128u) r_h = ld_rec4(srec, kRecPos1 + 4u * tid);
     if (tid < 256u) r_p = ld_rec4(srec, (tid < 128u ? kRecPos2 : kRecPos3) + 4u * (tid & 127u));
-#if NEB_DESC_PREFETCH
-    // the wave's first packet descriptor, loaded before the fill so its latency overlaps it
-    const uint32_t p0 = (blockIdx.x + wave * gridDim.x) * kPpw + lane / kLpp;
-    neb_desc d0 = {};
-    if (p0 < args.npkt) d0 = args.desc[p0];
-#endif
     const TLook4 T{lds.ttab, ttab4_lane_base(lane)};
     fill_ttab<2u * 256u * 32u, kSingleThreads>(lds.ttab, tid, ttab4_entry);
     if (tid < 512u) lds.full[tid] = r_full;
@@ -1195,12 +1189,7 @@ __global__ __launch_bounds__(kSingleThreads, kSingleWpe) void gcm_single_kernel(
             const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
 #endif
             const uint32_t p = grp * kPpw + lane / kLpp;
-#if NEB_DESC_PREFETCH
-            const neb_desc dd = grp == blockIdx.x + wave * gridDim.x ? d0 : p < npkt ? args.desc[p] : neb_desc{};
-            gcm_packet_group<OPEN, CS, RX>(args, p, p < npkt, args.key_hint, key_ok, rkp, gh, T, lane, kLg, cs_pow, &dd);
-#else
             gcm_packet_group<OPEN, CS, RX>(args, p, p < npkt, args.key_hint, key_ok, rkp, gh, T, lane, kLg, cs_pow);
-#endif
 #ifdef NEB_WAVE_TRACE
             wave_trace(lane, trace_k++, blockIdx.x << 20 | wave << 16 | 16u << 8 | 2u << 4 | 1u, grp, tc0,
                        __builtin_amdgcn_s_memrealtime());

@@ -29,10 +29,7 @@
 
 namespace neb {
 
-#ifndef NEB_CH_WAVES
-#define NEB_CH_WAVES 4
-#endif
-constexpr int kChWavesPerWG = NEB_CH_WAVES;
+constexpr int kChWavesPerWG = 4;  // 1, 2 and 4 measured equal on the uncapped grid, 8 -3%, 16 -13%
 constexpr int kChThreads = kChWavesPerWG * kWave;
 
 // ---- ChaCha20 quad ---------------------------------------------------------------------------
