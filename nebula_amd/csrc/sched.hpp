@@ -42,7 +42,16 @@ constexpr uint32_t kCntPackets = 0;      // cursor into sorted[]
 constexpr uint32_t kCntFrontChunks = 1;  // chunks of groups at 4 lanes per packet, chunks[0, F)
 constexpr uint32_t kCntBackChunks = 2;   // long tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
 constexpr uint32_t kCntShortChunks = 3;  // short tails, chunks[max_chunks + j] (sched_tail_long)
+#ifndef NEB_CHUNK_STEAL  // gcm_chunk_kernel: the last 1/NEB_CHUNK_STEAL of a batch's chunks drawn per XCD (0: off)
+#define NEB_CHUNK_STEAL 8
+#endif
+#if NEB_CHUNK_STEAL
+// the chunk kernel's per-XCD cursors over the batch's last chunks, 128 B apart (gcm_chunk_kernel)
+constexpr uint32_t kCntSteal = 32, kStealStride = 32;
+constexpr uint32_t kSchedCounters = kCntSteal + 8 * kStealStride;
+#else
 constexpr uint32_t kSchedCounters = 4;
+#endif
 // sorted[] entry of a packet the crypto kernel must skip (the device receive's refused packets)
 constexpr uint32_t kSortedSkip = 0xFFFFFFFFu;
 
