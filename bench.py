@@ -324,6 +324,10 @@ def main():
     ap.add_argument("--tx-superpackets", type=int, default=1457,
                     help="tx mode: 64 KiB TSO superpackets per batch (45 segments each; 1457 -> 65 565 wires, "
                          "1456 -> 65 520: within one pass of the 4096 waves of 16 packets)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="--config 4 on one rank: run only shard --shard-rank of the 1 Mi C5 batch split N ways "
+                         "(the packets one GPU of an N-GPU run gets), so the per-GPU shape is measured on one GPU")
+    ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # tests: launch + aggregation, no GPU
     args = ap.parse_args()
 
@@ -364,12 +368,16 @@ def main():
         2: (L.ALG_AESGCM, 65536, 4096),
         3: (L.ALG_CHACHAPOLY, 65536, 4096),
     }[cfg], seed=W.SEED ^ rank, name=f"C{cfg + 1}") if cfg in (0, 1, 2, 3) else \
-        W.shard(W.config(4), rank, world)
+        W.shard(W.config(4), *((args.shard_rank, args.shard_of) if args.shard_of else (rank, world)))
     workload_name = {0: "C1 AES-256-GCM, 1 tunnel key, 1024 x 1300 B packets, device-resident",
                      1: "C2 AES-256-GCM, 1 tunnel key, 65536 x 1300 B packets, device-resident",
                      2: "C3 AES-256-GCM, 4096 tunnel keys, 65536 x 1300 B packets, device-resident",
                      3: "C4 ChaCha20-Poly1305, 4096 tunnel keys, 65536 x 1300 B packets, device-resident",
                      4: "C5 AES-256-GCM, 4096 tunnel keys, IMIX 90/576/1300 (7:4:1), 1 Mi packets sharded"}[cfg]
+    if cfg == 4 and args.shard_of:
+        if world != 1:
+            raise SystemExit("--shard-of runs one shard on one rank")
+        workload_name += f": shard {args.shard_rank} of {args.shard_of} alone ({b.n} packets, one GPU's part)"
     log(f"[rank {rank}] batch {b.name}: {b.n} pkts, {b.payload_bytes / 1e6:.1f} MB payload "
         f"({time.time() - t0:.1f}s to build)")
 
@@ -488,7 +496,7 @@ def main():
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
     # the kernel the dispatch-bound events were bound to, as the library names it
     kern_tag = seal_kernel if bound else "event brackets around the whole seal call"
-    pmc = pmc_config(f"C{cfg + 1}")
+    pmc = pmc_config(f"C{cfg + 1}" + (f"/{args.shard_of}" if cfg == 4 and args.shard_of else ""))
     lens = b.desc["len"].astype(np.int64)
     out = {
         "metric": "GiB/s device-resident AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch"

@@ -97,6 +97,9 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x 
 __device__ __forceinline__ uint4 x34(uint4 a, uint4 b, uint4 c) {
     return make_uint4(x3(a.x, b.x, c.x), x3(a.y, b.y, c.y), x3(a.z, b.z, c.z), x3(a.w, b.w, c.w));
 }
+__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
 __device__ __forceinline__ uint4 bswap4(uint4 v) { return make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w)); }
 __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
     return make_uint4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m), __shfl_xor(v.w, m));
@@ -877,15 +880,30 @@ struct GhChunk4 {
                           [&](uint4 a, uint32_t off) { return gf_mul_shoup(a, off, shoup); });
     }
 };
-// Tail chunks (1-8 packets at 8 or 16 lanes): Horner on the position tables of H^(2^lg), the tree
-// on M_1, M_2, M_4, M_8.
-
-struct GhChunkTree {
-    const uint4* shoup;  // M_1, M_2, M_4, M_8
+// Tail chunks (1-8 packets at 8 or 16 lanes): Horner on the position tables of H^(2^lg); the final
+// as quads, then a short tree over the packet's quads (round 6). Lane l = 4a + b of a packet needs
+// A_l·H^(LPP-l) = A_l·H^(4-b)·H^(4(LPP/4-1-a)): the permuted one-multiply final of the 4-lane chunks
+// gives every quad Q_a = Σ_b A_(4a+b)·H^(4-b) (final_perm treats each quad as a packet), then
+// LPP 8: Q_0·H^4 ⊕ Q_1; LPP 16: (Q_0·H^4 ⊕ Q_1)·H^8 ⊕ (Q_2·H^4 ⊕ Q_3). Every lane of a level multiplies
+// by the same table (M_4, then M_8), so the lookups stay conflict-free: 2 or 3 dependent multiplies
+// instead of the pairwise tree's 4 or 5 (that tree cost ≈ 2 rounds of VALU per tail chunk, and tail
+// chunks are half of a C5 shard's chunks).
+struct GhChunkTail {
+    const uint4* shoup;  // M_1, M_2, M_3, M_4, M_8
     const uint4* pos;    // position tables of H^(2^lg)
     __device__ __forceinline__ uint4 horner(uint4 a, uint32_t) const { return gf_mul_pos(a, pos); }
     __device__ __forceinline__ uint4 final(uint4 A, uint32_t lane, uint32_t lg) const {
-        return tree_final(A, lane, lg, shoup, [](uint32_t i) { return i * 256u; });
+        const uint32_t ln = lane;
+        const uint32_t tab_off[4] = {3u * 256u, 2u * 256u, 256u, 0u};  // M_4, M_3, M_2, M_1
+        const uint4 Q = final_perm(A, final_perm_lanes(ln, tab_off),
+                                   [&](uint4 a, uint32_t off) { return gf_mul_shoup(a, off, shoup); });
+        const uint32_t a = (ln >> 2) & ((1u << (lg - 2u)) - 1u);  // the quad's index in its packet
+        // (selects per component: a select of two uint4 values went through a scratch array)
+        const uint4 W = sel4((a & 1u) != 0u, Q, gf_mul_shoup(Q, 3u * 256u, shoup));  // even quads: Q·H^4
+        const uint4 P = xor4(W, shfl_xor4(W, 4));  // quads (0,1): Q_0·H^4 ⊕ Q_1, (2,3): Q_2·H^4 ⊕ Q_3
+        if (lg == 3u) return P;
+        const uint4 U = sel4((a & 2u) != 0u, P, gf_mul_shoup(P, 4u * 256u, shoup));  // quads 0, 1: ·H^8
+        return xor4(U, shfl_xor4(U, 8));
     }
 };
 
@@ -942,6 +960,23 @@ __device__ __forceinline__ uint4 gcm_csum_fix(const neb_desc& d, uint32_t n, uin
     return corr;
 }
 
+#ifdef NEB_WAVE_TRACE
+// per-wave phase times of the packet groups (tools/wave_trace.py, trace build only): the chunk kernel
+// clears them per chunk and records them; s_memrealtime ticks summed over the chunk's groups, each
+// phase closed by a full s_waitcnt (so a phase's time includes the latency of its own accesses)
+constexpr uint32_t kWavePhaseWaves = 8192;
+__device__ uint32_t g_wphase[kWavePhaseWaves * 4];  // desc, rounds, final, finish
+__device__ __forceinline__ uint32_t wave_gid() { return blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); }
+__device__ __forceinline__ uint64_t phase_now() {
+    __builtin_amdgcn_s_waitcnt(0);
+    return __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void phase_add(uint32_t k, uint64_t t0, uint64_t t1) {
+    const uint32_t w = wave_gid();
+    if ((threadIdx.x & 63u) == 0u && w < kWavePhaseWaves) g_wphase[4u * w + k] += (uint32_t)(t1 - t0);
+}
+#endif
+
 // Seal or open packet `p` (lanes (lane >> lg) << lg ... + LPP-1 of the wave). `expect_key`: the key
 // this wave's round keys and tables belong to; key_ok: that key is installed with the right
 // algorithm. lg is wave-uniform.
@@ -955,12 +990,19 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                                                  const neb_desc* own = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
+#ifdef NEB_WAVE_TRACE
+    const uint64_t tq0 = phase_now();
+#endif
     neb_desc d = {};
     uint32_t admit = 1u;
     if (valid) {
         d = own ? *own : args.desc[p];
         if constexpr (RX) admit = args.adm[p];  // (beside the descriptor's load, not behind it)
     }
+#ifdef NEB_WAVE_TRACE
+    const uint64_t tq1 = phase_now();
+    phase_add(0, tq0, tq1);
+#endif
     // the device receive opens only what its windows admitted (the rest keep the plan's status)
     if constexpr (RX) valid = valid && admit != 0u;
     uint32_t st = NEB_STATUS_OK;
@@ -1076,7 +1118,15 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     __builtin_amdgcn_s_waitcnt(0);
     const uint64_t tp1 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef NEB_WAVE_TRACE
+    const uint64_t tq2 = phase_now();
+    phase_add(1, tq1, tq2);
+#endif
     uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
+#ifdef NEB_WAVE_TRACE
+    const uint64_t tq3 = phase_now();
+    phase_add(2, tq2, tq3);
+#endif
 #if NEB_ONE_TRACE
     __builtin_amdgcn_s_waitcnt(0);
     const uint64_t tp2 = __builtin_amdgcn_s_memrealtime();
@@ -1087,6 +1137,9 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     }
     if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
     if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
+#ifdef NEB_WAVE_TRACE
+    phase_add(3, tq3, phase_now());
+#endif
 }
 
 __device__ __forceinline__ void load_round_keys(const uint32_t* rec, uint32_t rks[60]) {
@@ -1368,14 +1421,14 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
 // per packet spilled 52-64 B per lane at 128 VGPRs, inside the chunk loop):
 //  front chunks (chunks[0, F)): groups of 16 packets at 4 lanes each, the layout of the single-key
 //               kernel (GhChunk4), one after another on one staging of the key;
-//  back chunks (chunks[max - 1 - j], j < B): tails of 1-8 packets at 8 or 16 lanes (GhChunkTree).
+//  back chunks (chunks[max - 1 - j], j < B): tails of 1-8 packets at 8 or 16 lanes (GhChunkTail).
 // The two-table AES (64 KiB): 16 waves per workgroup, one workgroup per CU.
 constexpr int kChunkWaves = 16;
 constexpr int kChunkWpe = 4;  // launch bound: waves per SIMD (at most 128 VGPRs)
 constexpr int kChunkThreads = kChunkWaves * kWave;
 
 struct ChunkLds {
-    uint4 shoup[kChunkWaves][4][16];  // per wave: Shoup tables (1 KiB): M_1..M_4 (full), M_1, M_2, M_4, M_8 (tails)
+    uint4 shoup[kChunkWaves][5][16];  // per wave: Shoup tables (1.25 KiB): M_1..M_4, and M_8 (tails)
     uint4 pos[kChunkWaves][8 * 16];   // per wave: position tables of H^(2^lg) (2 KiB)
     uint2 ttab[256 * 32];             // 64 KiB T-table pairs, 32 copies
 };
@@ -1383,17 +1436,20 @@ struct ChunkLds {
 // Stage a chunk key's GHASH tables in the wave's LDS slice, computed from the record's raw powers
 // H^1..H^16 (16 B each) rather than copied from its precomputed tables: 128 B of key material per
 // chunk instead of 3 KiB, which for IMIX-sized chunks was a third of the kernel's memory traffic.
-//   shoup[t][v] = v·H^(e_t), t < 4: e = 1, 2, 3, 4 (FULL) or 1, 2, 4, 8 (tails)
+//   shoup[t][v] = v·H^(t+1), t < 4, and (tails) shoup[4][v] = v·H^8
 //   pos[r][v]   = v·x^(4r)·P, r < 8, P = H^(2^lg): XOR of the basis P·x^(4r+j) over the set bits
 //                 of v (bit 3 ↔ j = 0), the basis P·x^i (i < 32) one per lane and shuffled
 template <bool FULL>
 __device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t lane, uint32_t lg, uint4* wtab,
                                                    uint4* wpos) {
     const uint32_t t = lane >> 4, v = lane & 15u;
-    const uint32_t e = FULL ? t + 1u : 1u << t;
-    const uint4 he = ld_rec4(rec, kRecHPow + 4u * (e - 1u));
+    const uint4 he = ld_rec4(rec, kRecHPow + 4u * t);
     const uint4 P = ld_rec4(rec, kRecHPow + 4u * ((1u << lg) - 1u));
     wtab[lane] = gf_tab_entry(he, v);
+    if constexpr (!FULL) {
+        const uint4 h8 = ld_rec4(rec, kRecHPow + 4u * 7u);
+        if (lane < 16u) wtab[64u + lane] = gf_tab_entry(h8, v);
+    }
     const uint4 B = gf_mul_xpow32(P, lane & 31u);
     uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -1409,14 +1465,14 @@ __device__ __forceinline__ void stage_chunk_tables(const uint32_t* rec, uint32_t
 
 struct ChunkArgs {
     const uint32_t* sorted;
-    const uint4* chunks;
-    uint32_t* counters;  // the scheduler's counters (sched.hpp kCnt*)
-    uint32_t max_chunks, max_short;
+    const uint4* chunks;  // [kBuckets][max_chunks] (sched.hpp)
+    uint32_t* counters;   // the scheduler's counters (sched.hpp kCnt*)
+    uint32_t max_chunks;
 };
 
-// Chunk order: the chunks of each kind come longest first (size class). Workgroup w owns chunks w,
-// w + G, w + 2G, ... of its kind (G workgroups) and its waves draw them from an LDS cursor as
-// each finishes its chunk. Balance stays dynamic inside the workgroup and no wave touches a global atomic (a global work cursor: returning
+// Chunk order: the cost buckets in turn, longest first (sched.hpp sched_bucket). Workgroup w owns
+// chunks w, w + G, w + 2G, ... of that order (G workgroups) and its waves draw them from an LDS
+// cursor as each finishes its chunk. Balance stays dynamic inside the workgroup and no wave touches a global atomic (a global work cursor: returning
 // atomics on one word serialise across the chip; C3 step -8%, IMIX -27% against it, A/B,
 // profiles/r2_micro/ab_chunk_order.log).
 template <bool OPEN, bool RX = false>
@@ -1426,12 +1482,18 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = tid >> 6;
-    const uint32_t nfront = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntFrontChunks]), ca.max_chunks);
-    const uint32_t nlong = min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBackChunks]), ca.max_chunks - nfront);
-    const uint32_t nback = nlong + min(__builtin_amdgcn_readfirstlane(ca.counters[kCntShortChunks]), ca.max_short);
-    // chunk index space: [0, nfront) the front chunks, then the long tails (chunks[max - 1 - j]),
-    // then the short ones (chunks[max + j])
-    const uint32_t c0 = 0u, nch = nfront + nback;
+    // chunk index space: bucket 0's chunks, then bucket 1's, ... (bucket b's records from b * max_chunks);
+    // the buckets' ends in LDS (read per chunk: held in registers they were spilled)
+    __shared__ uint32_t s_bend[kBuckets];
+    uint32_t nch = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < kBuckets; b++) nch += min(__builtin_amdgcn_readfirstlane(ca.counters[kCntBucket + b]), ca.max_chunks);
+    if (tid < kBuckets) {
+        uint32_t e = 0;
+        for (uint32_t b = 0; b <= tid; b++) e += min(ca.counters[kCntBucket + b], ca.max_chunks);
+        s_bend[tid] = e;
+    }
+    const uint32_t c0 = 0u;
     if (c0 + blockIdx.x >= nch) return;  // owns no chunk (uniform over the workgroup)
 #ifdef NEB_WAVE_TRACE
     const uint64_t tk0 = __builtin_amdgcn_s_memrealtime();
@@ -1446,9 +1508,16 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     uint4* wtab = &lds.shoup[wave][0][0];
     uint4* wpos = &lds.pos[wave][0];
     auto chunk_at = [&](uint32_t c) {
-        return ca.chunks[c < nfront ? c : c < nfront + nlong ? ca.max_chunks - 1u - (c - nfront) : ca.max_chunks + (c - nfront - nlong)];
+        uint32_t b = 0, lo = 0;
+        for (uint32_t k = 0; k + 1u < kBuckets; k++) {
+            const uint32_t e = __builtin_amdgcn_readfirstlane(s_bend[k]);
+            if (c < e) break;
+            b = k + 1u;
+            lo = e;
+        }
+        return ca.chunks[(size_t)b * ca.max_chunks + (c - lo)];
     };
-    // Workgroup w owns chunks w, w + G, w + 2G, ... (front chunks first: the longest) and its waves
+    // Workgroup w owns chunks w, w + G, w + 2G, ... (the longest first) and its waves
     // draw them from an LDS cursor as they finish. Drawing the last 10-50% from a global cursor
     // instead (dynamic balance across workgroups) made the C3 kernel 26-50% slower: the returning
     // atomics on one word serialise across the chip (A/B).
@@ -1488,7 +1557,8 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
 #endif
     while (c < nch) {
         const uint4 ch = ch_next;
-        const bool full = c < nfront;
+        const uint32_t cw = __builtin_amdgcn_readfirstlane(ch.w);
+        const bool full = (cw >> 20) & 1u;  // 4-lane groups (front), or one group at 8 or 16 lanes
 #ifdef NEB_WAVE_TRACE
         const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1498,38 +1568,57 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));
         const TLook T{lds.ttab, ttab_lane_base(ln)};
+#ifdef NEB_WAVE_TRACE
+        if (lane == 0u && wave_gid() < kWavePhaseWaves)
+            for (uint32_t k = 0; k < 4u; k++) g_wphase[4u * wave_gid() + k] = 0u;
+        const uint64_t tcd = phase_now();  // the chunk's descriptor in
+#endif
+        // the chunk's packets: segment 0 (count0 from start0 in sorted), then segment 1 (a smaller
+        // class's leftover packets riding in free slots, sched_key_chunks)
         const uint32_t start = __builtin_amdgcn_readfirstlane(ch.x);
-        const uint32_t count = __builtin_amdgcn_readfirstlane(ch.y);
+        const uint32_t start1 = __builtin_amdgcn_readfirstlane(ch.y);
+        const uint32_t count0 = cw & 0xFFu, count = count0 + ((cw >> 8) & 0xFFu);
         const uint32_t key = __builtin_amdgcn_readfirstlane(ch.z);
+        auto sorted_at = [&](uint32_t q) { return ca.sorted[q < count0 ? start + q : start1 + (q - count0)]; };
         const uint32_t* rec = args.keys + (size_t)(key < args.max_keys ? key : 0u) * kKeyRecDwords;
         const bool key_ok = key < args.max_keys && rec[kRecAlg] == NEB_ALG_AESGCM;
         uint32_t rks[60];
         load_round_keys(rec, rks);
+#ifdef NEB_WAVE_TRACE
+        const uint64_t tck = phase_now();  // round keys in
+        uint64_t tcs = tck;
+#endif
         if (full) {
             stage_chunk_tables<true>(rec, ln, 2u, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef NEB_WAVE_TRACE
+            tcs = phase_now();
+#endif
             // the chunk's groups of 16 packets at 4 lanes, one after another on the staged tables
             const GhChunk4 gh{wtab, wpos};
             for (uint32_t g0 = 0; g0 < count; g0 += kChunkPkts) {
                 const uint32_t q = g0 + (ln >> 2);
-                const uint32_t sp = q < count ? ca.sorted[start + q] : kSortedSkip;
+                const uint32_t sp = q < count ? sorted_at(q) : kSortedSkip;
                 const bool valid = sp != kSortedSkip;  // (a device receive's refused packet: skipped)
                 const uint32_t p = valid ? sp : 0u;
                 gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, 2u);
             }
         } else {
-            const uint32_t lg = __builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift);  // 3 or 4
+            const uint32_t lg = (cw >> kChunkLgShift) & 15u;  // 3 or 4
             stage_chunk_tables<false>(rec, ln, lg, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef NEB_WAVE_TRACE
+            tcs = phase_now();
+#endif
             const uint32_t q = ln >> lg;
-            const uint32_t sp = q < count ? ca.sorted[start + q] : kSortedSkip;
+            const uint32_t sp = q < count ? sorted_at(q) : kSortedSkip;
             const bool valid = sp != kSortedSkip;
             const uint32_t p = valid ? sp : 0u;
-            const GhChunkTree gh{wtab, wpos};
+            const GhChunkTail gh{wtab, wpos};
             gcm_packet_group<OPEN, false, RX>(args, p, valid, key, key_ok, RkRegs{rks}, gh, T, ln, lg);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten next chunk
@@ -1545,9 +1634,17 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         if (cn < nch) ch_next = chunk_at(cn);
 #ifdef NEB_WAVE_TRACE
         wave_trace(lane, trace_k++,
-                   blockIdx.x << 20 | wave << 16 | min((uint32_t)__builtin_amdgcn_readfirstlane(ch.y), 255u) << 8 |
-                       (full ? 2u : (uint32_t)__builtin_amdgcn_readfirstlane(ch.w >> kChunkLgShift)) << 4 | (full ? 1u : 0u),
+                   blockIdx.x << 20 | wave << 16 | min(count, 255u) << 8 | ((cw >> kChunkLgShift) & 15u) << 4 |
+                       (full ? 1u : 0u),
                    c, tc0, __builtin_amdgcn_s_memrealtime());
+        if (trace_k <= 21u) {  // phases: {descriptor in, round keys in, tables staged} and the groups' sums
+            const uint32_t w = wave_gid() < kWavePhaseWaves ? wave_gid() : 0u;
+            const uint32_t* ph = &g_wphase[4u * w];
+            const uint32_t tag = blockIdx.x << 20 | wave << 16;
+            wave_trace(lane, 20u + 2u * (trace_k - 1u), tag, 0xFFFFFFFEu,
+                       (uint32_t)(tcd - tc0) | (uint32_t)(tck - tcd) << 16, (uint32_t)(tcs - tck));
+            wave_trace(lane, 21u + 2u * (trace_k - 1u), tag, 0xFFFFFFFDu, ph[0] | ph[1] << 16, ph[2] | ph[3] << 16);
+        }
 #endif
         c = cn;
     }
@@ -1951,11 +2048,11 @@ extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
-                                            uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
+                                            uint32_t* d_counters, uint32_t max_chunks,
                                             int cu_count, hipStream_t s, int hdr_from_dst,
                                             hipEvent_t stop, const uint8_t* rx) {
     neb::GcmArgs a{d_desc, n, d_arena, d_keys, max_keys, NEB_KEYS_MIXED, d_status, nullptr, (uint32_t)hdr_from_dst, 0u, rx};
-    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks, max_short};
+    neb::ChunkArgs ca{d_sorted, d_chunks, d_counters, max_chunks};
     // one workgroup per chunk up to the occupancy cap (tails make chunks outnumber n / 16), so a
     // small batch's chunks spread over the CUs; the chunk counts are only known on the device:
     // workgroups past them exit before filling their tables. Full chunks first, then the tails.

@@ -51,7 +51,7 @@ extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_
 extern "C" hipError_t neb_gcm_batch_chunked(int open, const neb_desc* d_desc, uint32_t n, uint8_t* d_arena,
                                             const uint32_t* d_keys, uint32_t max_keys, int32_t* d_status,
                                             const uint32_t* d_sorted, const uint4* d_chunks,
-                                            uint32_t* d_counters, uint32_t max_chunks, uint32_t max_short,
+                                            uint32_t* d_counters, uint32_t max_chunks,
                                             int cu_count, hipStream_t s, int hdr_from_dst, hipEvent_t stop,
                                             const uint8_t* rx);
 extern "C" hipError_t neb_gcm_probe(void);
@@ -318,10 +318,19 @@ class PktLease {
     PktLease(const PktLease&) = delete;
     PktLease& operator=(const PktLease&) = delete;
     PktSlot* operator->() const { return s_; }
-    // room for `bytes` of staging (the slot is exclusively ours; its stream is idle between leases)
+    // room for `bytes` of staging (the slot is exclusively ours). A per-packet call returns as soon as
+    // its kernel has published the status word, so the previous lease's kernel may still be draining
+    // on the slot's stream: wait for it before the buffer it writes is freed.
     bool reserve(size_t bytes) {
         if (bytes <= s_->cap) return true;
-        if (s_->h) hipHostFree(s_->h);
+        if (s_->h) {
+            const hipError_t err = hipStreamSynchronize(s_->stream);
+            if (err != hipSuccess) {
+                set_error("PktLease::reserve", err);
+                return false;
+            }
+            hipHostFree(s_->h);
+        }
         s_->h = nullptr;
         s_->cap = 0;
         const size_t cap = std::max(kStageMin, align_up(bytes, 1 << 16));
@@ -794,10 +803,10 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     }
     const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
     const uint32_t nb = neb::sched_nbins(e->max_keys);
-    const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys), ms = neb::sched_max_short(cap, e->max_keys);
+    const uint32_t mc = neb::sched_max_chunks(cap, e->max_keys);
     const size_t b_counters = align_up((neb::kSchedCounters + (size_t)neb::kSubBins * nb) * 4u, 256);
     const size_t b_base = align_up((size_t)neb::kSubBins * nb * 4u, 256);
-    const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up(((size_t)mc + ms) * 16u, 256);
+    const size_t b_idx = align_up((size_t)cap * 4u, 256), b_chunks = align_up((size_t)neb::kBuckets * mc * 16u, 256);
     const size_t b_tcnt = tiles ? align_up((size_t)neb::kTileMax * neb::sched_tile_words(nb) * 4u, 256) : 0;
     const size_t b_tpre = tiles ? align_up((size_t)neb::kTileMax * nb * 4u, 256) : 0;
     const size_t bytes = b_counters + b_base + 3 * b_idx + b_chunks + b_tcnt + b_tpre;
@@ -826,7 +835,6 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     m += b_tcnt;
     sp.ws.tpre = tiles ? (uint32_t*)m : nullptr;
     sp.ws.max_chunks = mc;
-    sp.ws.max_short = ms;
     sp.bytes = bytes;
     sp.n_cap = cap;
     err = hipMemsetAsync(sp.ws.counters, 0, b_counters, s);  // once: the binning clears its counts as it uses them
@@ -871,7 +879,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
         }
         if (err == hipSuccess)  // sp.done bound to the chunk kernel's dispatch: no marker packet between batches
             err = neb_gcm_batch_chunked(open, d_desc, n, d_arena, e->d_keys, e->max_keys, d_status, sp.ws.sorted,
-                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, sp.ws.max_short, e->cu_count,
+                                        sp.ws.chunks, sp.ws.counters, sp.ws.max_chunks, e->cu_count,
                                         s, hdr_from_dst, bind_events() ? sp.done : nullptr,
                                         prebinned ? nullptr : rx);  // (prebinned: refused packets unlisted)
         if (err == hipSuccess && !bind_events()) err = hipEventRecord(sp.done, s);

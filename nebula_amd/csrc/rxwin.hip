@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void rx_sort_pass_kernel(RxSort so, uint32_t p
     if (blockIdx.x >= so.nblk) {  // the open's binning: pass 2 beside the first sort pass, 3 beside the second
         const uint32_t r = blockIdx.x - so.nblk;
         if (FIRST) {
-            __shared__ SchedAllocLds<1> sl;
+            __shared__ SchedAllocLds sl;
             sched_alloc_block<1>(bin.max_keys, bin.ws, r, sl);
         } else {
             const uint32_t i = r * 256u + threadIdx.x;

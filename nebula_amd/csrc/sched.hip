@@ -22,7 +22,7 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
 
 template <uint32_t SUB>
 __global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
-    __shared__ SchedAllocLds<SUB> sl;
+    __shared__ SchedAllocLds sl;
     sched_alloc_block<SUB>(max_keys, ws, blockIdx.x, sl);
 }
 
@@ -129,12 +129,17 @@ __global__ __launch_bounds__(256) void sched_tile_scan_kernel(SchedWs ws, uint32
 // (blockIdx mod 8, a placement observed, not promised: it only decides which L2 caches the row):
 // XCD slot x takes tiles x, x + 8, …, each row then pulled into one L2 instead of all eight (P is a
 // multiple of 256, so a workgroup's 256 packets lie in one tile).
+// With fewer than 8 tiles the XCD slots past T would get no work: the pieces are then dealt to the
+// whole grid instead (every workgroup strides over all T · P / 256 of them).
 __global__ void sched_tile_scatter_kernel(SchedWs ws, uint32_t n, const uint32_t* dn, uint32_t P, uint32_t nb, uint32_t T) {
     if (dn) n = min(n, *dn);
-    const uint32_t x = blockIdx.x & 7u, per_tile = P >> 8;
-    const uint32_t mine = (T > x ? (T - x + 7u) >> 3 : 0u) * per_tile;  // workgroup-sized pieces of XCD slot x
-    for (uint32_t k = blockIdx.x >> 3; k < mine; k += gridDim.x >> 3) {
-        const uint32_t t = x + 8u * (k / per_tile);
+    const bool flat = T < 8u;
+    const uint32_t x = flat ? 0u : blockIdx.x & 7u, per_tile = P >> 8;
+    const uint32_t xs = flat ? 1u : 8u;  // tiles between one slot's consecutive tiles
+    // workgroup-sized pieces of XCD slot x (flat: of every tile)
+    const uint32_t mine = (flat ? T : (T > x ? (T - x + 7u) >> 3 : 0u)) * per_tile;
+    for (uint32_t k = flat ? blockIdx.x : blockIdx.x >> 3; k < mine; k += flat ? gridDim.x : gridDim.x >> 3) {
+        const uint32_t t = x + xs * (k / per_tile);
         const uint32_t i = t * P + (k % per_tile) * 256u + threadIdx.x;
         if (i < n) {
             const uint32_t b = ws.binof[i];

@@ -1,12 +1,13 @@
 // sched.hpp — batch scheduling for mixed-key / mixed-size batches (shared by the AEAD kernels).
 //
 // A batch with many tunnel keys and mixed packet sizes is regrouped on the device before the
-// crypto kernel runs: packets are binned by (size class, key) with global atomics, each bin is
-// cut into chunks of at most kChunkPkts packets, and one wavefront processes one chunk. Inside a
-// chunk the key is wave-uniform (round keys in scalar registers, one set of GHASH tables) and the
-// packets need a similar number of rounds, so lanes neither diverge on keys nor idle on sizes.
-// No prefix scan is needed: bins reserve their output ranges with an atomic cursor, so the order
-// of bins (and of packets inside a bin) is arbitrary — every packet's result is independent of it.
+// crypto kernel runs: packets are binned by (size class, key) with global atomics, each key's bins
+// are cut into chunks of groups of up to kChunkPkts packets, and one wavefront processes one chunk.
+// Inside a chunk the key is wave-uniform (round keys in scalar registers, one set of GHASH tables)
+// and the packets need a similar number of rounds, so lanes neither diverge on keys nor idle on
+// sizes. No prefix scan over packets is needed: keys reserve their output ranges with an atomic
+// cursor, so the order of keys (and of packets inside a bin) is arbitrary — every packet's result is
+// independent of it.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,16 +19,20 @@ namespace neb {
 constexpr uint32_t kChunkPkts = 16;   // packets per packet group at 4 lanes per packet
 constexpr uint32_t kSizeClasses = 8;  // round-count classes at 4 lanes per packet: 1, 2, 3-4, 5-8, 9-16, 17-32, 33-64, 65+
 
-// A bin of c packets becomes c / 16 full groups of 16 packets at 4 lanes per packet, and one tail
-// of the c mod 16 others at 2^lg lanes per packet: lg 4 (16 lanes) for up to 4 packets, 3 for up
-// to 8, else 2 — capped for short packets so that no lane idles on a block that does not exist
-// (size class 0: <= 4 blocks, lg 2; class 1: <= 8 blocks, lg 3). A wave then runs a tail of 1-4
-// packets in a quarter of the rounds instead of leaving 48-60 of its lanes idle.
-// Groups at 4 lanes (the full ones, and a tail of 9-15 packets) are packed into "front" chunks of
-// up to sched_groups(cls) groups: one wave runs a chunk's groups one after another on one staging
-// of the key's tables and round keys, so short packets (IMIX 90 B: 2 rounds per group) do not pay
-// the staging per 16 packets. Tails at 8 or 16 lanes are "back" chunks of their own.
-constexpr uint32_t kChunkLgShift = 8;  // chunk.w = size class | lg << kChunkLgShift
+// A bin of c packets becomes c / 16 full groups of 16 packets at 4 lanes per packet, packed into
+// "front" chunks of up to sched_groups(cls) groups: one wave runs a chunk's groups one after another
+// on one staging of the key's tables and round keys, so short packets (IMIX 90 B: 2 rounds per
+// group) do not pay the staging per 16 packets. The c mod 16 others (the bin's leftover) form one
+// group at 2^lg lanes per packet: lg 4 (16 lanes) for up to 4 packets, 3 for up to 8, else 2 —
+// capped for short packets so that no lane idles on a block that does not exist (size class 0:
+// <= 4 blocks, lg 2; class 1: <= 8 blocks, lg 3). A wave then runs a leftover of 1-4 packets in a
+// quarter of the rounds instead of leaving 48-60 of its lanes idle.
+// Round 6: the leftovers of one key are planned together (sched_key_chunks), largest class first,
+// and a leftover group's free packet slots take the next smaller class's leftover packets: a smaller
+// class needs no more rounds at the same lanes, so they ride along for free, and when a class's whole
+// leftover is taken its own chunk (key staging, GHASH final, descriptor loads) is gone. A chunk is
+// then up to two segments of `sorted` (its own class's, and the absorbed class's).
+constexpr uint32_t kChunkLgShift = 16;  // chunk record .w: count0 | count1 << 8 | lg << 16 | front << 20 | cls << 24
 __host__ __device__ inline uint32_t sched_tail_lg(uint32_t count, uint32_t cls) {
     const uint32_t fit = count <= 4u ? 4u : (count <= 8u ? 3u : 2u);
     const uint32_t size = cls == 0u ? 2u : (cls == 1u ? 3u : 4u);
@@ -36,12 +41,31 @@ __host__ __device__ inline uint32_t sched_tail_lg(uint32_t count, uint32_t cls) 
 // groups of 16 packets per front chunk: about 8 rounds of work per chunk for the short classes
 __host__ __device__ inline uint32_t sched_groups(uint32_t cls) { return cls >= 3u ? 1u : 8u >> cls; }
 constexpr uint32_t kMaxChunkPkts = 8u * kChunkPkts;
+// chunk record {start of segment 0 in sorted, start of segment 1, key_id, w}
+__host__ __device__ inline uint32_t chunk_w(uint32_t c0, uint32_t c1, uint32_t lg, bool front, uint32_t cls) {
+    return c0 | c1 << 8 | lg << kChunkLgShift | (front ? 1u : 0u) << 20 | cls << 24;
+}
+
+// Chunks are ordered longest first (round 6): each is filed in one of kBuckets cost buckets, a
+// bucket holding up to max_chunks records (the bound on the whole batch's chunks), and the crypto
+// kernel enumerates bucket 0, then 1, ... Workgroup w owns chunks w, w + G, ... of that order, so
+// every workgroup's waves start on the longest work and its last chunks are the shortest. The cost
+// is in rounds at the class's upper bound (2^cls rounds at 4 lanes), plus one per group (its final)
+// and two per leftover group at 8-16 lanes (its deeper final).
+constexpr uint32_t kBuckets = 8;
+__host__ __device__ inline uint32_t sched_bucket(uint32_t cost) {
+    return cost >= 24u ? 0u : cost >= 16u ? 1u : cost >= 12u ? 2u : cost >= 9u ? 3u :
+           cost >= 7u ? 4u : cost >= 5u ? 5u : cost >= 3u ? 6u : 7u;
+}
+__host__ __device__ inline uint32_t sched_front_cost(uint32_t groups, uint32_t cls) { return groups * ((1u << cls) + 1u); }
+__host__ __device__ inline uint32_t sched_tail_cost(uint32_t cls, uint32_t lg) {
+    const uint32_t r = (1u << cls) * 4u >> lg;
+    return (r ? r : 1u) + 2u;
+}
 
 // counters[] slots
-constexpr uint32_t kCntPackets = 0;      // cursor into sorted[]
-constexpr uint32_t kCntFrontChunks = 1;  // chunks of groups at 4 lanes per packet, chunks[0, F)
-constexpr uint32_t kCntBackChunks = 2;   // long tails at 8 or 16 lanes per packet, chunks[max_chunks - 1 - j]
-constexpr uint32_t kCntShortChunks = 3;  // short tails, chunks[max_chunks + j] (sched_tail_long)
+constexpr uint32_t kCntPackets = 0;  // cursor into sorted[]
+constexpr uint32_t kCntBucket = 1;   // [kBuckets] chunks filed in each cost bucket
 #ifndef NEB_CHUNK_STEAL  // gcm_chunk_kernel: the last 1/NEB_CHUNK_STEAL of a batch's chunks drawn per XCD (0: off)
 #define NEB_CHUNK_STEAL 8
 #endif
@@ -50,7 +74,7 @@ constexpr uint32_t kCntShortChunks = 3;  // short tails, chunks[max_chunks + j] 
 constexpr uint32_t kCntSteal = 32, kStealStride = 32;
 constexpr uint32_t kSchedCounters = kCntSteal + 8 * kStealStride;
 #else
-constexpr uint32_t kSchedCounters = 4;
+constexpr uint32_t kSchedCounters = 16;
 #endif
 // sorted[] entry of a packet the crypto kernel must skip (the device receive's refused packets)
 constexpr uint32_t kSortedSkip = 0xFFFFFFFFu;
@@ -96,9 +120,8 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
     uint32_t* binof;      // [n] sub-bin (bin * kSubBins + sub) of each packet
     uint32_t* binpos;     // [n] rank of each packet within its bin (the histogram atomic's return)
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
-    uint4* chunks;        // [max_chunks + max_short] {start in sorted, count (<= kMaxChunkPkts), key_id, size class | lg << 8}
-    uint32_t max_chunks;  // fronts from 0 up, long tails from max_chunks - 1 down
-    uint32_t max_short;   // short tails from max_chunks up
+    uint4* chunks;        // [kBuckets][max_chunks] chunk records (chunk_w), bucket b's from b * max_chunks
+    uint32_t max_chunks;  // the batch's chunks at most, and each bucket's capacity
     uint32_t* tcnt;       // [kTileMax][sched_tile_words] per-tile bin counts, 16 bits each (null: no tiles)
     uint32_t* tpre;       // [kTileMax][nbins] each (tile, bin)'s offset inside its bin
 };
@@ -108,17 +131,6 @@ __host__ __device__ inline uint32_t sched_max_chunks(uint32_t n, uint32_t max_ke
     const uint32_t nb = sched_nbins(max_keys);
     return (n + kChunkPkts - 1u) / kChunkPkts + (n < nb ? n : nb);
 }
-// at most one tail per bin
-__host__ __device__ inline uint32_t sched_max_short(uint32_t n, uint32_t max_keys) {
-    const uint32_t nb = sched_nbins(max_keys);
-    return n < nb ? n : nb;
-}
-// The tails are handed out longest first (a workgroup's waves take them as their front chunks end,
-// and a long tail taken last runs on with few waves beside it): a tail at 2^lg lanes of size class
-// cls takes up to 2^(cls + 2 - lg) rounds; "long" (>= 16: 1300-B packets at 8 lanes, 11 rounds)
-// ahead of "short" (1300 B at 16 lanes: 6 rounds; everything shorter).
-__host__ __device__ inline bool sched_tail_long(uint32_t cls, uint32_t lg) { return cls >= lg + 2u; }
-
 }  // namespace neb
 
 // Host launcher (sched.hip): the three binning passes on stream s. The workspace's counters and

@@ -5,8 +5,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <hipcub/hipcub.hpp>
-
 #include "sched.hpp"
 
 namespace neb {
@@ -63,79 +61,129 @@ __device__ __forceinline__ void sched_clear_cursors(const SchedWs& ws) {
     for (uint32_t i = threadIdx.x; i < kSchedCounters; i += blockDim.x) ws.counters[i] = 0;
 }
 
-// pass 2: every non-empty bin reserves its range of `sorted` and its chunks. The reservations are
-// aggregated per workgroup (block scans, then one atomic per counter and workgroup): one atomic per
-// bin put ~4096 returning atomics on a single word for a 4096-tunnel batch. blk: this workgroup's
-// index among the pass's (the grid covers the bins exactly once, kAllocThreads threads each).
+// pass 2 (round 6: per key): every non-empty bin reserves its range of `sorted`, and each key's
+// chunks are written into the cost buckets (sched_key_chunks). One thread per bin, the 8 bins
+// (size classes) of a key on 8 neighbouring lanes, so a key's plan is computed beside its counts
+// (shuffles within the 8 lanes) and every class emits its own chunks in parallel. Reservations go
+// through LDS atomics per workgroup, then one global atomic per counter and workgroup (one atomic
+// per bin put ~4096 returning atomics on a single word for a 4096-tunnel batch). blk: this
+// workgroup's index among the pass's (the grid covers the 8 (max_keys + 1) bins once, kAllocThreads
+// each).
 constexpr int kAllocThreads = 256;
-template <uint32_t SUB>
+constexpr uint32_t kAllocCounts = 1u + kBuckets;  // packets, then chunks per bucket
 struct SchedAllocLds {
-    typename hipcub::BlockScan<uint32_t, kAllocThreads>::TempStorage tmp;
-    uint32_t wg_base[4];
+    uint32_t cnt[kAllocCounts];
+    uint32_t wg_base[kAllocCounts];
 };
+
+// The leftover group of class i of one key (counts c[cls], class cls's range of `sorted` from
+// bstart[cls]): the key's leftovers (c mod 16 per class) are planned largest class first, each one
+// group at sched_tail_lg lanes that also takes as many of the next smaller class's leftover packets as
+// it has free slots (its second segment; a smaller class needs no more rounds at the same lanes).
+// Returns false when class i has no group of its own (no leftover, or all of it rode along).
+__device__ __forceinline__ bool sched_leftover_group(uint32_t i, uint32_t key, const uint32_t (&c)[kSizeClasses],
+                                                     const uint32_t (&bstart)[kSizeClasses], uint32_t& bucket,
+                                                     uint4& rec) {
+    uint32_t left[kSizeClasses], lpos[kSizeClasses];
+#pragma unroll
+    for (uint32_t k = 0; k < kSizeClasses; k++) {
+        left[k] = c[k] % kChunkPkts;
+        lpos[k] = bstart[k] + c[k] / kChunkPkts * kChunkPkts;
+    }
+    bool mine = false;
+#pragma unroll
+    for (int g = (int)kSizeClasses - 1; g >= 0; g--) {
+        const uint32_t L = left[g];
+        if (L == 0u) continue;
+        const uint32_t lg = sched_tail_lg(L, (uint32_t)g), free = (64u >> lg) - L;
+        uint32_t s1 = 0, c1 = 0;
+        bool found = false;
+#pragma unroll
+        for (int j = g - 1; j >= 0; j--) {  // the next smaller class with a leftover fills the free slots
+            if (!found && left[j] != 0u) {
+                found = true;
+                c1 = min(free, left[j]);
+                s1 = lpos[j];
+                lpos[j] += c1;
+                left[j] -= c1;
+            }
+        }
+        if ((uint32_t)g == i) {
+            const bool front = lg == 2u;
+            bucket = sched_bucket(front ? sched_front_cost(1u, (uint32_t)g) : sched_tail_cost((uint32_t)g, lg));
+            rec = make_uint4(lpos[g], s1, key, chunk_w(L, c1, lg, front, (uint32_t)g));
+            mine = true;
+        }
+    }
+    return mine;
+}
+
 template <uint32_t SUB>
 __device__ __forceinline__ void sched_alloc_block(uint32_t max_keys, const SchedWs& ws, uint32_t blk,
-                                                  SchedAllocLds<SUB>& sl) {
-    using Scan = hipcub::BlockScan<uint32_t, kAllocThreads>;
-    const uint32_t nb = sched_nbins(max_keys);
-    const uint32_t b = blk * kAllocThreads + threadIdx.x;
+                                                  SchedAllocLds& sl) {
+    const uint32_t K1 = max_keys + 1u;
+    const uint32_t t = blk * kAllocThreads + threadIdx.x, key = t / kSizeClasses, cls = t % kSizeClasses;
+    const uint32_t lane = threadIdx.x & 63u, grp = lane & ~(kSizeClasses - 1u);
+    const bool valid = key < K1;
+    const uint32_t bin = cls * K1 + key;
+    if (threadIdx.x < kAllocCounts) sl.cnt[threadIdx.x] = 0;
     uint32_t sc[SUB], c = 0;
 #pragma unroll
     for (uint32_t j = 0; j < SUB; j++) {
-        sc[j] = b < nb ? ws.hist[b * SUB + j] : 0u;
+        sc[j] = valid ? ws.hist[bin * SUB + j] : 0u;
         c += sc[j];
     }
     if (c)  // clear for the next batch
 #pragma unroll
-        for (uint32_t j = 0; j < SUB; j++) ws.hist[b * SUB + j] = 0u;
-    const uint32_t key = b % (max_keys + 1u), cls = b / (max_keys + 1u);
-    const uint32_t nfull = c / kChunkPkts, tail = c % kChunkPkts;
-    const uint32_t lg = tail ? sched_tail_lg(tail, cls) : 2u;
-    // the bin's first `fpk` packets run in groups at 4 lanes per packet (a 9-15 packet tail is a
-    // partial group), packed sched_groups(cls) groups to a front chunk; a tail at 8 or 16 lanes is
-    // one back chunk. The crypto kernels take the front chunks, then the back ones. Front <= n/16 +
-    // bins, back <= bins and front + back <= n/16 + min(n, bins): the ranges never meet inside
-    // max_chunks (sched_max_chunks).
-    const uint32_t fpk = nfull * kChunkPkts + (tail && lg == 2u ? tail : 0u);
-    const uint32_t cpk = sched_groups(cls) * kChunkPkts;  // packets per front chunk
-    const uint32_t nfront = (fpk + cpk - 1u) / cpk;
-    const bool back = tail && lg != 2u;
-    const bool is_long = back && sched_tail_long(cls, lg);
-    const uint32_t nlong = is_long ? 1u : 0u, nshort = back && !is_long ? 1u : 0u;
-    uint32_t off_p, off_f, off_l, off_s, tot_p, tot_f, tot_l, tot_s;
-    Scan(sl.tmp).ExclusiveSum(c, off_p, tot_p);
+        for (uint32_t j = 0; j < SUB; j++) ws.hist[bin * SUB + j] = 0u;
+    uint32_t cc[kSizeClasses];  // the key's counts
+#pragma unroll
+    for (uint32_t k = 0; k < kSizeClasses; k++) cc[k] = (uint32_t)__shfl((int)c, (int)(grp + k));
+    // this class's front chunks: nfc of g groups, the last one of lastg; and the leftover group
+    const uint32_t nf = c / kChunkPkts, g = sched_groups(cls);
+    const uint32_t nfc = (nf + g - 1u) / g, lastg = nf - (nfc ? nfc - 1u : 0u) * g;
+    const uint32_t bfull = sched_bucket(sched_front_cost(g, cls)), blast = sched_bucket(sched_front_cost(lastg, cls));
+    uint32_t lb = 0;
+    uint4 lrec;
+    const uint32_t zero[kSizeClasses] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool has_left = c != 0u && sched_leftover_group(cls, key, cc, zero, lb, lrec);
     __syncthreads();
-    Scan(sl.tmp).ExclusiveSum(nfront, off_f, tot_f);
+    // reservations inside the workgroup (LDS atomics), then the workgroup's totals globally
+    uint32_t o_pk = 0, o_full = 0, o_last = 0, o_left = 0;
+    if (c) o_pk = atomicAdd(&sl.cnt[0], c);
+    if (nfc > 1u) o_full = atomicAdd(&sl.cnt[1u + bfull], nfc - 1u);
+    if (nfc) o_last = atomicAdd(&sl.cnt[1u + blast], 1u);
+    if (has_left) o_left = atomicAdd(&sl.cnt[1u + lb], 1u);
     __syncthreads();
-    Scan(sl.tmp).ExclusiveSum(nlong, off_l, tot_l);
-    __syncthreads();
-    Scan(sl.tmp).ExclusiveSum(nshort, off_s, tot_s);
-    if (threadIdx.x == 0) {
-        sl.wg_base[0] = tot_p ? atomicAdd(&ws.counters[kCntPackets], tot_p) : 0u;
-        sl.wg_base[1] = tot_f ? atomicAdd(&ws.counters[kCntFrontChunks], tot_f) : 0u;
-        sl.wg_base[2] = tot_l ? atomicAdd(&ws.counters[kCntBackChunks], tot_l) : 0u;
-        sl.wg_base[3] = tot_s ? atomicAdd(&ws.counters[kCntShortChunks], tot_s) : 0u;
+    if (threadIdx.x < kAllocCounts) {
+        const uint32_t all = sl.cnt[threadIdx.x];
+        sl.wg_base[threadIdx.x] = all ? atomicAdd(&ws.counters[threadIdx.x == 0 ? kCntPackets : kCntBucket + threadIdx.x - 1u], all) : 0u;
     }
     __syncthreads();
-    if (c == 0u) return;
-    const uint32_t base = sl.wg_base[0] + off_p;
-    uint32_t sb = base;
+    // the bin's range of sorted[] (its sub-bins in turn), and the key's other bins' starts
+    const uint32_t base = sl.wg_base[0] + o_pk;
+    uint32_t pos = base;
 #pragma unroll
     for (uint32_t j = 0; j < SUB; j++) {
-        ws.base[b * SUB + j] = sb;
-        sb += sc[j];
+        if (c) ws.base[bin * SUB + j] = pos;
+        pos += sc[j];
     }
-    const uint32_t cf = sl.wg_base[1] + off_f;
-    for (uint32_t j = 0; j < nfront && cf + j < ws.max_chunks; j++)
-        ws.chunks[cf + j] = make_uint4(base + j * cpk, min(cpk, fpk - j * cpk), key, cls | (2u << kChunkLgShift));
-    if (back) {
-        const uint4 ch = make_uint4(base + fpk, tail, key, cls | (lg << kChunkLgShift));
-        const uint32_t tl = sl.wg_base[2] + off_l, ts = sl.wg_base[3] + off_s;
-        if (is_long) {
-            if (tl < ws.max_chunks) ws.chunks[ws.max_chunks - 1u - tl] = ch;
-        } else if (ts < ws.max_short) {
-            ws.chunks[ws.max_chunks + ts] = ch;
-        }
+    uint32_t bs[kSizeClasses];
+#pragma unroll
+    for (uint32_t k = 0; k < kSizeClasses; k++) bs[k] = (uint32_t)__shfl((int)base, (int)(grp + k));
+    if (!c) return;
+    auto put = [&](uint32_t b, uint32_t slot, uint4 rec) {
+        if (slot < ws.max_chunks) ws.chunks[(size_t)b * ws.max_chunks + slot] = rec;
+    };
+    for (uint32_t j = 0; j < nfc; j++) {
+        const bool last = j + 1u == nfc;
+        const uint32_t gc = last ? lastg : g;
+        put(last ? blast : bfull, last ? sl.wg_base[1u + blast] + o_last : sl.wg_base[1u + bfull] + o_full + j,
+            make_uint4(base + j * g * kChunkPkts, 0u, key, chunk_w(gc * kChunkPkts, 0u, 2u, true, cls)));
+    }
+    if (has_left) {
+        sched_leftover_group(cls, key, cc, bs, lb, lrec);
+        put(lb, sl.wg_base[1u + lb] + o_left, lrec);
     }
 }
 

@@ -150,9 +150,10 @@ def test_binning_paths_vs_oracle(engine, oracle_mod, knobs, path, n, nkeys, size
 
 @pytest.mark.parametrize("max_keys", [1024, 4096])
 def test_tile_binning_lds_rows_vs_oracle(oracle_mod, knobs, max_keys):
-    """The tile binning's scatter with each tile's row of bin offsets in LDS (sched.hip), which the
-    shared 8192-slot engine's 65 544 bins do not fit: engines with 1024 and 4096 key slots (8200 /
-    32 776 bins), an IMIX batch over 1000 keys in 21 tiles, seal twice and open."""
+    """The tile binning (sched.hip) on engines with 1024 and 4096 key slots (8200 / 32 776 bins,
+    against the shared 8192-slot engine's 65 544): the counting pass's per-tile LDS histogram at
+    these sizes, the scan over the tiles, and the scatter reading each tile's bin offsets from its
+    row of tpre in global memory. An IMIX batch over 1000 keys in 21 tiles, seal twice and open."""
     from nebula_amd import Engine
 
     knobs(L.KNOB_TILE_BINS_FROM, 0)

@@ -2,6 +2,7 @@
 recvmmsg flush, connection_state.go:99-119) against the oracle's packet-by-packet receive loop
 (oracle/replay_oracle.py rx_sequential + oracle AEAD): statuses, every arena byte (refused packets
 untouched, forged ones zeroed, accepted ones decrypted in place), window state and counters."""
+import contextlib
 import os
 import random
 
@@ -57,7 +58,10 @@ def _expected(oracle_mod, R, alg, keys, arrivals, arena, pts, window_len, seeds,
 
 
 def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=None, installed=None, seed=1,
-         lens=None, device=False, strict=False, count=None):
+         lens=None, device=False, strict=False, count=None, hint=False, knobs=()):
+    """hint: the device receive is told the batch's one tunnel key (key_hint = the first arrival's
+    slot), so its open runs the single-key kernels' RX instantiations; knobs: (knob, value) pairs set
+    around the receive."""
     import replay_oracle as R
     from nebula_amd.connection_state import Bits, rx_open_batch
     from nebula_amd.noiseutil import CipherAESGCM, CipherChaChaPoly
@@ -98,9 +102,13 @@ def _run(engine, oracle_mod, alg, arrivals, ntunnels=3, window_len=8192, seeds=N
                 d_desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
                 d_arena = torch.from_numpy(arena).to(dev)
                 d_status = torch.full((len(d),), -1, dtype=torch.int32, device=dev)
+                key_hint = slot_of[arrivals[0][0]] if hint else L.KEYS_MIXED
                 # strict: the parallel form only: the call fails if any window needs the host
-                with L.knob(L.KNOB_RX_STRICT, 1 if strict else 0):
-                    rx_open_batch_device(engine, alg, dw, d_desc, d_arena, d_status)
+                with contextlib.ExitStack() as knob_stack:
+                    knob_stack.enter_context(L.knob(L.KNOB_RX_STRICT, 1 if strict else 0))
+                    for k, v in knobs:
+                        knob_stack.enter_context(L.knob(k, v))
+                    rx_open_batch_device(engine, alg, dw, d_desc, d_arena, d_status, key_hint=key_hint)
                 torch.cuda.synchronize()
                 got = d_status.cpu().numpy()
                 arena[:] = d_arena.cpu().numpy()
@@ -219,6 +227,43 @@ def test_rx_batch_large(engine, oracle_mod, device):
             arr.append((t, cur[t], False))
     _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=6, window_len=256, seed=5, lens=[0, 1, 16, 40, 100],
          device=device)
+
+
+def _one_tunnel_arrivals(rng, n, forge):
+    arr = _random_arrivals(rng, n, 1, forge)
+    arr += [(0, c, False) for (_, c, f) in arr[:50] if not f]  # replays of accepted packets: REPLAY, untouched
+    return arr
+
+
+@pytest.mark.parametrize("n,grid", [(700, 0), (20000, 0), (20000, 3)])
+@pytest.mark.parametrize("forge", [0.0, 0.03])
+def test_rx_device_single_key_hint(engine, oracle_mod, n, grid, forge):
+    """A one-tunnel receive told its key (key_hint): the open runs the single-key kernels' RX
+    instantiations behind the admission mask — gcm_single_tail_kernel<RX> for a small batch,
+    gcm_single_kernel<RX> for a large one, and (grid capped at 3 workgroups, NEB_KNOB_SINGLE_MAX_GRID)
+    both, the tail taking the partial last pass. A refused packet must keep its REPLAY status and its
+    bytes; forged packets, replays of accepted ones and in-batch duplicates included."""
+    rng = random.Random(n * 7 + grid + int(forge * 100))
+    arr = _one_tunnel_arrivals(rng, n, forge)
+    knobs = [(L.KNOB_SINGLE_MAX_GRID, grid)] if grid else []
+    st = _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=1, window_len=1024, seed=21, lens=[0, 16, 90, 600],
+              device=True, hint=True, knobs=knobs, strict=forge == 0.0)
+    assert (st == L.STATUS_REPLAY).sum() >= 50
+    if forge:
+        assert (st == L.STATUS_AUTH_FAILED).sum() > 0
+
+
+@pytest.mark.parametrize("n", [3000, 20000])
+def test_rx_device_mixed_key_unprebinned(engine, oracle_mod, n):
+    """A mixed-key receive binned by the open itself (NEB_KNOB_SUB_BINS_FROM 0: as a batch past the
+    sub-bin threshold is, instead of prebinned by the plan's launches): gcm_chunk_kernel<open, RX>
+    with the admission mask read per packet. Replays, duplicates and forgeries over 8 tunnels against
+    the sequential oracle; refused packets untouched."""
+    rng = random.Random(n)
+    arr = _random_arrivals(rng, n, 8, 0.04)
+    st = _run(engine, oracle_mod, L.ALG_AESGCM, arr, ntunnels=8, window_len=128, seed=23, lens=[0, 16, 90, 600, 1300],
+              device=True, knobs=[(L.KNOB_SUB_BINS_FROM, 0)])
+    assert (st == L.STATUS_REPLAY).sum() > 0 and (st == L.STATUS_AUTH_FAILED).sum() > 0
 
 
 @pytest.mark.parametrize("length", [1, 64, 256, 8192])

@@ -1,10 +1,12 @@
 """CPU: the mixed-key scheduler's chunk plan (tools/sched_model.py, rule for rule as
-nebula_amd/csrc/sched.hpp / sched.hip) on the BASELINE configs' key and size mixes and on random
-batches: every packet in exactly one chunk, one key and one size class per chunk, no chunk wider
-than a wave, short classes never run at more lanes than they have blocks, the front and tail
-ranges inside the workspace bounds the engine allocates (sched_max_chunks / sched_max_short), and
-C3's lane utilisation as DESIGN.md §3.2 states it. The GPU tests check the ciphertexts these plans
-produce (tests/test_gpu_parity.py); this pins the plan's own arithmetic."""
+nebula_amd/csrc/sched.hpp / sched_body.hpp) on the BASELINE configs' key and size mixes and on random
+batches: every packet in exactly one chunk, one key per chunk, segment 0 of one size class and
+segment 1 (packets riding in a leftover group's free slots) of a smaller class, no chunk wider than
+a wave, short classes never run at more lanes than they have blocks, the chunks inside the
+workspace bound the engine allocates (sched_max_chunks, and each cost bucket's capacity), the
+buckets ordered longest first, and C3's lane utilisation as DESIGN.md §3.2 states it. The GPU tests
+check the ciphertexts these plans produce (tests/test_gpu_parity.py); this pins the plan's own
+arithmetic."""
 import os
 import sys
 
@@ -18,32 +20,35 @@ import sched_model as M  # noqa: E402
 from nebula_amd import workload as W  # noqa: E402
 
 
-def _check(key_id, aad_len, length, max_keys, split_cls=M.SPLIT_TAIL_CLASS):
+def _check(key_id, aad_len, length, max_keys):
     n = len(key_id)
-    chunks = M.plan(key_id, aad_len, length, max_keys, split_cls)
+    chunks = M.plan(key_id, aad_len, length, max_keys)
     seen = np.concatenate([c.packets for c in chunks]) if chunks else np.zeros(0, np.int64)
     assert np.array_equal(np.sort(seen), np.arange(n)), "every packet in exactly one chunk"
     cls = M.size_class(aad_len, length)
     key = np.where(key_id < max_keys, key_id, max_keys)
     nblk = M.blocks(aad_len, length)
     for c in chunks:
-        assert (key[c.packets] == c.key).all() and (cls[c.packets] == c.cls).all()
+        assert (key[c.packets] == c.key).all()
+        seg0, seg1 = c.packets[:c.count0], c.packets[c.count0:]
+        assert len(seg0) >= 1 and (cls[seg0] == c.cls).all()
+        assert (cls[seg1] < c.cls).all(), "absorbed packets come from a smaller class"
+        assert len(c.packets) <= 255 and len(seg1) <= 15  # the record's 8-bit counts
         lpp = 1 << c.lg
         if c.kind == "front":
             assert c.lg == 2 and 1 <= len(c.packets) <= M.groups(c.cls) * M.CHUNK_PKTS
+            assert len(seg1) == 0 or len(c.packets) <= M.CHUNK_PKTS  # a leftover group only
         else:
             assert c.lg in (3, 4) and 1 <= len(c.packets) * lpp <= M.WAVE
-            assert c.kind == ("long" if M.tail_long(c.cls, c.lg) else "short")
             # capped for short classes: at 2**lg lanes the shortest class-cls packet has a block per lane
             assert (c.cls, c.lg) not in ((0, 3), (0, 4), (1, 4))
-            assert nblk[c.packets].max() > lpp // 2 or c.cls == 0
-    nfront = sum(c.kind == "front" for c in chunks)
-    nlong = sum(c.kind == "long" for c in chunks)
-    nshort = sum(c.kind == "short" for c in chunks)
+            assert nblk[seg0].max() > lpp // 2 or c.cls == 0
+        # an absorbed packet needs no more rounds than segment 0's class allows at these lanes
+        if len(seg1):
+            assert ((nblk[seg1] + lpp - 1) // lpp).max() <= ((4 << c.cls) + lpp - 1) // lpp
     # the engine sizes the workspace for max(n, 64 Ki) packets (engine.cpp sched_reserve); the bound
-    # must hold for n itself, so the fronts (from 0 up) never meet the long tails (from the top down)
-    assert nfront + nlong <= M.max_chunks(n, max_keys)
-    assert nshort <= M.max_short(n, max_keys)
+    # must hold for n itself: all chunks, and so every bucket, within max_chunks
+    assert len(chunks) <= M.max_chunks(n, max_keys)
     return chunks, nblk
 
 
@@ -57,7 +62,7 @@ def test_baseline_mixed_configs(idx):
     chunks, nblk = _check(kid, aad, lens, 4096)
     if idx == 2:
         # C3: Poisson(16) packets per key; with the 8/16-lane tails 86.7% of the lane-rounds carry a
-        # block; the round-4 split of 9-12 packet tails would make it 89.4%
+        # block; one size class, so nothing is absorbed
         used = int(nblk.sum())
         spent = sum(M.lane_rounds(c, nblk) for c in chunks)
         assert abs(used / spent - 0.867) < 0.005
@@ -65,8 +70,22 @@ def test_baseline_mixed_configs(idx):
         tails = len(chunks) - fronts
         # ≈ 16 fronts and 7 tails per workgroup on 256 CUs (the wave timeline)
         assert 15 <= fronts / 256 <= 17 and 6 <= tails / 256 <= 8
-        split, _ = _check(kid, aad, lens, 4096, split_cls=M.EXPERIMENT_SPLIT_CLASS)
-        assert abs(used / sum(M.lane_rounds(c, nblk) for c in split) - 0.894) < 0.005
+        # longest first: the 21-round fronts, then 8-lane tails (11 rounds), then 16-lane (6)
+        assert [c.bucket for c in chunks if c.kind == "front"] == [0] * fronts
+        assert {(c.lg, c.bucket) for c in chunks if c.kind == "tail"} == {(3, 1), (4, 3)}
+
+
+def test_c5_shard_absorbs_leftovers():
+    """C5's 8-GPU shard (131 072 IMIX packets over 4096 keys, 32 per key): a key's leftover groups
+    take the next smaller class's leftover packets, which removes chunks and lane-rounds against
+    planning each (class, key) bin alone."""
+    full = W.config(4, scale=1.0 / 8)
+    d = full.desc
+    chunks, nblk = _check(d["key_id"], d["aad_len"], d["len"], 4096)
+    absorbed = sum(len(c.packets) - c.count0 for c in chunks)
+    assert absorbed > 0.04 * len(d)
+    spent = sum(M.lane_rounds(c, nblk) for c in chunks) // M.WAVE
+    assert len(chunks) < 14000 and spent < 68000  # per-bin plans: 14 564 chunks, ≈ 73 000 wave-rounds
 
 
 def test_random_batches():
@@ -81,21 +100,27 @@ def test_random_batches():
 
 
 def test_bin_tail_shapes():
-    """One bin of c packets, c = 1..40: c // 16 full groups, then a 9-15 packet tail as a partial
-    4-lane group, a 5-8 packet tail at 8 lanes, a 1-4 packet tail at 16 (1300-B packets); with the
-    experiment's split, a 9-12 packet tail as 8 packets at 8 lanes and the rest at 16."""
-    for split_cls in (M.SPLIT_TAIL_CLASS, M.EXPERIMENT_SPLIT_CLASS):
-        for c in range(1, 41):
-            kid = np.zeros(c, np.uint32)
-            chunks, _ = _check(kid, np.full(c, 16, np.uint32), np.full(c, 1300, np.uint32), 4, split_cls)
-            t = c % 16
-            lo = 13 if split_cls < 99 else 9
-            front = [len(x.packets) for x in chunks if x.kind == "front"]
-            back = [(len(x.packets), x.lg) for x in chunks if x.kind != "front"]
-            assert sum(front) == c // 16 * 16 + (t if t >= lo else 0)
-            if t == 0 or t >= lo:
-                assert back == []
-            elif t >= 9:
-                assert back == [(8, 3), (t - 8, 4)]
-            else:
-                assert back == [(t, 4 if t <= 4 else 3)]
+    """One bin of c packets, c = 1..40: c // 16 full groups, then a 9-15 packet leftover as a partial
+    4-lane group, a 5-8 packet leftover at 8 lanes, a 1-4 packet leftover at 16 (1300-B packets)."""
+    for c in range(1, 41):
+        kid = np.zeros(c, np.uint32)
+        chunks, _ = _check(kid, np.full(c, 16, np.uint32), np.full(c, 1300, np.uint32), 4)
+        t = c % 16
+        front = [len(x.packets) for x in chunks if x.kind == "front"]
+        back = [(len(x.packets), x.lg) for x in chunks if x.kind != "front"]
+        assert sum(front) == c // 16 * 16 + (t if t >= 9 else 0)
+        if t == 0 or t >= 9:
+            assert back == []
+        else:
+            assert back == [(t, 4 if t <= 4 else 3)]
+
+
+def test_leftover_absorption_rules():
+    """3 large (1300 B) + 6 medium (576 B) + 2 small (90 B) packets of one key: the large leftover
+    at 16 lanes takes 1 medium packet, the 5 remaining medium packets at 8 lanes take 3 small ones
+    (the 2 there are), so the key runs 2 chunks instead of 3."""
+    lens = np.array([1300] * 3 + [576] * 6 + [90] * 2, np.uint32)
+    kid = np.zeros(len(lens), np.uint32)
+    chunks, _ = _check(kid, np.full(len(lens), 16, np.uint32), lens, 4)
+    shapes = sorted((c.cls, c.lg, c.count0, len(c.packets) - c.count0) for c in chunks)
+    assert shapes == [(4, 3, 5, 2), (5, 4, 3, 1)]

@@ -58,8 +58,7 @@ def main(lat=3.2, ov=1.0):
     aad = np.full(n, 16, np.uint32)
     plan = M.plan(kid, aad, lens, 4096)
     nblk = M.blocks(aad, lens)
-    order = [c for c in plan if c.kind == "front"] + [c for c in plan if c.kind == "long"] + \
-        [c for c in plan if c.kind == "short"]
+    order = sorted(plan, key=lambda c: c.bucket)  # the kernel's order: cost buckets, longest first
     rounds = [chunk_rounds(c, nblk) for c in order]
     spans = [workgroup_span(rounds[w::CUS], lat, ov) for w in range(CUS)]
     bound = (sum(rounds) + ov * len(rounds)) / CUS * T16 / WAVES

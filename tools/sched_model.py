@@ -1,5 +1,6 @@
 """CPU model of the mixed-key scheduler (nebula_amd/csrc/sched.hpp, sched.hip): the (size class,
-key) binning, the chunk plan of sched_alloc_kernel and the workspace bounds, rule for rule, so the
+key) binning, the per-key chunk plan of sched_alloc_kernel (round 6: a key's leftovers planned
+together, longest-first cost buckets) and the workspace bounds, rule for rule, so the
 tests can check the plan's invariants and its lane utilisation on the BASELINE configs' shapes
 without a GPU. The order of bins and of packets inside a bin is arbitrary on the device (atomics);
 the model fixes one order, and no invariant checked depends on it."""
@@ -30,20 +31,29 @@ def tail_lg(count: int, cls: int) -> int:
     return min(fit, size)
 
 
-SPLIT_TAIL_CLASS = 99  # the product never splits a tail (sched.hip)
-# the round-4 experiment: from size class 4 a 9-12 packet tail = 8 packets at 8 lanes + the rest at
-# 16. More lane-rounds busy in this model (C3 0.867 -> 0.894), slower on the GPU (each extra chunk
-# pays its key staging and tree final: C3 469-472 -> 456-459 GiB/s, profiles/r4/split_tails.log)
-EXPERIMENT_SPLIT_CLASS = 4
-
-
 def groups(cls: int) -> int:
     """sched_groups: groups of 16 packets per front chunk."""
     return 1 if cls >= 3 else 8 >> cls
 
 
-def tail_long(cls: int, lg: int) -> bool:
-    return cls >= lg + 2
+BUCKETS = 8
+
+
+def bucket(cost: int) -> int:
+    """sched_bucket: cost (rounds at the class's upper bound + finals) -> bucket, longest first."""
+    for b, lo in enumerate((24, 16, 12, 9, 7, 5, 3)):
+        if cost >= lo:
+            return b
+    return 7
+
+
+def front_cost(ngroups: int, cls: int) -> int:
+    return ngroups * ((1 << cls) + 1)
+
+
+def tail_cost(cls: int, lg: int) -> int:
+    r = ((1 << cls) * 4) >> lg
+    return max(r, 1) + 2
 
 
 def nbins(max_keys: int) -> int:
@@ -55,48 +65,66 @@ def max_chunks(n: int, max_keys: int) -> int:
     return (n + CHUNK_PKTS - 1) // CHUNK_PKTS + min(n, nb)
 
 
-def max_short(n: int, max_keys: int) -> int:
-    return min(n, nbins(max_keys))
-
-
 @dataclass
 class Chunk:
-    kind: str          # "front", "long" or "short"
-    packets: np.ndarray  # packet indices (a range of `sorted`)
+    kind: str            # "front" (4-lane groups) or "tail" (one group at 8 or 16 lanes)
+    packets: np.ndarray  # packet indices: segment 0 (class cls), then segment 1 (a smaller class)
     key: int
-    cls: int
-    lg: int            # lanes per packet = 2**lg
+    cls: int             # segment 0's size class
+    lg: int              # lanes per packet = 2**lg
+    count0: int          # packets in segment 0
+    bucket: int
 
 
-def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: int,
-         split_cls: int = SPLIT_TAIL_CLASS) -> List[Chunk]:
-    """The chunks sched_alloc_kernel writes for one batch (every bin, its front chunks and tail)."""
+def key_chunks(key: int, counts, starts):
+    """sched_key_chunks for one key: counts[cls] packets of class cls from starts[cls] in `sorted`.
+    Returns (kind, cls, lg, (start0, count0), (start1, count1), bucket) in emission order."""
+    out = []
+    left, lpos = [0] * SIZE_CLASSES, [0] * SIZE_CLASSES
+    for c in range(SIZE_CLASSES):
+        nf, g = counts[c] // CHUNK_PKTS, groups(c)
+        for j in range(0, nf, g):
+            gc = min(g, nf - j)
+            out.append(("front", c, 2, (starts[c] + j * CHUNK_PKTS, gc * CHUNK_PKTS), (0, 0), bucket(front_cost(gc, c))))
+        left[c] = counts[c] % CHUNK_PKTS
+        lpos[c] = starts[c] + nf * CHUNK_PKTS
+    for i in range(SIZE_CLASSES - 1, -1, -1):
+        L = left[i]
+        if L == 0:
+            continue
+        lg = tail_lg(L, i)
+        free = (64 >> lg) - L
+        s1 = c1 = 0
+        for j in range(i - 1, -1, -1):  # the next smaller class with a leftover fills the free slots
+            if left[j]:
+                c1 = min(free, left[j])
+                s1 = lpos[j]
+                lpos[j] += c1
+                left[j] -= c1
+                break
+        front = lg == 2
+        out.append(("front" if front else "tail", i, lg, (lpos[i], L), (s1, c1),
+                    bucket(front_cost(1, i) if front else tail_cost(i, lg))))
+    return out
+
+
+def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: int) -> List[Chunk]:
+    """The chunks sched_alloc_kernel writes for one batch: per key, its classes one after another in
+    `sorted`, and sched_key_chunks' records."""
     key = np.where(key_id < max_keys, key_id, max_keys).astype(np.int64)
     cls = size_class(aad_len, length)
-    b = cls * (max_keys + 1) + key
-    order = np.argsort(b, kind="stable")
-    sb = b[order]
-    starts = np.r_[0, np.flatnonzero(np.diff(sb)) + 1]
-    ends = np.r_[starts[1:], len(sb)]
+    order = np.lexsort((cls, key))  # sorted[]: key-major, classes in turn (any order inside a bin)
     out: List[Chunk] = []
-    for s, e in zip(starts, ends):
-        if s == e:
-            continue
-        bin_ = int(sb[s])
-        k, c = bin_ % (max_keys + 1), bin_ // (max_keys + 1)
-        cnt = int(e - s)
-        nfull, tail = divmod(cnt, CHUNK_PKTS)
-        lg = tail_lg(tail, c) if tail else 2
-        split = lg == 2 and 9 <= tail <= 12 and c >= split_cls
-        fpk = nfull * CHUNK_PKTS + (tail if tail and lg == 2 and not split else 0)
-        cpk = groups(c) * CHUNK_PKTS
-        for j in range(0, fpk, cpk):
-            out.append(Chunk("front", order[s + j:s + min(fpk, j + cpk)], k, c, 2))
-        if split:
-            out.append(Chunk("long" if tail_long(c, 3) else "short", order[s + fpk:s + fpk + 8], k, c, 3))
-            out.append(Chunk("long" if tail_long(c, 4) else "short", order[s + fpk + 8:e], k, c, 4))
-        elif tail and lg != 2:
-            out.append(Chunk("long" if tail_long(c, lg) else "short", order[s + fpk:e], k, c, lg))
+    sk, sc = key[order], cls[order]
+    kstarts = np.r_[0, np.flatnonzero(np.diff(sk)) + 1] if len(sk) else np.zeros(0, np.int64)
+    kends = np.r_[kstarts[1:], len(sk)]
+    for s, e in zip(kstarts, kends):
+        k = int(sk[s])
+        counts = [int((sc[s:e] == c).sum()) for c in range(SIZE_CLASSES)]
+        starts = list(s + np.r_[0, np.cumsum(counts)[:-1]])
+        for kind, c, lg, (s0, c0), (s1, c1), b in key_chunks(k, counts, starts):
+            pk = np.r_[order[s0:s0 + c0], order[s1:s1 + c1]].astype(np.int64)
+            out.append(Chunk(kind, pk, k, c, lg, c0, b))
     return out
 
 

@@ -36,6 +36,16 @@ def fetch(lib):
 
 def analyse(tr, waves_per_wg=16):
     a, c, t0, t1 = (tr[:, i].astype(np.int64) for i in range(4))
+    # phase records (trace build, round 6): per chunk {descriptor in | round keys in << 16, tables
+    # staged} and the groups' sums {desc | rounds << 16, final | finish << 16}, in 10-ns ticks
+    pa, pb = c == 0xFFFFFFFE, c == 0xFFFFFFFD
+    phases = None
+    if pa.any() and pb.any():
+        lo, hi = lambda x: (x & 0xFFFF) * TICK_NS / 1e3, lambda x: (x >> 16) * TICK_NS / 1e3
+        phases = {"chunk_desc": lo(t0[pa]), "round_keys": hi(t0[pa]), "stage": t1[pa] * TICK_NS / 1e3,
+                  "pkt_desc": lo(t0[pb]), "rounds": hi(t0[pb]), "final": lo(t1[pb]), "finish": hi(t1[pb])}
+    keep = ~(pa | pb)
+    a, c, t0, t1 = a[keep], c[keep], t0[keep], t1[keep]
     t1 = np.where(t1 < t0, t1 + (1 << 32), t1)
     wg, wave = a >> 20, (a >> 16) & 15
     start = c == 0xFFFFFFFF
@@ -66,6 +76,10 @@ def analyse(tr, waves_per_wg=16):
     step = max(1, nb // 40)
     out["active_waves_per_us"] = [int(x) for x in act[::step]]
     out["active_waves_step_us"] = step
+    if phases is not None:
+        out["phase_us_mean"] = {k: round(float(v.mean()), 2) for k, v in phases.items()}
+        out["phase_us_total_per_wave"] = {k: round(float(v.sum()) / max(1, len(np.unique(a[start] >> 16))), 2)
+                                          for k, v in phases.items()}
     # chunk durations by kind
     kinds = {}
     for f, l, n_, d in zip(full[ch], lg[ch], count[ch], dur[ch]):
@@ -108,6 +122,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--shard-of", type=int, default=0, help="--config 4: shard 0 of the 1 Mi batch split N ways")
     args = ap.parse_args()
     if args.out:
         os.makedirs(os.path.dirname(args.out), exist_ok=True)
@@ -124,7 +139,7 @@ def main():
     lib.neb_debug_wave_trace.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     b = {1: lambda: W.make_batch(L.ALG_AESGCM, 65536, 1, name="C2"),
          2: lambda: W.make_batch(L.ALG_AESGCM, 65536, 4096, name="C3"),
-         4: lambda: W.config(4)}[args.config]()
+         4: lambda: W.shard(W.config(4), 0, args.shard_of) if args.shard_of else W.config(4)}[args.config]()
     eng = Engine(0, max_keys=max(4096, b.nkeys))
     ciphers = install_keys(eng, b)
     db = DeviceBatch(eng, b, ciphers)
