@@ -328,6 +328,9 @@ def main():
                     help="--config 4 on one rank: run only shard --shard-rank of the 1 Mi C5 batch split N ways "
                          "(the packets one GPU of an N-GPU run gets), so the per-GPU shape is measured on one GPU")
     ap.add_argument("--shard-rank", type=int, default=0)
+    ap.add_argument("--shard-by", choices=["key", "range"], default="key",
+                    help="--config 4 over N GPUs: each rank takes the tunnels with key_id mod N = rank (key: a "
+                         "tunnel's packets and state on one device), or a contiguous packet range (range)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # tests: launch + aggregation, no GPU
     args = ap.parse_args()
 
@@ -368,7 +371,8 @@ def main():
         2: (L.ALG_AESGCM, 65536, 4096),
         3: (L.ALG_CHACHAPOLY, 65536, 4096),
     }[cfg], seed=W.SEED ^ rank, name=f"C{cfg + 1}") if cfg in (0, 1, 2, 3) else \
-        W.shard(W.config(4), *((args.shard_rank, args.shard_of) if args.shard_of else (rank, world)))
+        (W.shard_by_key if args.shard_by == "key" else W.shard)(
+            W.config(4), *((args.shard_rank, args.shard_of) if args.shard_of else (rank, world)))
     workload_name = {0: "C1 AES-256-GCM, 1 tunnel key, 1024 x 1300 B packets, device-resident",
                      1: "C2 AES-256-GCM, 1 tunnel key, 65536 x 1300 B packets, device-resident",
                      2: "C3 AES-256-GCM, 4096 tunnel keys, 65536 x 1300 B packets, device-resident",
@@ -377,7 +381,8 @@ def main():
     if cfg == 4 and args.shard_of:
         if world != 1:
             raise SystemExit("--shard-of runs one shard on one rank")
-        workload_name += f": shard {args.shard_rank} of {args.shard_of} alone ({b.n} packets, one GPU's part)"
+        workload_name += (f": shard {args.shard_rank} of {args.shard_of} alone ({b.n} packets, one GPU's part; "
+                          + ("tunnels with key_id mod N = r)" if args.shard_by == "key" else "contiguous packet range)"))
     log(f"[rank {rank}] batch {b.name}: {b.n} pkts, {b.payload_bytes / 1e6:.1f} MB payload "
         f"({time.time() - t0:.1f}s to build)")
 

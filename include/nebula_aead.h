@@ -143,7 +143,12 @@ enum {
     NEB_KNOB_TILE_BINS_FROM = 4,  /* NEB_TILE_BINS_FROM: mixed-key batches of at least this many packets bin
                                    * through per-workgroup LDS histograms (sched.hpp: no per-packet global
                                    * atomic); smaller ones through the atomic histogram */
-    NEB_KNOB_COUNT = 5
+    NEB_KNOB_SMALL_BATCH = 5,     /* NEB_SMALL_BATCH: a mixed-key AES-GCM batch with fewer packets than this
+                                   * per resident wave of the chunk kernel (16 per CU) is chunked finer, up to
+                                   * NEB_KNOB_FRONT_GROUPS groups per chunk (default 48; 0: never) */
+    NEB_KNOB_FRONT_GROUPS = 6,    /* NEB_FRONT_GROUPS: the 16-packet groups per front chunk of the short size
+                                   * classes in such a batch at most (default 1; the classes' own: up to 8) */
+    NEB_KNOB_COUNT = 7
 };
 NEB_API int neb_set_knob(int knob, int64_t value);
 NEB_API int64_t neb_get_knob(int knob); /* -1 for an unknown knob */

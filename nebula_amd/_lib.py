@@ -44,6 +44,7 @@ REJECT_AFTER_MESSAGES = (1 << 64) - 1 - REJECT_HEADROOM
 KEYS_MIXED = 0xFFFFFFFF
 # neb_set_knob (include/nebula_aead.h)
 KNOB_HOST_MODE, KNOB_SUB_BINS_FROM, KNOB_SINGLE_MAX_GRID, KNOB_RX_STRICT, KNOB_TILE_BINS_FROM = 0, 1, 2, 3, 4
+KNOB_SMALL_BATCH, KNOB_FRONT_GROUPS = 5, 6
 RX_OWN_SOURCE = 0x80000000  # or-ed into neb_rx_packet.len: outside.go:66-74 refused the datagram
 
 # neb_desc (include/nebula_aead.h)

@@ -39,6 +39,13 @@
 #include "sched.hpp"
 #include "timing.hpp"
 
+// ISA region markers for tools/r6/isa_regions.py (an analysis build only: -DNEB_ISA_MARKS)
+#ifdef NEB_ISA_MARKS
+#define NEB_MARK(x) asm volatile(";NEBMARK " #x)
+#else
+#define NEB_MARK(x) ((void)0)
+#endif
+
 namespace neb {
 
 // ------------------------------------------------------------------------------------------
@@ -990,6 +997,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                                                  const neb_desc* own = nullptr) {
     const uint32_t LPP = 1u << lg;
     const uint32_t l = lane & (LPP - 1u);
+    NEB_MARK(grp_begin);
 #ifdef NEB_WAVE_TRACE
     const uint64_t tq0 = phase_now();
 #endif
@@ -1031,6 +1039,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         CtrConst cc{};
         if constexpr (CM == 2) cc = aes_ctr_prep8(c1, c2, T, rk);
         else if constexpr (CM == 1) cc = aes_ctr_prep(c1, c2, T, rk);
+        NEB_MARK(ctr_done);
         // The common round: every active lane holds a full payload block with a 16-B aligned
         // destination (the arena base counts too: a caller may pass an arena at any byte address);
         // a source off 16-B alignment (a TX segment inside its TUN read) is read as two aligned
@@ -1083,6 +1092,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
         // one round on the LDS: GHASH of the previous rounds first, then this round's T-table AES
         // (one phase's registers at a time)
         auto tround = [&](uint32_t r) {
+            NEB_MARK(round_begin);
             if (r < sh.R) {
                 const LaneBlock b = lane_block(sh, r, l, lg);
                 const bool fast = fast_round(b);
@@ -1096,6 +1106,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
                 if (__any(b.is_ct || b.is_len)) ks = gcm_lane_ks<CM>(b, c1, c2, cc, T, rk);
                 io(b, G, ks, fast, pre);
             }
+            NEB_MARK(round_end);
         };
         // rounds until no packet of the wave has one left (a ballot, no cross-lane reduction; a
         // shuffle max of the round counts first was 4-7% slower in the chunk kernel)
@@ -1122,7 +1133,9 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     const uint64_t tq2 = phase_now();
     phase_add(1, tq1, tq2);
 #endif
+    NEB_MARK(rounds_done);
     uint4 V = gh.final(A, lane, lg);  // every lane: the tree shuffles across the packet's lanes
+    NEB_MARK(final_done);
 #ifdef NEB_WAVE_TRACE
     const uint64_t tq3 = phase_now();
     phase_add(2, tq2, tq3);
@@ -1137,6 +1150,7 @@ __device__ __forceinline__ void gcm_packet_group(const GcmArgs& args, uint32_t p
     }
     if (run && gcm_finish<OPEN>(d, V, ej0.get(), lane, l, LPP, args.arena)) st = NEB_STATUS_AUTH_FAILED;
     if (valid && l == LPP - 1u) args.status[p] = (int32_t)st;
+    NEB_MARK(grp_end);
 #ifdef NEB_WAVE_TRACE
     phase_add(3, tq3, phase_now());
 #endif
@@ -1557,6 +1571,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
 #endif
     while (c < nch) {
         const uint4 ch = ch_next;
+        NEB_MARK(chunk_begin);
         const uint32_t cw = __builtin_amdgcn_readfirstlane(ch.w);
         const bool full = (cw >> 20) & 1u;  // 4-lane groups (front), or one group at 8 or 16 lanes
 #ifdef NEB_WAVE_TRACE
@@ -1589,6 +1604,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         uint64_t tcs = tck;
 #endif
         if (full) {
+            NEB_MARK(stage_full);
             stage_chunk_tables<true>(rec, ln, 2u, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1607,6 +1623,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
             }
         } else {
             const uint32_t lg = (cw >> kChunkLgShift) & 15u;  // 3 or 4
+            NEB_MARK(stage_tail);
             stage_chunk_tables<false>(rec, ln, lg, wtab, wpos);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1630,8 +1647,10 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
         // (tools/wave_trace.py). A/B, alternating (profiles/r5/ab_balance): C3 526-527 -> 536-537 GiB/s,
         // C5 504-505 -> 515-516; claiming ahead only while more than a round of chunks is left:
         // C3 537-542, C5 506-508.
+        NEB_MARK(chunk_claim);
         const uint32_t cn = claim();
         if (cn < nch) ch_next = chunk_at(cn);
+        NEB_MARK(chunk_claimed);
 #ifdef NEB_WAVE_TRACE
         wave_trace(lane, trace_k++,
                    blockIdx.x << 20 | wave << 16 | min(count, 255u) << 8 | ((cw >> kChunkLgShift) & 15u) << 4 |

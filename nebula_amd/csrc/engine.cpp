@@ -267,6 +267,10 @@ int64_t neb::knob(int k) {
         g_knobs[NEB_KNOB_RX_STRICT] = std::getenv("NEB_RXDEV_STRICT") ? 1 : 0;
         const char* tb = std::getenv("NEB_TILE_BINS_FROM");
         g_knobs[NEB_KNOB_TILE_BINS_FROM] = tb ? (int64_t)std::strtoull(tb, nullptr, 10) : (int64_t)neb::kTileBinsFrom;
+        const char* sb2 = std::getenv("NEB_SMALL_BATCH");
+        g_knobs[NEB_KNOB_SMALL_BATCH] = sb2 ? (int64_t)std::strtoull(sb2, nullptr, 10) : (int64_t)neb::kSmallBatchPerWave;
+        const char* fg = std::getenv("NEB_FRONT_GROUPS");
+        g_knobs[NEB_KNOB_FRONT_GROUPS] = fg ? (int64_t)std::strtoull(fg, nullptr, 10) : (int64_t)neb::kSmallBatchGroups;
         return true;
     }();
     (void)init;
@@ -843,6 +847,15 @@ static hipError_t sched_reserve(neb_engine* e, SchedSpace& sp, uint32_t n, hipSt
     return hipSuccess;
 }
 
+// Groups per front chunk at most (sched_groups' own: up to 8) for a batch of n packets: below
+// NEB_KNOB_SMALL_BATCH packets per resident wave of the chunk kernel (16 per CU) the front chunks hold
+// NEB_KNOB_FRONT_GROUPS groups at most (sched.hpp kSmallBatchPerWave).
+static uint32_t front_groups(const neb_engine* e, uint32_t n) {
+    const int64_t below = neb::knob(NEB_KNOB_SMALL_BATCH), cap = neb::knob(NEB_KNOB_FRONT_GROUPS);
+    const uint64_t waves = (uint64_t)std::max(e->cu_count, 1) * 16u;
+    return below > 0 && cap > 0 && (uint64_t)n < (uint64_t)below * waves ? (uint32_t)std::min<int64_t>(cap, 8) : 8u;
+}
+
 // NEB_BIND_EVENTS=0 (read once): markers after each batch instead of events bound to its last
 // kernel's dispatch (the A/B of round 4's binding for mixed-key AES-GCM and ChaCha batches)
 static bool bind_events() {
@@ -875,6 +888,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
             err = sched_reserve(e, sp, n, s);
             if (err == hipSuccess && !sp.last.same(s)) err = hipStreamWaitEvent(s, sp.done, 0);  // the previous batch on it
             neb::SchedWs ws = sp.ws;
+            ws.max_groups = front_groups(e, n);
             if (err == hipSuccess) err = neb_sched_build(d_desc, n, d_n, e->max_keys, 4u, &ws, s);
         }
         if (err == hipSuccess)  // sp.done bound to the chunk kernel's dispatch: no marker packet between batches
@@ -1124,6 +1138,7 @@ int neb_rx_sched_begin(neb_engine* e, uint32_t n, void* sched, hipStream_t s, ne
         return NEB_ERR_HIP;
     }
     *ws = sp.ws;
+    ws->max_groups = front_groups(e, n);
     *max_keys = e->max_keys;
     return NEB_OK;
 }

@@ -63,6 +63,19 @@ __host__ __device__ inline uint32_t sched_tail_cost(uint32_t cls, uint32_t lg) {
     return (r ? r : 1u) + 2u;
 }
 
+// A batch that gives each resident wave of the chunk kernel only one or two chunks balances badly
+// (C5's 8-GPU shard by tunnel, 131 072 packets over 512 keys, 32 per wave: waves 0.69 busy over the
+// span). Below kSmallBatchPerWave packets per wave the front chunks of the short classes hold
+// kSmallBatchGroups groups at most (SchedWs::max_groups), so the waves draw smaller pieces. A/B
+// (profiles/r6/ab/front_groups*.jsonl): that shard 377 -> 410 GiB/s at 1 group (402 at 2); at 64 and
+// 128 packets per wave equal or slower, 1 Mi (256) 528 -> 512, so those keep sched_groups. Running
+// the 576 B+ classes' full groups as two 8-lane halves as well was slower everywhere (C3 545 -> 512,
+// the shard 410 -> 378).
+#ifndef NEB_SMALL_BATCH_PER_WAVE
+#define NEB_SMALL_BATCH_PER_WAVE 48
+#endif
+constexpr uint32_t kSmallBatchPerWave = NEB_SMALL_BATCH_PER_WAVE, kSmallBatchGroups = 1;
+
 // counters[] slots
 constexpr uint32_t kCntPackets = 0;  // cursor into sorted[]
 constexpr uint32_t kCntBucket = 1;   // [kBuckets] chunks filed in each cost bucket
@@ -122,6 +135,7 @@ struct SchedWs {          // device workspace, sized for n packets and nbins bin
     uint32_t* sorted;     // [n] packet indices, bin-contiguous
     uint4* chunks;        // [kBuckets][max_chunks] chunk records (chunk_w), bucket b's from b * max_chunks
     uint32_t max_chunks;  // the batch's chunks at most, and each bucket's capacity
+    uint32_t max_groups = 8;  // cap on sched_groups (groups per front chunk) for this batch
     uint32_t* tcnt;       // [kTileMax][sched_tile_words] per-tile bin counts, 16 bits each (null: no tiles)
     uint32_t* tpre;       // [kTileMax][nbins] each (tile, bin)'s offset inside its bin
 };

@@ -140,7 +140,7 @@ __device__ __forceinline__ void sched_alloc_block(uint32_t max_keys, const Sched
 #pragma unroll
     for (uint32_t k = 0; k < kSizeClasses; k++) cc[k] = (uint32_t)__shfl((int)c, (int)(grp + k));
     // this class's front chunks: nfc of g groups, the last one of lastg; and the leftover group
-    const uint32_t nf = c / kChunkPkts, g = sched_groups(cls);
+    const uint32_t nf = c / kChunkPkts, g = min(sched_groups(cls), ws.max_groups);
     const uint32_t nfc = (nf + g - 1u) / g, lastg = nf - (nfc ? nfc - 1u : 0u) * g;
     const uint32_t bfull = sched_bucket(sched_front_cost(g, cls)), blast = sched_bucket(sched_front_cost(lastg, cls));
     uint32_t lb = 0;

@@ -179,3 +179,21 @@ def shard(b: Batch, rank: int, world: int) -> Batch:
         d[f] -= base
     arena = b.arena[lo * b.stride:hi * b.stride].copy()
     return Batch(b.alg, b.keys, b.remote_index, d, arena, b.stride, f"{b.name} shard {rank}/{world}")
+
+
+def shard_by_key(b: Batch, rank: int, world: int) -> Batch:
+    """The packets of the tunnels with key_id mod world == rank (SURVEY.md §8e's partition by key):
+    every tunnel's packets on one GPU, in their batch order. A tunnel's state — its replay window and
+    message counter (connection_state.go:37-49) — then lives on one device, which a receive batch
+    needs (its windows see every packet of their tunnel), and each GPU's batch keeps the whole batch's
+    packets per tunnel. Offsets rebased to the shard's own arena (the selected slots, in order)."""
+    idx = np.flatnonzero(b.desc["key_id"] % np.uint32(world) == rank)
+    d = b.desc[idx].copy()
+    slots = b.arena.reshape(b.n, b.stride)[idx]
+    base = np.arange(len(idx), dtype=np.uint64) * np.uint64(b.stride)
+    old = idx.astype(np.uint64) * np.uint64(b.stride)
+    for f in ("src_off", "dst_off", "aad_off"):
+        d[f] = d[f] - old + base
+    return Batch(b.alg, b.keys, b.remote_index, d, slots.reshape(-1).copy(), b.stride,
+                 f"{b.name} tunnels mod {world} = {rank}")
+

@@ -20,9 +20,9 @@ import sched_model as M  # noqa: E402
 from nebula_amd import workload as W  # noqa: E402
 
 
-def _check(key_id, aad_len, length, max_keys):
+def _check(key_id, aad_len, length, max_keys, max_groups=8):
     n = len(key_id)
-    chunks = M.plan(key_id, aad_len, length, max_keys)
+    chunks = M.plan(key_id, aad_len, length, max_keys, max_groups)
     seen = np.concatenate([c.packets for c in chunks]) if chunks else np.zeros(0, np.int64)
     assert np.array_equal(np.sort(seen), np.arange(n)), "every packet in exactly one chunk"
     cls = M.size_class(aad_len, length)
@@ -113,6 +113,18 @@ def test_bin_tail_shapes():
             assert back == []
         else:
             assert back == [(t, 4 if t <= 4 else 3)]
+
+
+def test_small_batch_front_groups():
+    """Below NEB_KNOB_SMALL_BATCH packets per wave (C5's shard by tunnel: 512 keys, 256 packets each)
+    every front chunk holds one group; the leftovers are planned as without the cap. (Here the tunnel
+    shard of a 131 072-packet IMIX batch: 512 keys, 32 packets each.)"""
+    d = W.shard_by_key(W.config(4, scale=1.0 / 8), 0, 8).desc
+    plain, _ = _check(d["key_id"], d["aad_len"], d["len"], 4096)
+    fine, _ = _check(d["key_id"], d["aad_len"], d["len"], 4096, max_groups=1)
+    assert max(len(c.packets) for c in fine if c.kind == "front") == M.CHUNK_PKTS
+    multi = sum(len(c.packets) // M.CHUNK_PKTS - 1 for c in plain if c.kind == "front" and c.count0 > M.CHUNK_PKTS)
+    assert multi > 0 and len(fine) == len(plain) + multi
 
 
 def test_leftover_absorption_rules():

@@ -76,13 +76,14 @@ class Chunk:
     bucket: int
 
 
-def key_chunks(key: int, counts, starts):
-    """sched_key_chunks for one key: counts[cls] packets of class cls from starts[cls] in `sorted`.
+def key_chunks(key: int, counts, starts, max_groups: int = 8):
+    """sched_alloc_block's chunks for one key: counts[cls] packets of class cls from starts[cls] in
+    `sorted`, front chunks of at most min(groups(cls), max_groups) groups.
     Returns (kind, cls, lg, (start0, count0), (start1, count1), bucket) in emission order."""
     out = []
     left, lpos = [0] * SIZE_CLASSES, [0] * SIZE_CLASSES
     for c in range(SIZE_CLASSES):
-        nf, g = counts[c] // CHUNK_PKTS, groups(c)
+        nf, g = counts[c] // CHUNK_PKTS, min(groups(c), max_groups)
         for j in range(0, nf, g):
             gc = min(g, nf - j)
             out.append(("front", c, 2, (starts[c] + j * CHUNK_PKTS, gc * CHUNK_PKTS), (0, 0), bucket(front_cost(gc, c))))
@@ -108,7 +109,8 @@ def key_chunks(key: int, counts, starts):
     return out
 
 
-def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: int) -> List[Chunk]:
+def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: int,
+         max_groups: int = 8) -> List[Chunk]:
     """The chunks sched_alloc_kernel writes for one batch: per key, its classes one after another in
     `sorted`, and sched_key_chunks' records."""
     key = np.where(key_id < max_keys, key_id, max_keys).astype(np.int64)
@@ -122,7 +124,7 @@ def plan(key_id: np.ndarray, aad_len: np.ndarray, length: np.ndarray, max_keys: 
         k = int(sk[s])
         counts = [int((sc[s:e] == c).sum()) for c in range(SIZE_CLASSES)]
         starts = list(s + np.r_[0, np.cumsum(counts)[:-1]])
-        for kind, c, lg, (s0, c0), (s1, c1), b in key_chunks(k, counts, starts):
+        for kind, c, lg, (s0, c0), (s1, c1), b in key_chunks(k, counts, starts, max_groups):
             pk = np.r_[order[s0:s0 + c0], order[s1:s1 + c1]].astype(np.int64)
             out.append(Chunk(kind, pk, k, c, lg, c0, b))
     return out

@@ -123,6 +123,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--out", default=None)
     ap.add_argument("--shard-of", type=int, default=0, help="--config 4: shard 0 of the 1 Mi batch split N ways")
+    ap.add_argument("--shard-by", choices=["key", "range"], default="key")
     args = ap.parse_args()
     if args.out:
         os.makedirs(os.path.dirname(args.out), exist_ok=True)
@@ -139,7 +140,8 @@ def main():
     lib.neb_debug_wave_trace.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     b = {1: lambda: W.make_batch(L.ALG_AESGCM, 65536, 1, name="C2"),
          2: lambda: W.make_batch(L.ALG_AESGCM, 65536, 4096, name="C3"),
-         4: lambda: W.shard(W.config(4), 0, args.shard_of) if args.shard_of else W.config(4)}[args.config]()
+         4: lambda: (W.shard_by_key if args.shard_by == "key" else W.shard)(W.config(4), 0, args.shard_of)
+         if args.shard_of else W.config(4)}[args.config]()
     eng = Engine(0, max_keys=max(4096, b.nkeys))
     ciphers = install_keys(eng, b)
     db = DeviceBatch(eng, b, ciphers)
