@@ -316,6 +316,10 @@ def main():
                     help="device mode: before the W warmup steps, untimed seal+open steps until this much wall "
                          "time has passed, so the GPU runs at the clocks a sustained load holds (0: none; "
                          "reported as `settle` in the line)")
+    ap.add_argument("--sustain-ms", type=float, default=1000.0,
+                    help="device mode: after the timed K steps, the same step repeated for about this long "
+                         "(a fixed step count from the timed rate, barrier + sync around it, max over ranks): "
+                         "the rate a long load holds, reported as `sustained` beside `value` (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inproc", action="store_true",
                     help="device mode, --gpus N engines in ONE process (Nebula is one process): each engine its "
@@ -492,6 +496,8 @@ def main():
     assert (st == 0).all(), "open failed inside the timed region"
     dt = ctrl.max(dt)
     total_payload = ctrl.sum(2 * payload * args.steps)
+    sus = sustained(args, ctrl, lambda: (db.seal(), db.open()), total_payload / args.steps, dt / args.steps * 1e3)
+    assert (db.status_host() == 0).all(), "open failed in the sustained run"
     multi = hbm_over_ranks(ctrl, world, alg_bytes, seal_ms, ndev)
 
     if rank != 0:
@@ -512,6 +518,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "settle": settled,  # untimed, before the warmup (settle())
+        "sustained": sus,  # after the timed steps: the rate over ~--sustain-ms of the same step (sustained())
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
         # C5 is one 1 Mi-packet batch split over the GPUs (BASELINE.json "sharded over 8xMI355X"):
@@ -551,6 +558,31 @@ def main():
             log(f"cpu_baseline failed: {e!r}")
             out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
+
+
+def sustained(args, ctrl, step, payload_all_ranks: float, ms_per_step: float):
+    """The rate over a long run of the same step after the timed region: ceil(--sustain-ms / the timed
+    step time) more steps between a barrier and a device sync, the max time over ranks. `value` is
+    the driver's K-step figure right after the settle; this one shows what a sustained load holds
+    (the clocks of a long load sit a few % below the first second's)."""
+    import math
+
+    import torch
+
+    if args.sustain_ms <= 0:
+        return None
+    n = max(1, math.ceil(args.sustain_ms / max(ms_per_step, 1e-3)))
+    ctrl.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n):
+        step()
+        if i % 64 == 63:
+            torch.cuda.synchronize()  # (the host stays within 64 steps of the device)
+    torch.cuda.synchronize()
+    dt = ctrl.max(time.perf_counter() - t0)
+    return {"steps": n, "ms": round(dt * 1e3, 1), "ms_per_step": round(dt / n * 1e3, 4),
+            "value": round(payload_all_ranks * n / dt / GIB, 3)}
 
 
 def whole_seal_ms(db, stream, reps: int = 4) -> float:

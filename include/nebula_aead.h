@@ -113,6 +113,9 @@ NEB_API int neb_engine_info(const neb_engine* e, int* device, uint32_t* max_keys
  * thread's neb_encrypt_danger / neb_decrypt_danger), per-packet calls, calls that waited for a
  * slot, keys installed (since creation). */
 NEB_API int neb_engine_stats(const neb_engine* e, uint64_t stats[4]);
+/* Per-packet AES-256-GCM calls that arrived while every launch slot was busy ride together in one
+ * launch (round 6): {such combined launches, calls they carried} since creation. */
+NEB_API int neb_engine_pkt_combined(const neb_engine* e, uint64_t out[2]);
 /* Every entry point restores the calling thread's current HIP device before it returns. Streams
  * passed to the batch calls must stay alive until the work enqueued on them has completed. */
 /* Human-readable text of a return code. */

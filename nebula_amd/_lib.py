@@ -74,6 +74,7 @@ SIGNATURES = {
     "neb_cipher_create_batch": (_i, [_vp, _i, _u8p, _u32, _vp]),
     "neb_cipher_create_multi": (_i, [_vp, _u32, _i, _u8p, _vp]),
     "neb_engine_stats": (_i, [_vp, _vp]),
+    "neb_engine_pkt_combined": (_i, [_vp, _vp]),
     "neb_cipher_destroy": (_i, [_vp]),
     "neb_cipher_key_id": (_u32, [_vp]),
     "neb_cipher_alg": (_i, [_vp]),

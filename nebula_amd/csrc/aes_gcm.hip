@@ -1345,6 +1345,7 @@ __global__ __launch_bounds__(kTailWaves * kWave) void gcm_single_tail_kernel(Gcm
 // the dispatch, so the kernel reads nothing over PCIe; it writes the result and the status into
 // the caller's pinned staging (posted writes). One wave, 64 lanes per packet (2 rounds for 1300 B).
 constexpr uint32_t kOneBytes = 2048;  // AAD (padded to 16) + payload (+ tag): larger packets take the batch path
+
 // The status goes out last, behind a system-scope release of the wave's result stores, so the host
 // may take the result as soon as it sees the status word change (engine.cpp one_packet) instead of
 // waiting for the stream (hipStreamSynchronize: ≈ 26 µs of a ≈ 36 µs call, round 4).
@@ -1426,6 +1427,82 @@ __global__ __launch_bounds__(kOneFillThreads) void gcm_one_kernel(OneArgs a) {
         printf("one %d: fill %u  keys %u  packet %u  (x10 ns)\n", (int)OPEN, (unsigned)(ts1 - ts0), (unsigned)(ts2 - ts1),
                (unsigned)(ts3 - ts2));
 #endif
+}
+
+// ---- per-packet calls that arrive together, in one launch (engine.cpp's combiner) -------------
+// Concurrent EncryptDanger / DecryptDanger calls (several threads, each its own tunnel) that arrive
+// while another call's launch is being made are collected in a pinned batch buffer and launched
+// together: one wave per request, four waves per workgroup. The waves fill the workgroup's T-table
+// image together; each stages its own key's GHASH tables (the per-packet kernel's set, GhShoup64)
+// in a slice of its own and copies its request's slot from host memory into LDS with one parallel
+// load (under the fill), then seals or opens it at 64 lanes, writes the result back into its slot
+// (in place, host memory) and publishes its status last (one_publish_status), as the per-packet
+// kernel does. The buffer (engine.cpp PktComb): descriptors (offsets from the slots' base; request r's
+// bytes in slot r, kCombSlot apart), statuses, slots.
+constexpr int kOneBatchWaves = 4;
+constexpr uint32_t kCombSlot = kOneBytes + 64u;  // AAD | payload (+ tag), room for the tag a seal appends
+struct OneBatchLds {
+    uint2 ttab[256 * 32];  // 64 KiB T-table pairs, 32 copies
+    struct KeyTabs {
+        uint4 shoup[kTailLg * 16];
+        uint4 pos[8 * 16];
+        uint4 m16[16 * 16];
+        uint4 hi[3 * 16];
+    } k[kOneBatchWaves];                              // 8.25 KiB each
+    uint4 data[kOneBatchWaves][kCombSlot / 16u];      // the request's slot
+    int32_t st[kOneBatchWaves];
+};
+template <bool OPEN>
+__global__ __launch_bounds__(kOneBatchWaves * kWave) void gcm_one_batch_kernel(const neb_desc* descs, int32_t* status,
+                                                                                uint8_t* slots, uint32_t n,
+                                                                                const uint32_t* keys,
+                                                                                uint32_t max_keys) {
+    __shared__ OneBatchLds lds;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r = blockIdx.x * kOneBatchWaves + w;
+    const bool have = r < n;
+    // the request's descriptor and bytes first (host memory: one PCIe round trip, under the fill)
+    constexpr uint32_t kSlotVecs = kCombSlot / 16u;
+    neb_desc d = {};
+    uint4 b[(kSlotVecs + kWave - 1) / kWave];
+    if (have) {
+        d = descs[r];
+#pragma unroll
+        for (uint32_t k = 0; k < (kSlotVecs + kWave - 1) / kWave; k++)
+            if (k * kWave + lane < kSlotVecs)
+                b[k] = *reinterpret_cast<const uint4*>(slots + (size_t)r * kCombSlot + 16u * (k * kWave + lane));
+    }
+    fill_ttab<256u * 32u, kOneBatchWaves * kWave>(lds.ttab, tid, ttab_entry);
+    const uint32_t key = __builtin_amdgcn_readfirstlane(d.key_id);
+    const uint32_t* srec = keys + (size_t)(key < max_keys ? key : 0u) * kKeyRecDwords;
+    OneBatchLds::KeyTabs& kt = lds.k[w];
+    if (have) {
+        for (uint32_t t = lane; t < 16u * kTailLg; t += kWave) kt.shoup[t] = ld_rec4(srec, rec_shoup_pow2(t >> 4) + 4u * (t & 15u));
+        for (uint32_t t = lane; t < 128u; t += kWave) kt.pos[t] = ld_rec4(srec, kRecPos64 + 4u * t);
+        for (uint32_t t = lane; t < 256u; t += kWave) kt.m16[t] = ld_rec4(srec, kRecShoup + 4u * t);
+        if (lane < 48u)
+            kt.hi[lane] = ld_rec4(srec, (lane < 16u ? kRecShoup + 15u * 64u : lane < 32u ? kRecShoup32 : kRecShoup48) + 4u * (lane & 15u));
+#pragma unroll
+        for (uint32_t k = 0; k < (kSlotVecs + kWave - 1) / kWave; k++)
+            if (k * kWave + lane < kSlotVecs) lds.data[w][k * kWave + lane] = b[k];
+    }
+    __syncthreads();
+    if (!have) return;
+    uint32_t rks[60];
+    load_round_keys(srec, rks);
+    const TLook T{lds.ttab, ttab_lane_base(lane)};
+    const GhShoup64 gh{kt.m16, kt.shoup, kt.pos, kt.hi};
+    const bool key_ok = key < max_keys && __builtin_amdgcn_readfirstlane(srec[kRecAlg]) == NEB_ALG_AESGCM;
+    // the bytes in LDS, addressed through a generic pointer (flat loads): the descriptor's offsets are
+    // from the slots' base, so the LDS copy stands at slot r's place; the output goes to the slot in
+    // host memory (a wrapping offset from there)
+    uint64_t lb = (uint64_t)(uintptr_t)(const void*)&lds.data[w][0] - (uint64_t)r * kCombSlot;
+    asm volatile("" : "+s"(lb));
+    uint8_t* base = reinterpret_cast<uint8_t*>(lb);
+    d.dst_off = d.dst_off + (uint64_t)(uintptr_t)slots - lb;
+    GcmArgs ga{nullptr, 1u, base, keys, max_keys, key, &lds.st[w], nullptr, 0u, 0u, nullptr};
+    gcm_packet_group<OPEN>(ga, 0u, true, key, key_ok, RkRegs{rks}, gh, T, lane, kTailLg, nullptr, &d);
+    one_publish_status(status + r, &lds.st[w]);
 }
 
 // ---- mixed keys: one key per chunk of the regrouped batch (sched.hpp) --------------------------
@@ -2061,6 +2138,18 @@ extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len
         hipLaunchKernelGGL(neb::gcm_one_kernel<true>, dim3(1), dim3(neb::kOneFillThreads), 0, s, a);
     else
         hipLaunchKernelGGL(neb::gcm_one_kernel<false>, dim3(1), dim3(neb::kOneFillThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// A combined launch of n per-packet requests (engine.cpp PktComb): descriptors, statuses and slots
+// (kCombSlot bytes each, the descriptors' offsets from `slots`) in pinned host memory.
+extern "C" hipError_t neb_gcm_one_batch(int open, const neb_desc* descs, int32_t* status, uint8_t* slots, uint32_t n,
+                                        const uint32_t* d_keys, uint32_t max_keys, hipStream_t s) {
+    const dim3 grid((n + neb::kOneBatchWaves - 1) / neb::kOneBatchWaves), block(neb::kOneBatchWaves * neb::kWave);
+    if (open)
+        hipLaunchKernelGGL(neb::gcm_one_batch_kernel<true>, grid, block, 0, s, descs, status, slots, n, d_keys, max_keys);
+    else
+        hipLaunchKernelGGL(neb::gcm_one_batch_kernel<false>, grid, block, 0, s, descs, status, slots, n, d_keys, max_keys);
     return hipGetLastError();
 }
 

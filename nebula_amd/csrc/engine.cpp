@@ -19,6 +19,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/nebula_aead.h"
@@ -45,6 +46,8 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
 extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in, uint32_t in_len,
                                   uint32_t len, uint64_t counter, uint8_t* out, int32_t* status, const uint32_t* d_keys,
                                   uint32_t max_keys, uint32_t key, hipStream_t s);
+extern "C" hipError_t neb_gcm_one_batch(int open, const neb_desc* descs, int32_t* status, uint8_t* slots, uint32_t n,
+                                        const uint32_t* d_keys, uint32_t max_keys, hipStream_t s);
 extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in,
                                      uint32_t in_len, uint32_t len, uint64_t counter, uint8_t* out, int32_t* status,
                                      const uint32_t* d_keys, uint32_t max_keys, uint32_t key, hipStream_t s);
@@ -106,25 +109,56 @@ struct SchedSpace {
 namespace {
 
 constexpr size_t kStageMin = 1 << 16;
-constexpr int kPipeStreams = 3;
+// The staged host pipeline (batch_host, round 6): chunks of kPipeChunkPkts packets through
+// kPipeSlots device buffers, with the copies in, the kernels and the copies back on three streams
+// of their own, chained by events: chunk k + 1's copy-in then runs beside chunk k - 1's copy-back
+// (PCIe carries both directions at once: 56 GB/s each alone, 96 GB/s together on this box).
+// Chunks ramp up from kPipeFirst packets (doubling) to kPipeChunkPkts and back down at the end, so the
+// first copy-in and the last copy-back, which run with nothing beside them, are short. A/B on C2
+// (profiles/r6/host/): chunks of 4096 / 8192 / 12288 / 16384 / 32768 packets 23.9 / 26.6 / 32.6-33.2 /
+// 32.6 / 28.5 GiB/s; a 16384-packet copy-in runs 395 µs alone and 520 µs beside a copy-back (42 + 51
+// GB/s), and the first and last of each call ran alone for ≈ 0.9 of its 2.7 ms.
+constexpr int kPipeSlots = 4;
 #ifndef NEB_PIPE_CHUNK
-#define NEB_PIPE_CHUNK 8192
+#define NEB_PIPE_CHUNK 16384
 #endif
-constexpr uint32_t kPipeChunkPkts = NEB_PIPE_CHUNK;  // packets per staged host chunk
+#ifndef NEB_PIPE_FIRST
+#define NEB_PIPE_FIRST 4096
+#endif
+constexpr uint32_t kPipeChunkPkts = NEB_PIPE_CHUNK;  // packets per staged host chunk at most
+constexpr uint32_t kPipeFirst = NEB_PIPE_FIRST;      // the first and last chunks' packets
+
+// chunk sizes for a batch of n packets: kPipeFirst, 2 kPipeFirst, ... up to kPipeChunkPkts at both
+// ends (while the rest still holds 4x the next size), full chunks between
+std::vector<uint32_t> pipe_plan(uint32_t n) {
+    std::vector<uint32_t> head, plan;
+    uint32_t rem = n;
+    for (uint32_t s = kPipeFirst; s < kPipeChunkPkts && rem >= 4u * s; s *= 2u) {
+        head.push_back(s);
+        rem -= 2u * s;
+    }
+    plan = head;
+    for (; rem; rem -= std::min(rem, kPipeChunkPkts)) plan.push_back(std::min(rem, kPipeChunkPkts));
+    plan.insert(plan.end(), head.rbegin(), head.rend());
+    return plan;
+}
 
 struct PipeSlot {
-    hipStream_t stream = nullptr;
     uint8_t* d_buf = nullptr;
     size_t d_cap = 0;
-    neb_desc* d_desc = nullptr;
-    int32_t* d_status = nullptr;
-    neb_desc* h_desc = nullptr;  // pinned
-    int32_t* h_status = nullptr; // pinned
+    neb_desc* h_desc = nullptr;  // pinned, mapped: the kernels read it in place
+    int32_t* h_status = nullptr; // pinned, mapped: the kernels write it in place
     int32_t* user_status = nullptr;
     uint32_t user_begin = 0, count = 0;
-    uint64_t lo = 0, hi = 0;      // arena span of the chunk in flight (count > 0)
-    hipEvent_t done = nullptr;    // recorded after the chunk's span is back in the arena
-    SchedSpace* sched = nullptr;  // own mixed-key workspace: the two pipeline streams never wait on each other
+    uint64_t lo = 0, hi = 0;        // arena span of the chunk in flight (count > 0)
+    hipEvent_t in_done = nullptr;   // the chunk's copies in are done (the kernel waits for it)
+    hipEvent_t k_done = nullptr;    // its kernel is done (the copies back wait for it)
+    hipEvent_t done = nullptr;      // its span and statuses are back (the slot is free)
+};
+struct Pipe {
+    hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    PipeSlot slot[kPipeSlots];
+    SchedSpace* sched = nullptr;  // the compute stream's mixed-key workspace
 };
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -185,6 +219,49 @@ struct PktPool {
     std::deque<PktWaiter*> waiters;
     std::atomic<uint64_t> calls{0}, waits{0};
 };
+// Per-packet AES-256-GCM calls that arrive while kPktSlots launches are in flight (round 6): they join
+// one pinned batch of up to kCombMax requests, which its first request (the leader) launches as a
+// whole (gcm_one_batch_kernel) as soon as one of the launches ahead completes; the leader polls
+// every status, wakes the others, and each copies its own result out. A call that finds a launch
+// free launches alone as before (the packet in the kernel arguments), so up to kPktSlots threads see
+// no change; past that the batches grow with the offered load.
+constexpr uint32_t kCombMax = 32;
+constexpr uint32_t kCombSlot = 2048u + 64u;  // aes_gcm.hip kCombSlot: AAD | payload (+ tag) of one request
+constexpr size_t kCombDescOff = 0, kCombStatusOff = 2048, kCombSlotsOff = 4096;
+constexpr size_t kCombBytes = kCombSlotsOff + (size_t)kCombMax * kCombSlot;
+struct CombBatch {
+    uint8_t* h = nullptr;  // pinned, mapped: descriptors | statuses | slots
+    uint32_t n = 0;        // requests joined
+    int alg = 0, open = 0;
+    bool launched = false;  // (PktComb::mu)
+    hipStream_t stream = nullptr;
+    std::atomic<uint32_t> left{0};  // requests whose owner has not copied its result out yet
+    // The leader saw every status: the owners may copy out. A mutex of the batch's own, so the
+    // owners' wake-ups do not queue on the engine's combiner mutex (64 threads on a 16-CPU share:
+    // p99 23 ms with one mutex for both).
+    std::mutex dmu;
+    std::condition_variable done_cv;
+    bool done = false, failed = false;  // (dmu)
+    neb_desc* desc() const { return reinterpret_cast<neb_desc*>(h + kCombDescOff); }
+    int32_t* status() const { return reinterpret_cast<int32_t*>(h + kCombStatusOff); }
+    uint8_t* slots() const { return h + kCombSlotsOff; }
+};
+struct PktComb {
+    std::mutex mu;
+    uint32_t inflight = 0;          // launches (alone or combined) not yet complete, at most kPktSlots
+    std::condition_variable launch_cv;  // a launch completed (the leaders of gathering batches wait)
+    CombBatch* open[2][2] = {};     // accepting requests: [AES-GCM / ChaCha20][seal / open]
+    std::vector<CombBatch*> free_, all;
+    uint32_t next = 0;              // the per-packet pool's streams carry the combined launches in turn
+    std::atomic<uint64_t> launches{0}, combined{0};
+    std::atomic<uint32_t> spinners{0};  // requests polling their own status word
+};
+// Requests of a combined batch poll their own status word (published behind a system-scope release
+// of the result, aes_gcm.hip gcm_one_batch_kernel) for up to kCombSpinUs while fewer than
+// kCombSpinners do, else sleep until the leader has seen the whole batch: a futex wake-up costs
+// ~10 µs, a 16-CPU share affords a few spinners but not 64.
+constexpr uint32_t kCombSpinners = 8;
+constexpr int kCombSpinUs = 200;
 struct KeyUse {
     hipStream_t s;
     hipEvent_t ev;
@@ -206,6 +283,7 @@ struct neb_engine {
     uint64_t installs = 0;
 
     PktPool pkt;  // per-packet calls and key installs
+    PktComb comb; // per-packet calls combined into one launch
 
     // Asynchronous batches still queued when a key is destroyed: per key slot, the last
     // single-key batch the engine launched on each stream, and the last mixed-key batch per
@@ -216,7 +294,7 @@ struct neb_engine {
     std::vector<KeyUse> mixed_use;
 
     std::mutex pipe_mu;
-    PipeSlot pipe[kPipeStreams];
+    Pipe pipe;
     // zero-copy host batches: device copies of pageable descriptors / statuses
     neb_desc* zc_desc = nullptr;
     int32_t* zc_status = nullptr;
@@ -492,19 +570,23 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
     if (!e) return NEB_ERR_INVALID;
     DeviceGuard dg(e->device);
     if (e->stream) hipStreamSynchronize(e->stream);
-    for (auto& s : e->pipe) {
-        if (s.stream) { hipStreamSynchronize(s.stream); hipStreamDestroy(s.stream); }
-        if (s.done) hipEventDestroy(s.done);
+    for (hipStream_t st : {e->pipe.h2d, e->pipe.comp, e->pipe.d2h})
+        if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
+    for (CombBatch* b : e->comb.all) {
+        if (b->h) hipHostFree(b->h);
+        delete b;
+    }
+    for (auto& s : e->pipe.slot) {
+        for (hipEvent_t ev : {s.in_done, s.k_done, s.done})
+            if (ev) hipEventDestroy(ev);
         if (s.d_buf) hipFree(s.d_buf);
-        if (s.d_desc) hipFree(s.d_desc);
-        if (s.d_status) hipFree(s.d_status);
         if (s.h_desc) hipHostFree(s.h_desc);
         if (s.h_status) hipHostFree(s.h_status);
-        if (s.sched) {
-            if (s.sched->done) { hipEventSynchronize(s.sched->done); hipEventDestroy(s.sched->done); }
-            if (s.sched->mem) hipFree(s.sched->mem);
-            delete s.sched;
-        }
+    }
+    if (SchedSpace* sp = e->pipe.sched) {
+        if (sp->done) { hipEventSynchronize(sp->done); hipEventDestroy(sp->done); }
+        if (sp->mem) hipFree(sp->mem);
+        delete sp;
     }
     if (e->sched.done) { hipEventSynchronize(e->sched.done); hipEventDestroy(e->sched.done); }
     if (e->sched.mem) hipFree(e->sched.mem);
@@ -915,7 +997,7 @@ static hipError_t launch_batch(neb_engine* e, int alg, int open, const neb_desc*
 // pinned-memory poll sees the kernel's last store within about a microsecond of it; the stream
 // synchronize took ≈ 26 µs of the ≈ 36 µs call at 4 threads in round 4.
 constexpr int kPollUs = 2000;
-static bool poll_status(const int32_t* p, int32_t* st) {
+static bool poll_status(const int32_t* p, int32_t* st, int us = kPollUs) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; i++) {
         const int32_t v = __atomic_load_n(p, __ATOMIC_ACQUIRE);
@@ -925,7 +1007,7 @@ static bool poll_status(const int32_t* p, int32_t* st) {
         }
         __builtin_ia32_pause();
         if ((i & 255u) == 255u &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kPollUs))
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us))
             return false;
     }
 }
@@ -949,8 +1031,8 @@ static void copy_result(int open, int32_t st, uint8_t* dst, const uint8_t* slot,
 // copied into the slot's pinned, mapped buffer ([desc | status | aad | payload (+tag)]), the batch
 // kernel seals or opens it there in place (zero-copy: no DMA either way) and the result is copied
 // out. Up to kPktSlots calls run side by side; later ones wait their turn in FIFO order.
-static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len, const uint8_t* in, size_t in_len,
-                      size_t pay_len, uint64_t n, uint8_t* dst, int32_t* st_out) {
+static int one_packet_solo(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len, const uint8_t* in,
+                           size_t in_len, size_t pay_len, uint64_t n, uint8_t* dst, int32_t* st_out) {
     neb_engine* e = c->e;
     const size_t o_desc = 0, o_status = 64, o_aad = 128;
     const size_t o_pay = align_up(o_aad + ad_len, 16);
@@ -1015,6 +1097,147 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
     }
     std::memcpy(st_out, h + o_status, 4);
     copy_result(open, *st_out, dst, h + o_pay, pay_len);
+    return NEB_OK;
+}
+
+// A per-packet call through the engine's combiner (PktComb): alone while a launch slot is free
+// (one_packet_solo: the packet in the kernel arguments), else as a request of the batch the next
+// completed launch frees a slot for. AES-256-GCM only (the ChaCha20-Poly1305 batch kernel's statuses carry no
+// release of the payload before them, so its calls stay alone).
+static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len, const uint8_t* in, size_t in_len,
+                      size_t pay_len, uint64_t n, uint8_t* dst, int32_t* st_out) {
+    neb_engine* e = c->e;
+    static const bool comb_on = [] {  // NEB_PKT_COMBINE=0: every call alone (A/B)
+        const char* v = std::getenv("NEB_PKT_COMBINE");
+        return !(v && v[0] == '0');
+    }();
+    const size_t pay = align_up(ad_len, 16);
+    if (!comb_on || c->alg != NEB_ALG_AESGCM || pay + std::max(in_len, pay_len + 16) > kCombSlot || pay + in_len > 2048)
+        return one_packet_solo(c, open, ad, ad_len, in, in_len, pay_len, n, dst, st_out);
+    PktComb& cb = e->comb;
+    std::unique_lock<std::mutex> lk(cb.mu);
+    CombBatch*& ob = cb.open[0][open ? 1 : 0];
+    // Alone while fewer than kPktSlots launches are in flight and no batch is gathering (the pool
+    // then has a free slot: each alone call holds one, and only these take slots here).
+    if (cb.inflight < kPktSlots && !ob) {
+        cb.inflight++;
+        lk.unlock();
+        const int rc = one_packet_solo(c, open, ad, ad_len, in, in_len, pay_len, n, dst, st_out);
+        lk.lock();
+        cb.inflight--;
+        lk.unlock();
+        cb.launch_cv.notify_all();
+        return rc;
+    }
+    DeviceGuard dg(e->device);
+    if (!ob) {
+        if (cb.free_.empty()) {
+            auto* nb = new (std::nothrow) CombBatch;
+            if (!nb) return NEB_ERR_INVALID;
+            if (hipHostMalloc((void**)&nb->h, kCombBytes, hipHostMallocDefault) != hipSuccess) {
+                delete nb;
+                set_error("hipHostMalloc (per-packet batch)", hipErrorOutOfMemory);
+                return NEB_ERR_HIP;
+            }
+            cb.all.push_back(nb);
+            cb.free_.push_back(nb);
+        }
+        ob = cb.free_.back();
+        cb.free_.pop_back();
+        ob->n = 0;
+        ob->launched = false;
+        {
+            std::lock_guard<std::mutex> g(ob->dmu);
+            ob->done = ob->failed = false;
+        }
+        ob->alg = c->alg;
+        ob->open = open;
+    }
+    CombBatch* b = ob;
+    const uint32_t i = b->n++;
+    if (b->n == kCombMax) ob = nullptr;  // full: the next call starts another
+    uint8_t* slot = b->slots() + (size_t)i * kCombSlot;
+    if (ad_len) std::memcpy(slot, ad, ad_len);
+    if (in_len) std::memcpy(slot + pay, in, in_len);
+    neb_desc& d = b->desc()[i];
+    d = neb_desc{};
+    d.aad_off = (uint64_t)i * kCombSlot;
+    d.src_off = d.dst_off = d.aad_off + pay;  // in place in the slot
+    d.counter = n;
+    d.len = (uint32_t)pay_len;
+    d.aad_len = (uint32_t)ad_len;
+    d.key_id = c->key_id;
+    __atomic_store_n(b->status() + i, -1, __ATOMIC_RELAXED);
+    // The batch's first request leads it: it waits until a launch completes, launches the batch as
+    // it stands then (every joined request is filled: joiners fill under the mutex), polls every
+    // status and wakes the others. Under load the batch gathers for as long as the launches ahead
+    // of it run, so its size follows the offered load; one thread spins per launch, the rest sleep
+    // (64 threads spinning on a 16-CPU share starved the launches: p99 37 ms).
+    if (i == 0) {
+        cb.launch_cv.wait(lk, [&] { return cb.inflight < kPktSlots; });
+        cb.inflight++;
+        if (ob == b) ob = nullptr;
+        b->launched = true;
+        b->left.store(b->n, std::memory_order_relaxed);
+        b->stream = e->pkt.slot[cb.next++ % kPktSlots].stream;
+        const uint32_t cnt = b->n;
+        e->pkt.calls.fetch_add(cnt, std::memory_order_relaxed);  // (neb_engine_stats: per-packet calls)
+        lk.unlock();
+        hipError_t err = neb_gcm_one_batch(open, b->desc(), b->status(), b->slots(), cnt, e->d_keys, e->max_keys,
+                                           b->stream);
+        cb.launches.fetch_add(1, std::memory_order_relaxed);
+        cb.combined.fetch_add(cnt, std::memory_order_relaxed);
+        if (err == hipSuccess) {
+            bool slow = false;
+            for (uint32_t k = 0; k < cnt && !slow; k++) {
+                int32_t v;
+                slow = !poll_status(b->status() + k, &v);
+            }
+            if (slow) err = hipStreamSynchronize(b->stream);  // a slow device: the stream says when
+        }
+        if (err != hipSuccess) set_error("per-packet batch launch", err);
+        lk.lock();
+        cb.inflight--;
+        lk.unlock();
+        cb.launch_cv.notify_all();
+        {
+            std::lock_guard<std::mutex> g(b->dmu);
+            b->failed = err != hipSuccess;
+            b->done = true;
+        }
+        b->done_cv.notify_all();
+    } else {
+        lk.unlock();
+    }
+    int32_t st = -1;
+    const bool spin = i && cb.spinners.fetch_add(1, std::memory_order_relaxed) < kCombSpinners;
+    const bool seen = spin && poll_status(b->status() + i, &st, kCombSpinUs);
+    if (i) cb.spinners.fetch_sub(1, std::memory_order_relaxed);
+    if (!seen) {
+        bool failed;
+        {
+            std::unique_lock<std::mutex> g(b->dmu);
+            b->done_cv.wait(g, [&] { return b->done; });
+            failed = b->failed;
+        }
+        st = failed ? -1 : __atomic_load_n(b->status() + i, __ATOMIC_ACQUIRE);
+    }
+    if (st != -1) copy_result(open, st, dst, slot + pay, pay_len);
+    if (b->left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        lk.lock();
+        cb.free_.push_back(b);
+        lk.unlock();
+    }
+    if (st == -1) return NEB_ERR_HIP;
+    *st_out = st;
+    return NEB_OK;
+}
+
+// Per-packet calls combined into shared launches: {launches of combined batches, calls they carried}
+NEB_API int neb_engine_pkt_combined(const neb_engine* e, uint64_t out[2]) {
+    if (!e || !out) return NEB_ERR_INVALID;
+    out[0] = e->comb.launches.load(std::memory_order_relaxed);
+    out[1] = e->comb.combined.load(std::memory_order_relaxed);
     return NEB_OK;
 }
 
@@ -1225,31 +1448,38 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
     if (rc != NEB_OK) return rc;
     if (n == 0) return NEB_OK;
     if (!desc || !arena || !status) return NEB_ERR_INVALID;
-    for (uint32_t i = 0; i < n; i++)
-        if (!neb_desc_in_arena(desc[i], open, arena_len)) return NEB_ERR_INVALID;
+    // Every descriptor is checked before the arena or the statuses are written. The staged path
+    // checks the first chunk's, starts that chunk's copy-in and kernel (they write device buffers
+    // only), and checks the rest while they run: ≈ 90 µs of checks per 64 Ki packets off the
+    // critical path. Its first copy back waits for the whole check.
+    uint32_t checked = 0;
+    auto check_upto = [&](uint32_t end) {
+        for (; checked < end; checked++)
+            if (!neb_desc_in_arena(desc[checked], open, arena_len)) return false;
+        return true;
+    };
     std::lock_guard<std::mutex> g(e->pipe_mu);
     DeviceGuard dg(e->device);
     // The kernels' vector fast path tests the absolute address (arena base + offset), so a mapped
     // arena at any byte address runs zero-copy. A staged arena lands in a device buffer with the
     // same alignment modulo 16, so the kernels take the same paths either way.
-    if (host_mode() == kHostZeroCopy && host_mapped(arena))
+    if (host_mode() == kHostZeroCopy && host_mapped(arena)) {
+        if (!check_upto(n)) return NEB_ERR_INVALID;
         return batch_host_zero_copy(e, alg, open, desc, n, arena, arena_len, status, key_hint);
-    for (auto& s : e->pipe) {
-        if (!s.stream) {
-            HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-            HIP_TRY(hipMalloc((void**)&s.d_desc, kPipeChunkPkts * sizeof(neb_desc)));
-            HIP_TRY(hipMalloc((void**)&s.d_status, kPipeChunkPkts * sizeof(int32_t)));
+    }
+    Pipe& P = e->pipe;
+    for (hipStream_t* st : {&P.h2d, &P.comp, &P.d2h})
+        if (!*st) HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+    if (!P.sched && !(P.sched = new (std::nothrow) SchedSpace)) return NEB_ERR_INVALID;
+    for (auto& s : P.slot) {
+        if (!s.done) {
+            for (hipEvent_t* ev : {&s.in_done, &s.k_done, &s.done})
+                HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming));
             HIP_TRY(hipHostMalloc((void**)&s.h_desc, kPipeChunkPkts * sizeof(neb_desc), hipHostMallocDefault));
             HIP_TRY(hipHostMalloc((void**)&s.h_status, kPipeChunkPkts * sizeof(int32_t), hipHostMallocDefault));
         }
-        if (!s.sched) {
-            s.sched = new (std::nothrow) SchedSpace;
-            if (!s.sched) return NEB_ERR_INVALID;
-        }
         s.count = 0;
     }
-    int slot = 0;
     auto retire = [](PipeSlot& s) -> hipError_t {
         hipError_t err = hipEventSynchronize(s.done);
         if (err != hipSuccess) return err;
@@ -1257,10 +1487,29 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         s.count = 0;
         return hipSuccess;
     };
-    for (uint32_t begin = 0; begin < n; begin += kPipeChunkPkts, slot = (slot + 1) % kPipeStreams) {
-        PipeSlot& s = e->pipe[slot];
-        if (s.count) HIP_TRY(retire(s));  // retire this slot's previous chunk before reusing its buffers
-        const uint32_t cnt = std::min(kPipeChunkPkts, n - begin);
+    // any failure below leaves work queued on the three streams: drain them before returning
+    auto fail = [&](const char* where, hipError_t err) {
+        set_error(where, err);
+        for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
+        for (auto& s : P.slot) s.count = 0;
+        return NEB_ERR_HIP;
+    };
+#define PIPE_TRY(x)                                     \
+    do {                                                \
+        hipError_t err_ = (x);                          \
+        if (err_ != hipSuccess) return fail(#x, err_);  \
+    } while (0)
+    const std::vector<uint32_t> plan = pipe_plan(n);
+    uint32_t begin = 0;
+    for (uint32_t k = 0; k < plan.size(); begin += plan[k], k++) {
+        PipeSlot& s = P.slot[k % kPipeSlots];
+        if (s.count) PIPE_TRY(retire(s));  // the slot's previous chunk is back: its buffers are free
+        const uint32_t cnt = plan[k];
+        if (!check_upto(begin + cnt)) {  // (only ever the first chunk: the rest were checked after it)
+            for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
+            for (auto& o : P.slot) o.count = 0;
+            return NEB_ERR_INVALID;
+        }
         uint64_t lo = ~0ULL, hi = 0;  // every sum below stays within arena_len (checked above)
         for (uint32_t i = 0; i < cnt; i++) {
             const neb_desc& d = desc[begin + i];
@@ -1271,36 +1520,63 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         lo &= ~(uint64_t)15;
         // A chunk copies its whole span back, so spans of chunks in flight must not overlap (the
         // descriptors need not be in arena order): retire any other slot whose span intersects.
-        for (auto& o : e->pipe)
-            if (&o != &s && o.count && o.lo < hi && lo < o.hi) HIP_TRY(retire(o));
+        for (auto& o : P.slot)
+            if (&o != &s && o.count && o.lo < hi && lo < o.hi) PIPE_TRY(retire(o));
         s.lo = lo;
         s.hi = hi;
         const size_t span = (size_t)(hi - lo);
-        if (span > s.d_cap) {
-            if (s.d_buf) { HIP_TRY(hipStreamSynchronize(s.stream)); hipFree(s.d_buf); s.d_buf = nullptr; s.d_cap = 0; }
+        if (span > s.d_cap) {  // (retired: nothing in flight uses it)
+            if (s.d_buf) { hipFree(s.d_buf); s.d_buf = nullptr; s.d_cap = 0; }
             size_t cap = align_up(span, 1 << 20);
-            HIP_TRY(hipMalloc((void**)&s.d_buf, cap));
+            PIPE_TRY(hipMalloc((void**)&s.d_buf, cap));
             s.d_cap = cap;
         }
+#ifndef NEB_PIPE_MODE  // A/B: 0 copies back on a stream of their own, 1 on the kernels' stream, 2 the kernels store into the arena
+#define NEB_PIPE_MODE 0
+#endif
+        // mode 2: the outputs go straight to the host arena (a wrapping offset from the device buffer)
+        const uint64_t out_rebase = NEB_PIPE_MODE == 2 ? (uint64_t)(uintptr_t)(arena + lo) - (uint64_t)(uintptr_t)s.d_buf : 0u;
         for (uint32_t i = 0; i < cnt; i++) {
             neb_desc d = desc[begin + i];
             d.src_off -= lo;
             d.aad_off -= lo;
-            d.dst_off -= lo;
+            d.dst_off = d.dst_off - lo + out_rebase;
             s.h_desc[i] = d;
         }
         s.user_status = status;
         s.user_begin = begin;
         s.count = cnt;
-        HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, cnt * sizeof(neb_desc), hipMemcpyHostToDevice, s.stream));
-        HIP_TRY(hipMemcpyAsync(s.d_buf, arena + lo, span, hipMemcpyHostToDevice, s.stream));
-        HIP_TRY(launch_batch(e, alg, open, s.d_desc, cnt, s.d_buf, s.d_status, key_hint, s.stream, nullptr, s.sched));
-        HIP_TRY(hipMemcpyAsync(arena + lo, s.d_buf, span, hipMemcpyDeviceToHost, s.stream));
-        HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
-        HIP_TRY(hipEventRecord(s.done, s.stream));
+        // the kernels read the chunk's descriptors and write its statuses in the slot's pinned, mapped
+        // buffers themselves (48 + 4 B per packet over PCIe): two fewer copies per chunk, whose
+        // per-copy latency left the copy-in stream idle between chunks (a 15-µs copy after a ≈ 40-µs
+        // gap, profiles/r6/host/)
+        PIPE_TRY(hipMemcpyAsync(s.d_buf, arena + lo, span, hipMemcpyHostToDevice, P.h2d));
+        PIPE_TRY(hipEventRecord(s.in_done, P.h2d));
+        if (NEB_PIPE_MODE == 2 && k == 0 && !check_upto(n)) {  // (mode 2's kernels write the arena)
+            for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
+            for (auto& o : P.slot) o.count = 0;
+            return NEB_ERR_INVALID;
+        }
+        PIPE_TRY(hipStreamWaitEvent(P.comp, s.in_done, 0));
+        PIPE_TRY(launch_batch(e, alg, open, s.h_desc, cnt, s.d_buf, s.h_status, key_hint, P.comp, nullptr, P.sched));
+        PIPE_TRY(hipEventRecord(s.k_done, P.comp));
+        if (k == 0 && !check_upto(n)) {  // the rest of the batch, while chunk 0 is copied in and run
+            for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
+            for (auto& o : P.slot) o.count = 0;
+            return NEB_ERR_INVALID;
+        }
+        if (NEB_PIPE_MODE == 2) {
+            PIPE_TRY(hipEventRecord(s.done, P.comp));
+        } else {
+            hipStream_t back = NEB_PIPE_MODE == 1 ? P.comp : P.d2h;
+            if (NEB_PIPE_MODE == 0) PIPE_TRY(hipStreamWaitEvent(P.d2h, s.k_done, 0));
+            PIPE_TRY(hipMemcpyAsync(arena + lo, s.d_buf, span, hipMemcpyDeviceToHost, back));
+            PIPE_TRY(hipEventRecord(s.done, back));
+        }
     }
-    for (auto& s : e->pipe)
-        if (s.count) HIP_TRY(retire(s));
+    for (auto& s : P.slot)
+        if (s.count) PIPE_TRY(retire(s));
+#undef PIPE_TRY
     return NEB_OK;
 }
 

@@ -112,7 +112,10 @@ class Engine:
     def stats(self) -> dict:
         v = (C.c_uint64 * 4)()
         L.check(L.lib().neb_engine_stats(self.handle, v), "neb_engine_stats")
-        return {"pkt_slots": v[0], "pkt_calls": v[1], "pkt_waits": v[2], "installs": v[3]}
+        c = (C.c_uint64 * 2)()
+        L.check(L.lib().neb_engine_pkt_combined(self.handle, c), "neb_engine_pkt_combined")
+        return {"pkt_slots": v[0], "pkt_calls": v[1], "pkt_waits": v[2], "installs": v[3],
+                "pkt_combined_launches": c[0], "pkt_combined_calls": c[1]}
 
     def close(self) -> None:
         if self.handle:

@@ -6,6 +6,7 @@ import os
 import numpy as np
 import pytest
 
+from nebula_amd import _lib as L
 from nebula_amd import noiseutil as N
 from nebula_amd.noiseutil import Slice
 
@@ -403,3 +404,56 @@ def test_one_packet_kernel_size_boundary(engine, oracle_mod):
                     cs.DecryptDanger(None, ad, bytes(bad), n)
     finally:
         cs.destroy()
+
+
+def test_concurrent_calls_combined_with_forgeries(engine, oracle_mod):
+    """Concurrent AES-256-GCM calls that the engine combines into one launch (engine.cpp PktComb:
+    calls arriving while another launch is made ride together): 24 threads over 6 tunnels, payloads
+    0-1400 B with AAD up to 48 B, every 5th open given a flipped ciphertext or tag bit — that call
+    alone must fail (ErrOpen, its output zeroed) while the others in the same launch succeed, every
+    byte against the oracle."""
+    import threading
+
+    from nebula_amd.noiseutil import CipherAESGCM, ErrOpen
+
+    rng = np.random.default_rng(23)
+    states = []
+    for _ in range(6):
+        k = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        states.append((CipherAESGCM.Cipher(engine, k), k))
+    errors = []
+
+    def worker(t):
+        try:
+            r = np.random.default_rng(500 + t)
+            for j in range(120):
+                cs, k = states[(t * 5 + j) % 6]
+                n = (t << 40) | j
+                pt = bytes(r.integers(0, 256, int(r.choice([0, 1, 15, 16, 17, 90, 576, 1300, 1400])), dtype=np.uint8))
+                ad = bytes(r.integers(0, 256, int(r.choice([0, 16, 48])), dtype=np.uint8))
+                ct = cs.EncryptDanger(None, ad, pt, n).bytes()
+                if ct != oracle_mod.seal(L.ALG_AESGCM, k, oracle_mod.nonce(L.ALG_AESGCM, n), ad, pt):
+                    raise AssertionError(f"seal mismatch t={t} j={j}")
+                if j % 5 == 2:
+                    bad = bytearray(ct)
+                    bad[int(r.integers(0, len(bad)))] ^= 1 << int(r.integers(0, 8))
+                    try:
+                        cs.DecryptDanger(None, ad, bytes(bad), n)
+                        raise AssertionError(f"forgery accepted t={t} j={j}")
+                    except ErrOpen:
+                        pass
+                elif cs.DecryptDanger(None, ad, ct, n).bytes() != pt:
+                    raise AssertionError(f"open mismatch t={t} j={j}")
+        except Exception as ex:
+            errors.append(ex)
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(24)]
+    try:
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errors, errors[:3]
+    finally:
+        for cs, _ in states:
+            cs.destroy()

@@ -665,3 +665,27 @@ def test_full_size_batches_match_oracle_digests(engine, name):
         for c in ciphers:
             c.destroy()
     print(f"{name}: {b.n} packets, {time.time() - t0:.1f} s")
+
+
+_C5 = {}
+
+
+@pytest.mark.parametrize("by,rank", [("key", 0), ("range", 7)])
+def test_c5_gpu_shard_vs_oracle(engine, oracle_mod, by, rank):
+    """One GPU's part of C5 over 8 GPUs at full size (131 072 IMIX packets): the tunnels with
+    key_id mod 8 = rank (the bench's split: 512 keys, ≈ 256 packets each, one 16-packet group per
+    front chunk below NEB_KNOB_SMALL_BATCH) and the contiguous range (4096 keys, 32 each: leftover
+    groups taking smaller classes' packets). Sealed arena byte for byte against the oracle, opened
+    back to the plaintext. (The byte-serial oracle takes ≈ 20 s per shard.)"""
+    if "b" not in _C5:
+        _C5["b"] = W.config(4)
+    b = (W.shard_by_key if by == "key" else W.shard)(_C5["b"], rank, 8)
+    assert 120000 < b.n < 142000
+    ref, st_ref = oracle_seal(oracle_mod, b)
+    got, st = run_device(engine, b, seal=True)
+    assert (st == 0).all() and (st_ref == 0).all()
+    assert np.array_equal(got, ref)
+    opened, st_o = run_device(engine, b, seal=False, arena=got)
+    assert (st_o == 0).all()
+    used = np.arange(b.stride)[None, :] < 16 + b.desc["len"][:, None].astype(np.int64)  # header + payload
+    assert np.array_equal(opened.reshape(b.n, b.stride)[used], b.arena.reshape(b.n, b.stride)[used])
