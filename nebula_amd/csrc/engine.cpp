@@ -14,12 +14,16 @@
 #include <cstring>
 #include <cxxabi.h>
 #include <cstdlib>
+#include <climits>
 #include <dlfcn.h>
+#include <linux/futex.h>
 #include <mutex>
 #include <new>
 #include <string>
+#include <sys/syscall.h>
 #include <thread>
 #include <type_traits>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/nebula_aead.h"
@@ -236,32 +240,35 @@ struct CombBatch {
     bool launched = false;  // (PktComb::mu)
     hipStream_t stream = nullptr;
     std::atomic<uint32_t> left{0};  // requests whose owner has not copied its result out yet
-    // The leader saw every status: the owners may copy out. A mutex of the batch's own, so the
-    // owners' wake-ups do not queue on the engine's combiner mutex (64 threads on a 16-CPU share:
-    // p99 23 ms with one mutex for both).
-    std::mutex dmu;
-    std::condition_variable done_cv;
-    bool done = false, failed = false;  // (dmu)
+    // The leader saw every status: the owners may copy out. A futex word of the batch's own, so the
+    // owners wake without queueing on a mutex (64 threads on a 16-CPU share: p99 23 ms when they
+    // woke through the engine's combiner mutex).
+    std::atomic<uint32_t> done{0};
+    bool failed = false;  // written before done's release
+    void finish(bool f) {
+        failed = f;
+        done.store(1, std::memory_order_release);
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(&done), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+    }
+    bool wait() {  // the failure flag
+        while (!done.load(std::memory_order_acquire))
+            syscall(SYS_futex, reinterpret_cast<uint32_t*>(&done), FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
+        return failed;
+    }
     neb_desc* desc() const { return reinterpret_cast<neb_desc*>(h + kCombDescOff); }
     int32_t* status() const { return reinterpret_cast<int32_t*>(h + kCombStatusOff); }
     uint8_t* slots() const { return h + kCombSlotsOff; }
 };
 struct PktComb {
     std::mutex mu;
-    uint32_t inflight = 0;          // launches (alone or combined) not yet complete, at most kPktSlots
+    uint32_t inflight = 0;          // launches (alone or combined) not yet complete, at most pkt_inflight()
+    uint32_t solo = 0;              // of them alone (each holds a pool slot), at most kPktSlots
     std::condition_variable launch_cv;  // a launch completed (the leaders of gathering batches wait)
     CombBatch* open[2][2] = {};     // accepting requests: [AES-GCM / ChaCha20][seal / open]
     std::vector<CombBatch*> free_, all;
     uint32_t next = 0;              // the per-packet pool's streams carry the combined launches in turn
     std::atomic<uint64_t> launches{0}, combined{0};
-    std::atomic<uint32_t> spinners{0};  // requests polling their own status word
 };
-// Requests of a combined batch poll their own status word (published behind a system-scope release
-// of the result, aes_gcm.hip gcm_one_batch_kernel) for up to kCombSpinUs while fewer than
-// kCombSpinners do, else sleep until the leader has seen the whole batch: a futex wake-up costs
-// ~10 µs, a 16-CPU share affords a few spinners but not 64.
-constexpr uint32_t kCombSpinners = 8;
-constexpr int kCombSpinUs = 200;
 struct KeyUse {
     hipStream_t s;
     hipEvent_t ev;
@@ -549,8 +556,21 @@ NEB_API int neb_engine_create(int device, uint32_t max_keys, neb_engine** out) {
               hipMalloc((void**)&e->d_keys, (size_t)max_keys * neb::kKeyRecBytes) == hipSuccess &&
               hipMemset(e->d_keys, 0, (size_t)max_keys * neb::kKeyRecBytes) == hipSuccess &&
               hipStreamSynchronize(nullptr) == hipSuccess;  // the null-stream memset, before any stream reads keys
+    // The per-packet pool's streams: high priority, which HIP gives a hardware queue of its own each.
+    // Streams of the default priority share the process's 4 queues, handed out in the order
+    // 1 2 3 4 4 3 2 1 (tools/native/queue_map.cpp under rocprofv3): after the null stream and the
+    // engine's stream the pool's 4 landed on 2 queues, and 4 threads' calls ran 2 kernels at a time
+    // (round 6 trace, profiles/r6/percall/). NEB_PKT_PRIO=0: default priority (A/B).
+    static const bool prio = [] {
+        const char* v = std::getenv("NEB_PKT_PRIO");
+        return !(v && v[0] == '0');
+    }();
+    int least = 0, greatest = 0;
+    if (prio) (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     for (PktSlot& sl : e->pkt.slot) {
-        ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess &&
+        ok = ok &&
+             (prio ? hipStreamCreateWithPriority(&sl.stream, hipStreamNonBlocking, greatest)
+                   : hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking)) == hipSuccess &&
              hipHostMalloc((void**)&sl.h, kStageMin, hipHostMallocDefault) == hipSuccess;
         if (ok) {
             sl.cap = kStageMin;
@@ -1114,17 +1134,24 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
     const size_t pay = align_up(ad_len, 16);
     if (!comb_on || c->alg != NEB_ALG_AESGCM || pay + std::max(in_len, pay_len + 16) > kCombSlot || pay + in_len > 2048)
         return one_packet_solo(c, open, ad, ad_len, in, in_len, pay_len, n, dst, st_out);
+    static const uint32_t max_inflight = [] {  // NEB_PKT_INFLIGHT: launches in flight (A/B), default 4
+        const char* v = std::getenv("NEB_PKT_INFLIGHT");
+        const int x = v ? std::atoi(v) : (int)kPktSlots;
+        return (uint32_t)std::min(std::max(x, 1), 64);
+    }();
     PktComb& cb = e->comb;
     std::unique_lock<std::mutex> lk(cb.mu);
     CombBatch*& ob = cb.open[0][open ? 1 : 0];
-    // Alone while fewer than kPktSlots launches are in flight and no batch is gathering (the pool
-    // then has a free slot: each alone call holds one, and only these take slots here).
-    if (cb.inflight < kPktSlots && !ob) {
+    // Alone while a launch and a pool slot are free and no batch is gathering (each alone call
+    // holds a pool slot; only these take slots here).
+    if (cb.inflight < max_inflight && cb.solo < kPktSlots && !ob) {
         cb.inflight++;
+        cb.solo++;
         lk.unlock();
         const int rc = one_packet_solo(c, open, ad, ad_len, in, in_len, pay_len, n, dst, st_out);
         lk.lock();
         cb.inflight--;
+        cb.solo--;
         lk.unlock();
         cb.launch_cv.notify_all();
         return rc;
@@ -1146,10 +1173,8 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
         cb.free_.pop_back();
         ob->n = 0;
         ob->launched = false;
-        {
-            std::lock_guard<std::mutex> g(ob->dmu);
-            ob->done = ob->failed = false;
-        }
+        ob->failed = false;
+        ob->done.store(0, std::memory_order_relaxed);
         ob->alg = c->alg;
         ob->open = open;
     }
@@ -1174,7 +1199,7 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
     // of it run, so its size follows the offered load; one thread spins per launch, the rest sleep
     // (64 threads spinning on a 16-CPU share starved the launches: p99 37 ms).
     if (i == 0) {
-        cb.launch_cv.wait(lk, [&] { return cb.inflight < kPktSlots; });
+        cb.launch_cv.wait(lk, [&] { return cb.inflight < max_inflight; });
         cb.inflight++;
         if (ob == b) ob = nullptr;
         b->launched = true;
@@ -1200,28 +1225,14 @@ static int one_packet(neb_cipher* c, int open, const uint8_t* ad, size_t ad_len,
         cb.inflight--;
         lk.unlock();
         cb.launch_cv.notify_all();
-        {
-            std::lock_guard<std::mutex> g(b->dmu);
-            b->failed = err != hipSuccess;
-            b->done = true;
-        }
-        b->done_cv.notify_all();
+        b->finish(err != hipSuccess);
     } else {
         lk.unlock();
     }
-    int32_t st = -1;
-    const bool spin = i && cb.spinners.fetch_add(1, std::memory_order_relaxed) < kCombSpinners;
-    const bool seen = spin && poll_status(b->status() + i, &st, kCombSpinUs);
-    if (i) cb.spinners.fetch_sub(1, std::memory_order_relaxed);
-    if (!seen) {
-        bool failed;
-        {
-            std::unique_lock<std::mutex> g(b->dmu);
-            b->done_cv.wait(g, [&] { return b->done; });
-            failed = b->failed;
-        }
-        st = failed ? -1 : __atomic_load_n(b->status() + i, __ATOMIC_ACQUIRE);
-    }
+    // (the owners sleep rather than poll their own status words: 8 spinners measured 317-336 k /
+    // 363-387 k calls/s at 16 / 32 threads against 338-341 k / 530-542 k sleeping)
+    const bool failed = b->wait();
+    const int32_t st = failed ? -1 : __atomic_load_n(b->status() + i, __ATOMIC_ACQUIRE);
     if (st != -1) copy_result(open, st, dst, slot + pay, pay_len);
     if (b->left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
         lk.lock();
