@@ -2149,6 +2149,58 @@ extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len
 
 // A combined launch of n per-packet requests (engine.cpp PktComb): descriptors, statuses and slots
 // (kCombSlot bytes each, the descriptors' offsets from `slots`) in pinned host memory.
+namespace neb {
+// A host-staged chunk's descriptors from pinned host memory into device memory (engine.cpp
+// batch_host), many loads in flight at once: the batch kernels then read them from HBM. Read in
+// place, each wave's descriptor loads waited behind the staging copies' PCIe traffic.
+__global__ __launch_bounds__(256) void copy_desc_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                        uint32_t nvec) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nvec; i += gridDim.x * 256u) dst[i] = src[i];
+}
+// A host-staged chunk's span between pinned host memory and HBM (engine.cpp batch_host,
+// NEB_PIPE_COPY): 16-byte vectors (both ends share their address mod 16), four in flight per lane,
+// bytes at the ragged ends.
+__global__ __launch_bounds__(256) void copy_span_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                        size_t head, size_t nvec, size_t bytes) {
+    const size_t tid = (size_t)blockIdx.x * 256u + threadIdx.x, nthr = (size_t)gridDim.x * 256u;
+    uint4* d = reinterpret_cast<uint4*>(dst + head);
+    const uint4* s = reinterpret_cast<const uint4*>(src + head);
+    size_t i = tid;
+    for (; i + 3u * nthr < nvec; i += 4u * nthr) {
+        const uint4 a = s[i], b = s[i + nthr], c = s[i + 2u * nthr], e = s[i + 3u * nthr];
+        d[i] = a;
+        d[i + nthr] = b;
+        d[i + 2u * nthr] = c;
+        d[i + 3u * nthr] = e;
+    }
+    for (; i < nvec; i += nthr) d[i] = s[i];
+    for (size_t j = tid; j < head; j += nthr) dst[j] = src[j];
+    for (size_t j = head + nvec * 16u + tid; j < bytes; j += nthr) dst[j] = src[j];
+}
+}  // namespace neb
+
+extern "C" hipError_t neb_copy_span(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return hipSuccess;
+    auto* d = static_cast<uint8_t*>(dst);
+    auto* src8 = static_cast<const uint8_t*>(src);
+    if (((uintptr_t)d & 15u) != ((uintptr_t)src8 & 15u)) return hipErrorInvalidValue;  // (the caller copies)
+    const size_t head = std::min(bytes, (size_t)((16u - ((uintptr_t)d & 15u)) & 15u));
+    const size_t nvec = (bytes - head) / 16u;
+    const uint32_t grid = (uint32_t)std::min<size_t>((nvec + 255u) / 256u, 2048u);
+    hipLaunchKernelGGL(neb::copy_span_kernel, dim3(std::max(grid, 1u)), dim3(256), 0, s, d, src8, head, nvec, bytes);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t neb_copy_desc(neb_desc* dst, const neb_desc* src, uint32_t n, hipStream_t s) {
+    static_assert(sizeof(neb_desc) % 16 == 0, "descriptors copy as 16-byte vectors");
+    const uint32_t nvec = n * (uint32_t)(sizeof(neb_desc) / 16);
+    if (!nvec) return hipSuccess;
+    const uint32_t grid = std::min((nvec + 255u) / 256u, 1024u);
+    hipLaunchKernelGGL(neb::copy_desc_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint4*>(dst),
+                       reinterpret_cast<const uint4*>(src), nvec);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t neb_gcm_one_batch(int open, const neb_desc* descs, int32_t* status, uint8_t* slots, uint32_t n,
                                         const uint32_t* d_keys, uint32_t max_keys, hipStream_t s) {
     if (n == 0 || n > neb::kOneBatchMax) return hipErrorInvalidValue;

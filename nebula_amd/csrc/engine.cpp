@@ -50,6 +50,8 @@ extern "C" hipError_t neb_gcm_batch_single(int open, const neb_desc* d_desc, uin
 extern "C" hipError_t neb_gcm_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in, uint32_t in_len,
                                   uint32_t len, uint64_t counter, uint8_t* out, int32_t* status, const uint32_t* d_keys,
                                   uint32_t max_keys, uint32_t key, hipStream_t s);
+extern "C" hipError_t neb_copy_span(void* dst, const void* src, size_t bytes, hipStream_t s);
+extern "C" hipError_t neb_copy_desc(neb_desc* dst, const neb_desc* src, uint32_t n, hipStream_t s);
 extern "C" hipError_t neb_gcm_one_batch(int open, const neb_desc* descs, int32_t* status, uint8_t* slots, uint32_t n,
                                         const uint32_t* d_keys, uint32_t max_keys, hipStream_t s);
 extern "C" hipError_t neb_chacha_one(int open, const uint8_t* aad, uint32_t aad_len, const uint8_t* in,
@@ -150,7 +152,8 @@ std::vector<uint32_t> pipe_plan(uint32_t n) {
 struct PipeSlot {
     uint8_t* d_buf = nullptr;
     size_t d_cap = 0;
-    neb_desc* h_desc = nullptr;  // pinned, mapped: the kernels read it in place
+    neb_desc* h_desc = nullptr;  // pinned: the chunk's rebased descriptors
+    neb_desc* d_desc = nullptr;  // their device copy, which the kernels read
     int32_t* h_status = nullptr; // pinned, mapped: the kernels write it in place
     int32_t* user_status = nullptr;
     uint32_t user_begin = 0, count = 0;
@@ -158,6 +161,7 @@ struct PipeSlot {
     hipEvent_t in_done = nullptr;   // the chunk's copies in are done (the kernel waits for it)
     hipEvent_t k_done = nullptr;    // its kernel is done (the copies back wait for it)
     hipEvent_t done = nullptr;      // its span and statuses are back (the slot is free)
+    bool back_pending = false;      // statuses taken at k_done; the copy back may still read d_buf
 };
 struct Pipe {
     hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
@@ -601,6 +605,7 @@ NEB_API int neb_engine_destroy(neb_engine* e) {
             if (ev) hipEventDestroy(ev);
         if (s.d_buf) hipFree(s.d_buf);
         if (s.h_desc) hipHostFree(s.h_desc);
+        if (s.d_desc) hipFree(s.d_desc);
         if (s.h_status) hipHostFree(s.h_status);
     }
     if (SchedSpace* sp = e->pipe.sched) {
@@ -1479,14 +1484,36 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         return batch_host_zero_copy(e, alg, open, desc, n, arena, arena_len, status, key_hint);
     }
     Pipe& P = e->pipe;
-    for (hipStream_t* st : {&P.h2d, &P.comp, &P.d2h})
-        if (!*st) HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+    // Each of the pipeline's streams on a hardware queue of its own: a stream with a CU mask gets
+    // one (all CUs here; tools/native/queue_map.cpp), where default streams share the process's 4
+    // and two of the pipeline's could land on one, so a chunk's kernel queued behind the previous
+    // chunk's copy back. NEB_PIPE_QUEUES=0: default streams, 2: low-priority streams (also a queue
+    // each) (A/B).
+    static const int own_queues = [] {
+        const char* v = std::getenv("NEB_PIPE_QUEUES");
+        return v ? std::atoi(v) : 1;
+    }();
+    for (hipStream_t* st : {&P.h2d, &P.comp, &P.d2h}) {
+        if (*st) continue;
+        if (own_queues == 2) {
+            int least = 0, greatest = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIP_TRY(hipStreamCreateWithPriority(st, hipStreamNonBlocking, least));
+        } else if (own_queues == 1) {
+            std::vector<uint32_t> mask(((uint32_t)e->cu_count + 31u) / 32u, 0u);
+            for (int c = 0; c < e->cu_count; c++) mask[c / 32] |= 1u << (c % 32);
+            HIP_TRY(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
+        } else {
+            HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        }
+    }
     if (!P.sched && !(P.sched = new (std::nothrow) SchedSpace)) return NEB_ERR_INVALID;
     for (auto& s : P.slot) {
         if (!s.done) {
             for (hipEvent_t* ev : {&s.in_done, &s.k_done, &s.done})
                 HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming));
             HIP_TRY(hipHostMalloc((void**)&s.h_desc, kPipeChunkPkts * sizeof(neb_desc), hipHostMallocDefault));
+            HIP_TRY(hipMalloc((void**)&s.d_desc, kPipeChunkPkts * sizeof(neb_desc)));
             HIP_TRY(hipHostMalloc((void**)&s.h_status, kPipeChunkPkts * sizeof(int32_t), hipHostMallocDefault));
         }
         s.count = 0;
@@ -1496,13 +1523,33 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         if (err != hipSuccess) return err;
         std::memcpy(s.user_status + s.user_begin, s.h_status, s.count * sizeof(int32_t));
         s.count = 0;
+        s.back_pending = false;
+        return hipSuccess;
+    };
+    // A slot taken for the next chunk: the host waits for the previous chunk's copy back (retire).
+    // The host's wait holds each copy-in until the copy back two chunks before it has ended (the
+    // blit copy's event completes with the next one), 284 µs per call idle on the copy-in stream
+    // (profiles/r6/host/final_*_trace.csv, tools/r6/copy_overlap.py). NEB_PIPE_GPU_WAIT=1 waits
+    // only for the kernel on the host and for the copy back on the device (hipStreamWaitEvent
+    // before the copy-in): 27.9-29.3 against 31.7-33.4 GiB/s (ab_gpu_wait.jsonl), so not default.
+    static const bool gpu_wait = [] {
+        const char* v = std::getenv("NEB_PIPE_GPU_WAIT");
+        return v && v[0] == '1';
+    }();
+    auto reuse = [&](PipeSlot& s) -> hipError_t {
+        if (!gpu_wait) return retire(s);
+        hipError_t err = hipEventSynchronize(s.k_done);
+        if (err != hipSuccess) return err;
+        std::memcpy(s.user_status + s.user_begin, s.h_status, s.count * sizeof(int32_t));
+        s.count = 0;
+        s.back_pending = true;
         return hipSuccess;
     };
     // any failure below leaves work queued on the three streams: drain them before returning
     auto fail = [&](const char* where, hipError_t err) {
         set_error(where, err);
         for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
-        for (auto& s : P.slot) s.count = 0;
+        for (auto& s : P.slot) s.count = 0, s.back_pending = false;
         return NEB_ERR_HIP;
     };
 #define PIPE_TRY(x)                                     \
@@ -1511,14 +1558,15 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         if (err_ != hipSuccess) return fail(#x, err_);  \
     } while (0)
     const std::vector<uint32_t> plan = pipe_plan(n);
+    bool arena_mapped = false;
     uint32_t begin = 0;
     for (uint32_t k = 0; k < plan.size(); begin += plan[k], k++) {
         PipeSlot& s = P.slot[k % kPipeSlots];
-        if (s.count) PIPE_TRY(retire(s));  // the slot's previous chunk is back: its buffers are free
+        if (s.count) PIPE_TRY(reuse(s));  // the slot's previous chunk's kernel is done
         const uint32_t cnt = plan[k];
         if (!check_upto(begin + cnt)) {  // (only ever the first chunk: the rest were checked after it)
             for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
-            for (auto& o : P.slot) o.count = 0;
+            for (auto& o : P.slot) o.count = 0, o.back_pending = false;
             return NEB_ERR_INVALID;
         }
         uint64_t lo = ~0ULL, hi = 0;  // every sum below stays within arena_len (checked above)
@@ -1531,12 +1579,18 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         lo &= ~(uint64_t)15;
         // A chunk copies its whole span back, so spans of chunks in flight must not overlap (the
         // descriptors need not be in arena order): retire any other slot whose span intersects.
-        for (auto& o : P.slot)
-            if (&o != &s && o.count && o.lo < hi && lo < o.hi) PIPE_TRY(retire(o));
+        // (A slot whose statuses are taken but whose copy back may still run: the copy-in waits for it.)
+        for (auto& o : P.slot) {
+            if (&o == &s || !(o.lo < hi && lo < o.hi)) continue;
+            if (o.count) PIPE_TRY(retire(o));
+            else if (o.back_pending) PIPE_TRY(hipStreamWaitEvent(P.h2d, o.done, 0));
+        }
         s.lo = lo;
         s.hi = hi;
         const size_t span = (size_t)(hi - lo);
         if (span > s.d_cap) {  // (retired: nothing in flight uses it)
+            if (s.back_pending) PIPE_TRY(hipEventSynchronize(s.done));
+            s.back_pending = false;
             if (s.d_buf) { hipFree(s.d_buf); s.d_buf = nullptr; s.d_cap = 0; }
             size_t cap = align_up(span, 1 << 20);
             PIPE_TRY(hipMalloc((void**)&s.d_buf, cap));
@@ -1557,23 +1611,51 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         s.user_status = status;
         s.user_begin = begin;
         s.count = cnt;
-        // the kernels read the chunk's descriptors and write its statuses in the slot's pinned, mapped
-        // buffers themselves (48 + 4 B per packet over PCIe): two fewer copies per chunk, whose
-        // per-copy latency left the copy-in stream idle between chunks (a 15-µs copy after a ≈ 40-µs
-        // gap, profiles/r6/host/)
-        PIPE_TRY(hipMemcpyAsync(s.d_buf, arena + lo, span, hipMemcpyHostToDevice, P.h2d));
+        // The kernels write the chunk's statuses in the slot's pinned, mapped buffer themselves (4 B
+        // per packet of posted writes). Its descriptors go to the device on the kernels' stream,
+        // ahead of them: read over PCIe in place they waited behind the copies' 90 GB/s, and the
+        // kernels ran 250-478 µs per 16 Ki-packet chunk instead of ≈ 25 (profiles/r6/host/); on the
+        // copy-in stream the small copy's latency left that stream idle between chunks.
+        static const int desc_dev = [] {  // NEB_PIPE_DESC=0: read in place, 2: hipMemcpyAsync (A/B)
+            const char* v = std::getenv("NEB_PIPE_DESC");
+            return v ? std::atoi(v) : 1;
+        }();
+        // NEB_PIPE_COPY (A/B): bit 0 copies back with a kernel of ours instead of hipMemcpyAsync, bit
+        // 1 copies in with one. Only for an arena the device can address (pinned and mapped at both
+        // ends: a kernel touching pageable memory faults the GPU) at the same address mod 16 as its
+        // device buffer; anything else takes hipMemcpyAsync.
+        static const int copy_k = [] {
+            const char* v = std::getenv("NEB_PIPE_COPY");
+            return v ? std::atoi(v) : 0;
+        }();
+        if (k == 0) arena_mapped = copy_k && arena_len && host_mapped(arena) && host_mapped(arena + arena_len - 1);
+        auto copy = [&](void* dst, const void* src, hipMemcpyKind kind, hipStream_t st) {
+            if (arena_mapped && (copy_k & (kind == hipMemcpyDeviceToHost ? 1 : 2)) &&
+                neb_copy_span(dst, src, span, st) == hipSuccess)
+                return hipSuccess;
+            (void)hipGetLastError();
+            return hipMemcpyAsync(dst, src, span, kind, st);
+        };
+        if (s.back_pending) PIPE_TRY(hipStreamWaitEvent(P.h2d, s.done, 0));
+        s.back_pending = false;
+        PIPE_TRY(copy(s.d_buf, arena + lo, hipMemcpyHostToDevice, P.h2d));
         PIPE_TRY(hipEventRecord(s.in_done, P.h2d));
         if (NEB_PIPE_MODE == 2 && k == 0 && !check_upto(n)) {  // (mode 2's kernels write the arena)
             for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
-            for (auto& o : P.slot) o.count = 0;
+            for (auto& o : P.slot) o.count = 0, o.back_pending = false;
             return NEB_ERR_INVALID;
         }
         PIPE_TRY(hipStreamWaitEvent(P.comp, s.in_done, 0));
-        PIPE_TRY(launch_batch(e, alg, open, s.h_desc, cnt, s.d_buf, s.h_status, key_hint, P.comp, nullptr, P.sched));
+        if (desc_dev == 2)
+            PIPE_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, cnt * sizeof(neb_desc), hipMemcpyHostToDevice, P.comp));
+        else if (desc_dev)
+            PIPE_TRY(neb_copy_desc(s.d_desc, s.h_desc, cnt, P.comp));
+        PIPE_TRY(launch_batch(e, alg, open, desc_dev ? s.d_desc : s.h_desc, cnt, s.d_buf, s.h_status, key_hint, P.comp,
+                              nullptr, P.sched));
         PIPE_TRY(hipEventRecord(s.k_done, P.comp));
         if (k == 0 && !check_upto(n)) {  // the rest of the batch, while chunk 0 is copied in and run
             for (hipStream_t st : {P.h2d, P.comp, P.d2h}) (void)hipStreamSynchronize(st);
-            for (auto& o : P.slot) o.count = 0;
+            for (auto& o : P.slot) o.count = 0, o.back_pending = false;
             return NEB_ERR_INVALID;
         }
         if (NEB_PIPE_MODE == 2) {
@@ -1581,12 +1663,15 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         } else {
             hipStream_t back = NEB_PIPE_MODE == 1 ? P.comp : P.d2h;
             if (NEB_PIPE_MODE == 0) PIPE_TRY(hipStreamWaitEvent(P.d2h, s.k_done, 0));
-            PIPE_TRY(hipMemcpyAsync(arena + lo, s.d_buf, span, hipMemcpyDeviceToHost, back));
+            PIPE_TRY(copy(arena + lo, s.d_buf, hipMemcpyDeviceToHost, back));
             PIPE_TRY(hipEventRecord(s.done, back));
         }
     }
-    for (auto& s : P.slot)
+    for (auto& s : P.slot) {
         if (s.count) PIPE_TRY(retire(s));
+        if (s.back_pending) PIPE_TRY(hipEventSynchronize(s.done));  // every copy back is in the arena
+        s.back_pending = false;
+    }
 #undef PIPE_TRY
     return NEB_OK;
 }
