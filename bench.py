@@ -507,7 +507,9 @@ def main():
     alg_name = "AES-256-GCM" if b.alg == L.ALG_AESGCM else "ChaCha20-Poly1305"
     # the kernel the dispatch-bound events were bound to, as the library names it
     kern_tag = seal_kernel if bound else "event brackets around the whole seal call"
-    pmc = pmc_config(f"C{cfg + 1}" + (f"/{args.shard_of}" if cfg == 4 and args.shard_of else ""))
+    # (shards: "C5/8" by tunnel, "C5/8r" by packet range)
+    pmc = pmc_config(f"C{cfg + 1}" + (f"/{args.shard_of}{'r' if args.shard_by == 'range' else ''}"
+                                      if cfg == 4 and args.shard_of else ""))
     lens = b.desc["len"].astype(np.int64)
     out = {
         "metric": "GiB/s device-resident AES-256-GCM seal+open, 1300 B pkts, 64 Ki batch"

@@ -20,10 +20,16 @@ __global__ void sched_hist_kernel(const neb_desc* __restrict__ desc, uint32_t n,
         sched_hist_round<SUB>(desc, n, max_keys, lpp, ws, i0, blockIdx.x);
 }
 
+// Workgroup size of the allocation pass (1024 threads, 4x fewer workgroups and so 4x fewer returning
+// atomics on the bucket counters: C5 shard 400 against 408 GiB/s, profiles/r6/ab/alloc_threads.jsonl)
+#ifndef NEB_SCHED_ALLOC_THREADS
+#define NEB_SCHED_ALLOC_THREADS 256
+#endif
+constexpr uint32_t kAllocThreadsSched = NEB_SCHED_ALLOC_THREADS;
 template <uint32_t SUB>
-__global__ __launch_bounds__(kAllocThreads) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
+__global__ __launch_bounds__(kAllocThreadsSched) void sched_alloc_kernel(uint32_t max_keys, SchedWs ws) {
     __shared__ SchedAllocLds sl;
-    sched_alloc_block<SUB>(max_keys, ws, blockIdx.x, sl);
+    sched_alloc_block<SUB, kAllocThreadsSched>(max_keys, ws, blockIdx.x, sl);
 }
 
 __global__ void sched_scatter_kernel(const neb_desc* __restrict__ desc, uint32_t n, const uint32_t* dn, SchedWs ws) {
@@ -192,7 +198,7 @@ extern "C" hipError_t neb_sched_build(const neb_desc* d_desc, uint32_t n, const 
     const uint32_t nb = neb::sched_nbins(max_keys);
     const uint32_t tpb = 256;
     const uint32_t gp = (n + tpb - 1) / tpb < 4096u ? (n + tpb - 1) / tpb : 4096u;
-    const dim3 ga((nb + neb::kAllocThreads - 1) / neb::kAllocThreads), ta(neb::kAllocThreads);
+    const dim3 ga((nb + neb::kAllocThreadsSched - 1) / neb::kAllocThreadsSched), ta(neb::kAllocThreadsSched);
     // NEB_KNOB_SUB_BINS_FROM (per batch): the A/B of the threshold, and the tests' coverage of both
     // counting layouts
     const int64_t from = neb::knob(NEB_KNOB_SUB_BINS_FROM);

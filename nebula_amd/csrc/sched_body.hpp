@@ -118,11 +118,12 @@ __device__ __forceinline__ bool sched_leftover_group(uint32_t i, uint32_t key, c
     return mine;
 }
 
-template <uint32_t SUB>
+// THREADS: the workgroup's size (the receive plan's launches run it in their 256-thread workgroups)
+template <uint32_t SUB, uint32_t THREADS = kAllocThreads>
 __device__ __forceinline__ void sched_alloc_block(uint32_t max_keys, const SchedWs& ws, uint32_t blk,
                                                   SchedAllocLds& sl) {
     const uint32_t K1 = max_keys + 1u;
-    const uint32_t t = blk * kAllocThreads + threadIdx.x, key = t / kSizeClasses, cls = t % kSizeClasses;
+    const uint32_t t = blk * THREADS + threadIdx.x, key = t / kSizeClasses, cls = t % kSizeClasses;
     const uint32_t lane = threadIdx.x & 63u, grp = lane & ~(kSizeClasses - 1u);
     const bool valid = key < K1;
     const uint32_t bin = cls * K1 + key;
@@ -150,7 +151,17 @@ __device__ __forceinline__ void sched_alloc_block(uint32_t max_keys, const Sched
     __syncthreads();
     // reservations inside the workgroup (LDS atomics), then the workgroup's totals globally
     uint32_t o_pk = 0, o_full = 0, o_last = 0, o_left = 0;
-    if (c) o_pk = atomicAdd(&sl.cnt[0], c);
+    {  // the packets' offset: a wave scan, then one LDS add per wave (not one per bin)
+        uint32_t inc = c;
+#pragma unroll
+        for (uint32_t d = 1; d < 64u; d *= 2u) {
+            const uint32_t v = (uint32_t)__shfl_up((int)inc, d);
+            if (lane >= d) inc += v;
+        }
+        uint32_t wbase = 0;
+        if (lane == 63u && inc) wbase = atomicAdd(&sl.cnt[0], inc);
+        o_pk = (uint32_t)__shfl((int)wbase, 63) + inc - c;
+    }
     if (nfc > 1u) o_full = atomicAdd(&sl.cnt[1u + bfull], nfc - 1u);
     if (nfc) o_last = atomicAdd(&sl.cnt[1u + blast], 1u);
     if (has_left) o_left = atomicAdd(&sl.cnt[1u + lb], 1u);
