@@ -1527,11 +1527,12 @@ static int batch_host(neb_engine* e, int alg, int open, const neb_desc* desc, ui
         return hipSuccess;
     };
     // A slot taken for the next chunk: the host waits for the previous chunk's copy back (retire).
-    // The host's wait holds each copy-in until the copy back two chunks before it has ended (the
-    // blit copy's event completes with the next one), 284 µs per call idle on the copy-in stream
-    // (profiles/r6/host/final_*_trace.csv, tools/r6/copy_overlap.py). NEB_PIPE_GPU_WAIT=1 waits
-    // only for the kernel on the host and for the copy back on the device (hipStreamWaitEvent
-    // before the copy-in): 27.9-29.3 against 31.7-33.4 GiB/s (ab_gpu_wait.jsonl), so not default.
+    // In the trace each copy-in then starts as the copy back two chunks before it ends, 284 µs per
+    // call idle on the copy-in stream (profiles/r6/host/final_*_trace.csv, tools/r6/
+    // copy_overlap.py). Two ways of removing that wait measured no better: NEB_PIPE_GPU_WAIT=1
+    // waits only for the kernel on the host and for the copy back on the device (hipStreamWaitEvent
+    // before the copy-in), 27.9-29.3 against 31.7-33.4 GiB/s (ab_gpu_wait.jsonl); an empty kernel
+    // after each copy back with the event after it, 30.5-32.3 against 31.3-32.9 (ab_mark.jsonl).
     static const bool gpu_wait = [] {
         const char* v = std::getenv("NEB_PIPE_GPU_WAIT");
         return v && v[0] == '1';
