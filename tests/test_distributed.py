@@ -64,6 +64,31 @@ def test_two_rank_shards_cover_batch_exactly(tmp_path, oracle_mod):
     assert float(metas[0][3]) == float(full.n)                   # sum of shard sizes
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tunnel_shards_partition_batch(oracle_mod, world):
+    """bench.py's default C5 sharding (`--shard-by key`, workload.shard_by_key): rank r takes the
+    tunnels with key_id mod world == r. Every packet lands in exactly one shard, every tunnel's
+    packets in one shard and in batch order, and sealing each shard with the oracle gives the
+    bytes sealing the whole batch gives at those packets' slots (rebased offsets)."""
+    from nebula_amd import workload as W
+
+    full = W.make_batch(1, 1500, 37, sizes=(90, 576, 1300), ratio=(7, 4, 1), name="tunnels")
+    ref = full.arena.copy()
+    assert (oracle_mod.batch(1, 0, full.keys, full.desc, ref) == 0).all()
+    ref_slots = ref.reshape(full.n, full.stride)
+    seen = np.zeros(full.n, np.int64)
+    for r in range(world):
+        part = W.shard_by_key(full, r, world)
+        idx = np.flatnonzero(full.desc["key_id"] % world == r)
+        assert part.n == len(idx) and (part.desc["key_id"] % world == r).all()
+        assert np.array_equal(part.desc["counter"], full.desc["counter"][idx])  # batch order kept
+        seen[idx] += 1
+        got = part.arena.copy()
+        assert (oracle_mod.batch(1, 0, part.keys, part.desc, got) == 0).all()
+        assert np.array_equal(got.reshape(part.n, part.stride), ref_slots[idx])
+    assert (seen == 1).all()
+
+
 @pytest.mark.parametrize("n,world", [(65536, 8), (1 << 20, 8), (7, 4), (1, 2)])
 def test_shard_ranges_tile(n, world):
     from nebula_amd.shard import shard_range

@@ -448,12 +448,20 @@ def test_concurrent_calls_combined_with_forgeries(engine, oracle_mod):
             errors.append(ex)
 
     ths = [threading.Thread(target=worker, args=(t,)) for t in range(24)]
+    before = engine.stats()
     try:
         for th in ths:
             th.start()
         for th in ths:
             th.join()
         assert not errors, errors[:3]
+        after = engine.stats()
+        # every call counted once, alone or combined (neb_engine_stats / neb_engine_pkt_combined)
+        assert after["pkt_calls"] - before["pkt_calls"] >= 24 * 120 * 2
+        combined = after["pkt_combined_calls"] - before["pkt_combined_calls"]
+        launches = after["pkt_combined_launches"] - before["pkt_combined_launches"]
+        assert combined >= launches >= 0 and combined <= 32 * launches
+        print(f"combined {combined} calls in {launches} launches")
     finally:
         for cs, _ in states:
             cs.destroy()
