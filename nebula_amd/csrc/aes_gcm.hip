@@ -1625,6 +1625,9 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     uint4 ch_next = make_uint4(0, 0, 0, 0);
     if (c < nch) ch_next = chunk_at(c);
 #if NEB_CHUNK_STEAL
+#ifndef NEB_STEAL_MIN_PER_WG
+#define NEB_STEAL_MIN_PER_WG 32u
+#endif
     // The batch's last 1/8 of chunks (the shortest) are not owned: a wave whose workgroup has run
     // out of its own draws them from its XCD's cursor (blockIdx mod 8, one word per XCD, 128 B
     // apart), so workgroups that drew lighter chunks take more of them. C5's workgroups carried
@@ -1632,7 +1635,7 @@ __global__ __launch_bounds__(kChunkThreads, kChunkWpe) void gcm_chunk_kernel(Gcm
     // alternating (profiles/r5/ab_balance): C3 547-548 -> 553-555 GiB/s, C5 512-514 -> 518; the
     // last 1/4 or 1/16 the same within noise. Every partition has a drawer (at least 8 workgroups)
     // and every wave's first chunk is still owned (at least 32 chunks per workgroup).
-    const uint32_t ndyn = (gridDim.x >= 8u && nch >= 32u * gridDim.x) ? nch / NEB_CHUNK_STEAL : 0u;
+    const uint32_t ndyn = (gridDim.x >= 8u && nch >= NEB_STEAL_MIN_PER_WG * gridDim.x) ? nch / NEB_CHUNK_STEAL : 0u;
     const uint32_t nstat = nch - ndyn;
     auto claim = [&]() -> uint32_t {
         uint32_t k = 0;
